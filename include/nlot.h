@@ -1,0 +1,232 @@
+/*
+ * nlot.h — C ABI of the MI355X-native batched trajectory optimiser (libnlot.so).
+ *
+ * This is the drop-in boundary for the reference's NLP constraint-evaluation hot path
+ * (SURVEY.md §8b).  Everything is plain C: POD structs, caller-owned pointers, int return codes,
+ * an explicit hipStream_t passed as void*, no exceptions and no global mutable state on the
+ * compute entry points (each call uses only its arguments and the caller's workspace).
+ *
+ * Replaced reference interfaces (file:line under /root/reference):
+ *   nlot_sdf_mlp_eval        <- gen/nn_sdf.cpp:57-60  nn_sdf        (value)
+ *                               gen/nn_sdf.cpp:67-70  jac_nn_sdf    (gradient)
+ *                               gen/nn_sdf.cpp:79-83  adj1_nn_sdf   (lambda * gradient)
+ *                               gen/nn_sdf.cpp:91-104 jac_adj1_nn_sdf (lambda * Hessian)
+ *                           batched over P points on the device instead of one 1x2 point per call.
+ *   nlot_solve_batch         <- src/nlotrajectories/core/runner.py:44-153 RunBenchmark.run
+ *                               (NLP of runner.py:46-108 solved by CasADi Opti + IPOPT,
+ *                               runner.py:113-133) for B independent start/goal instances.
+ *   nn_sdf / jac_nn_sdf / adj1_nn_sdf / jac_adj1_nn_sdf and their _n_in/_n_out/_sparsity_*
+ *                            <- gen/nn_sdf.cpp:36-104, same CasADi external signatures, served by
+ *                               the model bound with nlot_casadi_bind (host buffers, like CasADi).
+ */
+#ifndef NLOT_H
+#define NLOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLOT_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------------------------- */
+#define NLOT_OK 0
+#define NLOT_ERR_INVALID -1    /* bad argument / unsupported configuration */
+#define NLOT_ERR_HIP -2        /* HIP runtime error */
+#define NLOT_ERR_WORKSPACE -3  /* workspace too small */
+
+/* ---- per-problem solve status (output array `status`) ----------------------------------- */
+#define NLOT_SOLVED 0             /* IPOPT "Solve_Succeeded" analogue: E_0 <= tol + abs. tols */
+#define NLOT_MAXITER 1            /* max_iter reached (IPOPT Maximum_Iterations_Exceeded)     */
+#define NLOT_LS_FAILED 2          /* alpha < alpha_min: IPOPT would enter restoration         */
+#define NLOT_NUMERIC 3            /* non-finite values / inertia correction failed            */
+
+/* ---- dynamics (core/dynamics.py:7-13, DYNAMICS_CLASS_MAP 151-158) ------------------------ */
+enum NlotDynamics {
+    NLOT_POINT_1ST = 0,   /* PointMass1stOrder  dynamics.py:33-41  nx=4 nu=2 */
+    NLOT_POINT_2ND = 1,   /* PointMass2ndOrder  dynamics.py:44-56  nx=4 nu=2 */
+    NLOT_UNICYCLE = 2,    /* Unicycle           dynamics.py:59-73  nx=3 nu=2 */
+    NLOT_UNICYCLE_2ND = 3,/* Unicycle2ndOrder   dynamics.py:76-96  nx=5 nu=2 */
+    NLOT_ACKERMANN = 4,   /* Ackermann          dynamics.py:99-118 nx=4 nu=2 */
+    NLOT_ACKERMANN_2ND = 5/* Ackermann2ndOrder  dynamics.py:121-148 nx=7 nu=2 (vector order as-is) */
+};
+
+/* ---- robot geometry (core/geometry.py) --------------------------------------------------- */
+enum NlotShape {
+    NLOT_SHAPE_DOT = 0,     /* DotGeometry geometry.py:59-70: sdf(x,y) >= 0, slack ignored      */
+    NLOT_SHAPE_POLYGON = 1  /* PolygonGeometry geometry.py:73-117 (rectangle 125-135, triangle
+                               138-144): soft-min over corners + slack, or per-corner >= 0       */
+};
+
+/* ---- analytic obstacles (core/sdf/casadi.py) ---------------------------------------------- */
+enum NlotObstacleType {
+    NLOT_OBS_CIRCLE = 0,  /* CircleObstacle.approximated_sdf casadi.py:33-41 */
+    NLOT_OBS_SQUARE = 1   /* SquareObstacle.approximated_sdf casadi.py:69-118 */
+};
+
+enum NlotSdfKind {
+    NLOT_SDF_ANALYTIC = 0, /* MultiObstacle.approximated_sdf casadi.py:385-386 (soft_min union) */
+    NLOT_SDF_MLP = 1       /* NNObstacle.approximated_sdf l4casadi.py:241-257 (learned)         */
+};
+
+#define NLOT_MAX_OBS 16
+#define NLOT_MAX_BODY 8
+#define NLOT_MAX_NU 4
+
+typedef struct NlotObstacle {
+    int32_t type;      /* NlotObstacleType */
+    int32_t pad_;
+    double cx, cy;     /* center */
+    double size;       /* circle: radius; square: side length */
+    double margin;
+} NlotObstacle;
+
+/* One NLP of runner.py:44-108 (all B instances share it; start/goal differ per instance). */
+typedef struct NlotProblem {
+    int32_t dynamics;        /* NlotDynamics */
+    int32_t shape;           /* NlotShape */
+    int32_t nx, nu;          /* must match the dynamics */
+    int32_t n_body;          /* polygon corner count (rectangle 4, triangle 3) */
+    int32_t N;               /* knots - 1 (solver.N) */
+    double body[NLOT_MAX_BODY][2]; /* corners in body frame, geometry.py:125-144 order */
+    double wheelbase;        /* Ackermann L */
+    double dt;
+    int32_t use_slack;       /* runner.py:66-69 */
+    int32_t use_smooth;      /* runner.py:91-96 */
+    double slack_penalty;    /* rho */
+    double smooth_weight;    /* w */
+    int32_t enforce_heading; /* runner.py:51-56 */
+    int32_t sdf_kind;        /* NlotSdfKind */
+    double umin[NLOT_MAX_NU], umax[NLOT_MAX_NU]; /* runner.py:101-103 */
+    double softmin_alpha;    /* utils.py:18 alpha = 10 */
+    double path_eps;         /* runner.py:81 epsilon = 1e-8 */
+    int32_t n_obs;
+    int32_t pad_;
+    NlotObstacle obs[NLOT_MAX_OBS];
+} NlotProblem;
+
+/* IPOPT options (runner.py:113-125 + IPOPT defaults).  See DESIGN.md §4 for the restatement. */
+typedef struct NlotSolverOptions {
+    double tol;                  /* 1e-4 (runner.py:118) */
+    int32_t max_iter;            /* 1000 (runner.py:117) */
+    int32_t mu_strategy;         /* 0 = monotone (Fiacco-McCormick); see DESIGN.md */
+    double mu_init;              /* 0.1 */
+    double barrier_tol_factor;   /* kappa_eps (IPOPT default 10) */
+    double dual_inf_tol;         /* 1 */
+    double constr_viol_tol;      /* 1e-4 */
+    double compl_inf_tol;        /* 1e-4 */
+    double constr_mult_init_max; /* 1e3 */
+    double bound_push;           /* 1e-2 */
+    double bound_frac;           /* 1e-2 */
+    int32_t max_soc;             /* second-order corrections per iteration (IPOPT default 4) */
+    int32_t pad_;
+} NlotSolverOptions;
+
+/* Learned SDF: an l4casadi-wrappable torch model, flattened.
+ *   FourierMLP (core/nn_architectures.py:30-72):  h0 = scale * cos(p @ A + b0)         (in_kind 1)
+ *   l4c.naive.MultiLayerPerceptron:              h0 = relu(p @ A + b0)                 (in_kind 0)
+ *   then n_hidden x  h_{l+1} = relu(W_l h_l + b_l);   f = w_out . h + b_out.
+ * All weights fp32 (the reference's l4casadi path evaluates the TorchScript graph in fp32,
+ * gen/nn_sdf.cpp casts the CasADi doubles to float).  Host OR device pointers depending on the
+ * consumer (nlot_mlp_create copies host arrays to the device). */
+#define NLOT_MLP_IN_LINEAR_RELU 0
+#define NLOT_MLP_IN_FOURIER 1
+
+typedef struct NlotMlpDesc {
+    int32_t in_kind;       /* NLOT_MLP_IN_* */
+    int32_t hidden;        /* H (multiple of 32, <= 256) */
+    int32_t n_hidden;      /* hidden HxH layers (>= 0) */
+    int32_t act;           /* 0 = ReLU (the only activation in round 1) */
+    float fourier_scale;   /* FourierFeatureLayer.scale */
+    float b_out;
+    const float* A;        /* [2][H]  (in, out) */
+    const float* b0;       /* [H] */
+    const float* W;        /* [n_hidden][H][H]  (out, in) = nn.Linear.weight */
+    const float* b;        /* [n_hidden][H] */
+    const float* w_out;    /* [H] */
+} NlotMlpDesc;
+
+typedef struct NlotMlp NlotMlp; /* opaque device-resident weights */
+
+/* ---- version / errors --------------------------------------------------------------------- */
+int32_t nlot_abi_version(void);
+/* Last error message of the calling thread (thread-local; never NULL). */
+const char* nlot_last_error(void);
+/* Fill `opt` with the defaults documented above. */
+void nlot_default_options(NlotSolverOptions* opt);
+
+/* ---- learned-SDF weights ------------------------------------------------------------------- */
+/* Copies the host arrays of `desc` to device memory; returns NULL on error (see nlot_last_error). */
+NlotMlp* nlot_mlp_create(const NlotMlpDesc* desc);
+void nlot_mlp_destroy(NlotMlp* mlp);
+
+/* Batched SDF-MLP evaluation on the device (the nn_sdf family, gen/nn_sdf.cpp:57-104).
+ *   pts  [P][2] fp32 device, row-major.   val [P] (required).
+ *   grad [P][2] or NULL: df/dp.             lam [P] or NULL (NULL = 1): adjoint seed.
+ *   hess [P][2][2] or NULL: lam * d2f/dp2 (jac_adj1).  When lam != NULL, grad is lam * df/dp (adj1).
+ * `stream` is a hipStream_t (NULL = default stream). Asynchronous. */
+int32_t nlot_sdf_mlp_eval(const NlotMlp* mlp, const float* pts, int64_t P, float* val, float* grad,
+                          const float* lam, float* hess, void* stream);
+
+/* ---- batched trajectory optimisation ------------------------------------------------------ */
+/* Bytes of device workspace nlot_solve_batch needs for B instances. */
+size_t nlot_solve_workspace_size(const NlotProblem* prob, int64_t B);
+
+/* Solve B independent instances of `prob` (start x0[b], goal xg[b]) on the device.
+ *   x0, xg    [B][nx] fp64 device
+ *   X_init    [B][N+1][nx] fp64 device, or NULL = LinearInitializer (trajectory_initialization.py:54-55)
+ *   X         [B][N+1][nx] fp64 device (out)   U [B][N][nu] fp64 (out)   S [B][N+1] fp64 or NULL
+ *   cost      [B] fp64 (out: objective value, runner.py:80-98 / run_benchmark.py:166)
+ *   status    [B] int32 (out: NLOT_SOLVED ...)   iters [B] int32 (out)
+ *   mlp       required iff prob->sdf_kind == NLOT_SDF_MLP
+ *   workspace >= nlot_solve_workspace_size(prob, B) bytes of device memory.
+ * Returns when all instances finished (the host drives the iteration loop on `stream`). */
+int32_t nlot_solve_batch(const NlotProblem* prob, const NlotSolverOptions* opt, const NlotMlp* mlp,
+                         const double* x0, const double* xg, const double* X_init, double* X,
+                         double* U, double* S, double* cost, int32_t* status, int32_t* iters,
+                         int64_t B, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-solve counters of the last nlot_solve_batch on this thread (host side, for benchmarking). */
+typedef struct NlotSolveStats {
+    int32_t iterations;        /* lock-step iterations run */
+    int32_t ls_rounds;         /* line-search rounds launched */
+    int64_t mlp_points_full;   /* points evaluated with value+grad+hess */
+    int64_t mlp_points_value;  /* points evaluated value-only (trial points) */
+    double mlp_full_ms;        /* summed device time of the full MLP launches (hipEvents) */
+    double mlp_value_ms;       /* summed device time of the value-only MLP launches */
+    int32_t mlp_full_launches;
+    int32_t mlp_value_launches;
+} NlotSolveStats;
+/* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
+void nlot_set_timing(int32_t enabled);
+void nlot_last_stats(NlotSolveStats* out);
+
+/* ---- CasADi external compatibility shim (gen/nn_sdf.cpp:36-104) ----------------------------
+ * A CasADi user can `casadi.external("nn_sdf", "libnlot.so")` after binding a model.  These are
+ * host functions on double buffers owned by CasADi, one 1x2 point per call, exactly like the
+ * generated file; they run the MLP on the GPU synchronously.  Bind with nlot_casadi_bind (the
+ * reference's static global L4CasADi object, gen/nn_sdf.cpp:3). */
+typedef double casadi_real_t;
+typedef long long int casadi_int_t;
+int32_t nlot_casadi_bind(const NlotMlp* mlp);
+casadi_int_t nn_sdf_n_in(void);
+casadi_int_t nn_sdf_n_out(void);
+const casadi_int_t* nn_sdf_sparsity_in(casadi_int_t i);
+const casadi_int_t* nn_sdf_sparsity_out(casadi_int_t i);
+int nn_sdf(const casadi_real_t** arg, casadi_real_t** res, casadi_int_t* iw, casadi_real_t* w, int mem);
+casadi_int_t jac_nn_sdf_n_in(void);
+casadi_int_t jac_nn_sdf_n_out(void);
+int jac_nn_sdf(const casadi_real_t** arg, casadi_real_t** res, casadi_int_t* iw, casadi_real_t* w, int mem);
+casadi_int_t adj1_nn_sdf_n_in(void);
+casadi_int_t adj1_nn_sdf_n_out(void);
+int adj1_nn_sdf(const casadi_real_t** arg, casadi_real_t** res, casadi_int_t* iw, casadi_real_t* w, int mem);
+casadi_int_t jac_adj1_nn_sdf_n_in(void);
+casadi_int_t jac_adj1_nn_sdf_n_out(void);
+int jac_adj1_nn_sdf(const casadi_real_t** arg, casadi_real_t** res, casadi_int_t* iw, casadi_real_t* w, int mem);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLOT_H */

@@ -1,0 +1,73 @@
+"""ctypes mirrors of the plain-C structs in include/nlot.h (layout must match the header)."""
+import ctypes as C
+
+NLOT_OK = 0
+NLOT_SOLVED, NLOT_MAXITER, NLOT_LS_FAILED, NLOT_NUMERIC = 0, 1, 2, 3
+STATUS_NAMES = {0: "solved", 1: "max_iter", 2: "line_search_failed", 3: "numeric"}
+
+# NlotDynamics (core/dynamics.py:7-13)
+DYNAMICS = {"point_1st": 0, "point_2nd": 1, "unicycle": 2, "unicycle_2nd": 3, "ackermann": 4,
+            "ackermann_2nd": 5}
+STATE_DIM = {"point_1st": 4, "point_2nd": 4, "unicycle": 3, "unicycle_2nd": 5, "ackermann": 4,
+             "ackermann_2nd": 7}
+CONTROL_DIM = {k: 2 for k in DYNAMICS}
+SHAPE_DOT, SHAPE_POLYGON = 0, 1
+OBS_CIRCLE, OBS_SQUARE = 0, 1
+SDF_ANALYTIC, SDF_MLP = 0, 1
+MLP_IN_LINEAR_RELU, MLP_IN_FOURIER = 0, 1
+MAX_OBS, MAX_BODY, MAX_NU = 16, 8, 4
+
+
+class NlotObstacle(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pad_", C.c_int32), ("cx", C.c_double), ("cy", C.c_double),
+                ("size", C.c_double), ("margin", C.c_double)]
+
+
+class NlotProblem(C.Structure):
+    _fields_ = [
+        ("dynamics", C.c_int32), ("shape", C.c_int32), ("nx", C.c_int32), ("nu", C.c_int32),
+        ("n_body", C.c_int32), ("N", C.c_int32), ("body", (C.c_double * 2) * MAX_BODY),
+        ("wheelbase", C.c_double), ("dt", C.c_double), ("use_slack", C.c_int32),
+        ("use_smooth", C.c_int32), ("slack_penalty", C.c_double), ("smooth_weight", C.c_double),
+        ("enforce_heading", C.c_int32), ("sdf_kind", C.c_int32), ("umin", C.c_double * MAX_NU),
+        ("umax", C.c_double * MAX_NU), ("softmin_alpha", C.c_double), ("path_eps", C.c_double),
+        ("n_obs", C.c_int32), ("pad_", C.c_int32), ("obs", NlotObstacle * MAX_OBS),
+    ]
+
+
+class NlotSolverOptions(C.Structure):
+    _fields_ = [
+        ("tol", C.c_double), ("max_iter", C.c_int32), ("mu_strategy", C.c_int32),
+        ("mu_init", C.c_double), ("barrier_tol_factor", C.c_double), ("dual_inf_tol", C.c_double),
+        ("constr_viol_tol", C.c_double), ("compl_inf_tol", C.c_double),
+        ("constr_mult_init_max", C.c_double), ("bound_push", C.c_double), ("bound_frac", C.c_double),
+        ("max_soc", C.c_int32), ("pad_", C.c_int32),
+    ]
+
+
+class NlotMlpDesc(C.Structure):
+    _fields_ = [
+        ("in_kind", C.c_int32), ("hidden", C.c_int32), ("n_hidden", C.c_int32), ("act", C.c_int32),
+        ("fourier_scale", C.c_float), ("b_out", C.c_float), ("A", C.POINTER(C.c_float)),
+        ("b0", C.POINTER(C.c_float)), ("W", C.POINTER(C.c_float)), ("b", C.POINTER(C.c_float)),
+        ("w_out", C.POINTER(C.c_float)),
+    ]
+
+
+class NlotSolveStats(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int32), ("ls_rounds", C.c_int32), ("mlp_points_full", C.c_int64),
+        ("mlp_points_value", C.c_int64), ("mlp_full_ms", C.c_double), ("mlp_value_ms", C.c_double),
+        ("mlp_full_launches", C.c_int32), ("mlp_value_launches", C.c_int32),
+    ]
+
+
+def default_options(**kw) -> NlotSolverOptions:
+    """IPOPT settings of runner.py:113-125 plus IPOPT defaults."""
+    o = NlotSolverOptions(tol=1e-4, max_iter=1000, mu_strategy=0, mu_init=0.1,
+                          barrier_tol_factor=10.0, dual_inf_tol=1.0, constr_viol_tol=1e-4,
+                          compl_inf_tol=1e-4, constr_mult_init_max=1e3, bound_push=1e-2,
+                          bound_frac=1e-2, max_soc=0)
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o

@@ -1,0 +1,208 @@
+"""Learned-SDF models and their flattened weights.
+
+`FourierMLP` / `SIREN` restate the reference architectures (core/nn_architectures.py:8-100) as
+torch modules so users can train or load them; `MultiLayerPerceptron` restates l4casadi's naive
+MLP used for `model.type: mlp` (scripts/run_benchmark.py:64-65; external l4casadi, unpinned:
+Linear(in,H) -> act -> hidden_layers x [Linear(H,H) -> act] -> Linear(H,out)).
+
+`MlpWeights` is the flat fp32 form the HIP kernel consumes (NlotMlpDesc in include/nlot.h).
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _abi
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+ARTEFACT_NPZ = os.path.join(DATA_DIR, "nn_sdf_artefact.npz")
+
+
+class FourierFeatureLayer(nn.Module):
+    """cos(x @ W + b) * scale, core/nn_architectures.py:30-38."""
+
+    def __init__(self, in_features, out_features, scale=1.0):
+        super().__init__()
+        self.scale = scale
+        self.weights = nn.Parameter(torch.randn(in_features, out_features) * scale)
+        self.bias = nn.Parameter(torch.zeros(out_features))
+
+    def forward(self, x):
+        return torch.cos(x @ self.weights + self.bias) * self.scale
+
+
+class FourierMLP(nn.Module):
+    """core/nn_architectures.py:42-72 (num_layers-2 hidden Linear+act layers)."""
+
+    _ACTS = {"ReLU": F.relu, "tanh": torch.tanh, "sigmoid": torch.sigmoid, "leaky_relu": F.leaky_relu}
+
+    def __init__(self, input_dim, hidden_dim, output_dim, num_layers=3, scale=1.0, activation_function="ReLU"):
+        super().__init__()
+        if activation_function not in self._ACTS:
+            raise ValueError(f"Unsupported activation function: {activation_function}")
+        self.activation_name = activation_function
+        self.activation_function = self._ACTS[activation_function]
+        self.fourier = FourierFeatureLayer(input_dim, hidden_dim, scale)
+        self.layers = nn.ModuleList([nn.Linear(hidden_dim, hidden_dim) for _ in range(num_layers - 2)])
+        self.output_layer = nn.Linear(hidden_dim, output_dim)
+
+    def forward(self, x):
+        x = self.fourier(x)
+        for layer in self.layers:
+            x = self.activation_function(layer(x))
+        return self.output_layer(x)
+
+
+class MultiLayerPerceptron(nn.Module):
+    """l4casadi.naive.MultiLayerPerceptron(in, hidden, out, hidden_layers, activation) restated."""
+
+    def __init__(self, in_features, hidden_features, out_features, hidden_layers, activation="ReLU"):
+        super().__init__()
+        if activation not in (None, "ReLU"):
+            raise ValueError("round-1 kernels support ReLU MLPs (see DESIGN.md §7)")
+        self.input_layer = nn.Linear(in_features, hidden_features)
+        self.hidden_layers = nn.ModuleList([nn.Linear(hidden_features, hidden_features) for _ in range(hidden_layers)])
+        self.output_layer = nn.Linear(hidden_features, out_features)
+        self.activation = activation
+
+    def forward(self, x):
+        x = F.relu(self.input_layer(x))
+        for layer in self.hidden_layers:
+            x = F.relu(layer(x))
+        return self.output_layer(x)
+
+
+class SineLayer(nn.Module):
+    """core/nn_architectures.py:8-26."""
+
+    def __init__(self, in_features, out_features, bias=True, is_first=False, omega_0=30):
+        super().__init__()
+        self.omega_0, self.is_first = omega_0, is_first
+        self.linear = nn.Linear(in_features, out_features, bias=bias)
+        with torch.no_grad():
+            if is_first:
+                self.linear.weight.uniform_(-1 / in_features, 1 / in_features)
+            else:
+                b = math.sqrt(6 / in_features) / omega_0
+                self.linear.weight.uniform_(-b, b)
+
+    def forward(self, x):
+        return torch.sin(self.omega_0 * self.linear(x))
+
+
+class SIREN(nn.Module):
+    """core/nn_architectures.py:75-100 (kernel support: DESIGN.md §7, next)."""
+
+    def __init__(self, input_dim, hidden_dim, output_dim, num_layers=3, omega_0=30):
+        super().__init__()
+        self.layers = nn.ModuleList([SineLayer(input_dim, hidden_dim, is_first=True, omega_0=omega_0)])
+        for _ in range(num_layers - 2):
+            self.layers.append(SineLayer(hidden_dim, hidden_dim, omega_0=omega_0))
+        self.output_layer = nn.Linear(hidden_dim, output_dim)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return self.output_layer(x)
+
+
+@dataclass
+class MlpWeights:
+    """Flat fp32 weights: h0 = phi(p @ A + b0); n_hidden x relu(W h + b); f = w_out . h + b_out."""
+
+    in_kind: int
+    hidden: int
+    n_hidden: int
+    fourier_scale: float
+    b_out: float
+    arrays: Dict[str, np.ndarray]
+
+    @property
+    def flops_per_point_fwd(self) -> int:
+        H = self.hidden
+        return 2 * (2 * H + self.n_hidden * H * H + H)
+
+    @property
+    def flops_per_point_fwd_grad(self) -> int:
+        return 2 * self.flops_per_point_fwd
+
+    def to(self, dtype=np.float32):
+        return self
+
+    def torch_module(self) -> nn.Module:
+        """Equivalent torch module (fp32), for reference evaluation in tests / the numpy path."""
+        H = self.hidden
+        if self.in_kind == _abi.MLP_IN_FOURIER:
+            m = FourierMLP(2, H, 1, num_layers=self.n_hidden + 2, scale=self.fourier_scale)
+            sd = {"fourier.weights": self.arrays["A"], "fourier.bias": self.arrays["b0"]}
+            for l in range(self.n_hidden):
+                sd[f"layers.{l}.weight"] = self.arrays["W"][l]
+                sd[f"layers.{l}.bias"] = self.arrays["b"][l]
+        else:
+            m = MultiLayerPerceptron(2, H, 1, self.n_hidden)
+            sd = {"input_layer.weight": self.arrays["A"].T, "input_layer.bias": self.arrays["b0"]}
+            for l in range(self.n_hidden):
+                sd[f"hidden_layers.{l}.weight"] = self.arrays["W"][l]
+                sd[f"hidden_layers.{l}.bias"] = self.arrays["b"][l]
+        sd["output_layer.weight"] = self.arrays["w_out"][None, :]
+        sd["output_layer.bias"] = np.array([self.b_out], np.float32)
+        m.load_state_dict({k: torch.as_tensor(np.ascontiguousarray(v)) for k, v in sd.items()})
+        return m.eval()
+
+    @staticmethod
+    def from_module(model: nn.Module) -> "MlpWeights":
+        """Flatten a FourierMLP / MultiLayerPerceptron (ReLU) into kernel form."""
+        g = lambda t: t.detach().cpu().float().numpy().copy()
+        if isinstance(model, FourierMLP) or hasattr(model, "fourier"):
+            if getattr(model, "activation_name", "ReLU") != "ReLU":
+                raise ValueError("round-1 kernels support ReLU hidden layers")
+            H = model.fourier.weights.shape[1]
+            Ws = [g(l.weight) for l in model.layers]
+            bs = [g(l.bias) for l in model.layers]
+            arrays = dict(A=g(model.fourier.weights), b0=g(model.fourier.bias),
+                          W=np.stack(Ws) if Ws else np.zeros((0, H, H), np.float32),
+                          b=np.stack(bs) if bs else np.zeros((0, H), np.float32),
+                          w_out=g(model.output_layer.weight)[0])
+            return MlpWeights(_abi.MLP_IN_FOURIER, H, len(Ws), float(model.fourier.scale),
+                              float(g(model.output_layer.bias)[0]), arrays)
+        if hasattr(model, "input_layer") and hasattr(model, "hidden_layers"):
+            H = model.input_layer.weight.shape[0]
+            Ws = [g(l.weight) for l in model.hidden_layers]
+            bs = [g(l.bias) for l in model.hidden_layers]
+            arrays = dict(A=g(model.input_layer.weight).T.copy(), b0=g(model.input_layer.bias),
+                          W=np.stack(Ws) if Ws else np.zeros((0, H, H), np.float32),
+                          b=np.stack(bs) if bs else np.zeros((0, H), np.float32),
+                          w_out=g(model.output_layer.weight)[0])
+            return MlpWeights(_abi.MLP_IN_LINEAR_RELU, H, len(Ws), 1.0, float(g(model.output_layer.bias)[0]), arrays)
+        raise TypeError(f"unsupported model type {type(model).__name__} (DESIGN.md §7)")
+
+    @staticmethod
+    def artefact() -> "MlpWeights":
+        """The reference artefact _l4c_generated/nn_sdf.pt (FourierMLP 2-128-128-1, scale 10),
+        extracted as raw data by tests/golden/make_golden.py."""
+        z = np.load(ARTEFACT_NPZ, allow_pickle=False)
+        H = z["A"].shape[1]
+        arrays = dict(A=z["A"].astype(np.float32), b0=z["b0"].astype(np.float32),
+                      W=z["W1"].astype(np.float32)[None], b=z["b1"].astype(np.float32)[None],
+                      w_out=z["w2"].astype(np.float32)[0])
+        return MlpWeights(_abi.MLP_IN_FOURIER, H, 1, float(z["scale"]), float(z["b2"][0]), arrays)
+
+    @staticmethod
+    def random_relu_mlp(hidden=256, n_hidden=3, seed=0) -> "MlpWeights":
+        """Seeded kaiming-uniform ReLU MLP (the stress config; l4casadi.py:69-74)."""
+        gen = torch.Generator().manual_seed(seed)
+        m = MultiLayerPerceptron(2, hidden, 1, n_hidden)
+        with torch.no_grad():
+            for mod in m.modules():
+                if isinstance(mod, nn.Linear):
+                    bound = math.sqrt(6.0 / mod.weight.shape[1])
+                    mod.weight.uniform_(-bound, bound, generator=gen)
+                    mod.bias.zero_()
+        return MlpWeights.from_module(m)

@@ -1,0 +1,174 @@
+"""Problem description: the NLP of RunBenchmark (runner.py:9-108) as a plain value object.
+
+`Problem` carries exactly the constructor arguments of the reference's `RunBenchmark`
+(src/nlotrajectories/core/runner.py:10-26) that shape the NLP, in the reference's vocabulary
+(dynamics, geometry, slack, smooth, control bounds, obstacles), and flattens them into the C struct
+`NlotProblem` of include/nlot.h.  Start and goal states are per-instance inputs of the batched
+solve, so they are not part of the problem.
+
+`BENCHMARKS` restates the six shipped scenarios (src/nlotrajectories/benchmarks/*.yaml) so the GPU
+box, which has no reference tree, can build them; `config.py` parses the YAML files themselves.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+from typing import List, Optional, Sequence, Tuple
+
+from . import _abi
+
+Obstacle = dict  # {"type": "circle"|"square", "center": (x, y), "radius"|"size": r, "margin": m}
+
+
+def rectangle_body(length: float, width: float):
+    """RectangleGeometry corner order (geometry.py:125-135)."""
+    lb, wb = length / 2, width / 2
+    return [(-lb, -wb), (-lb, wb), (lb, wb), (lb, -wb)]
+
+
+def triangle_body(length: float, width: float):
+    """TriangleGeometry corner order (geometry.py:138-144)."""
+    return [(length / 2, 0.0), (-length / 2, width / 2), (-length / 2, -width / 2)]
+
+
+@dataclass
+class Problem:
+    dynamics: str = "unicycle_2nd"
+    shape: str = "rectangle"            # dot | rectangle | triangle
+    length: float = 0.2
+    width: float = 0.1
+    wheelbase: float = 1.0              # Ackermann2ndOrder default (dynamics.py:122)
+    N: int = 50
+    dt: float = 0.1
+    use_slack: bool = True
+    slack_penalty: float = 50.0
+    use_smooth: bool = False
+    smooth_weight: float = 0.2
+    enforce_heading: bool = False
+    control_bounds: Sequence[Tuple[float, float]] = ((-2.0, 2.0), (-2.0, 2.0))
+    obstacles: List[Obstacle] = field(default_factory=list)
+    sdf: str = "analytic"               # analytic | mlp
+    softmin_alpha: float = 10.0         # utils.py:18
+    path_eps: float = 1e-8              # runner.py:81
+
+    @property
+    def nx(self) -> int:
+        return _abi.STATE_DIM[self.dynamics]
+
+    @property
+    def nu(self) -> int:
+        return _abi.CONTROL_DIM[self.dynamics]
+
+    @property
+    def body(self):
+        if self.shape == "rectangle":
+            return rectangle_body(self.length, self.width)
+        if self.shape == "triangle":
+            return triangle_body(self.length, self.width)
+        return [(0.0, 0.0)]
+
+    def ineq_per_knot(self) -> int:
+        if self.shape == "dot":
+            return 1
+        return 1 if self.use_slack else len(self.body)
+
+    def with_(self, **kw) -> "Problem":
+        return replace(self, **kw)
+
+    def to_c(self) -> _abi.NlotProblem:
+        if self.dynamics not in _abi.DYNAMICS:
+            raise ValueError(f"Unknown dynamics type: {self.dynamics}")
+        if len(self.control_bounds) != self.nu:
+            raise ValueError("control_bounds must have one (min, max) pair per control")
+        if self.sdf == "analytic" and not self.obstacles:
+            raise ValueError("analytic SDF needs at least one obstacle")
+        if len(self.obstacles) > _abi.MAX_OBS:
+            raise ValueError(f"at most {_abi.MAX_OBS} obstacles")
+        p = _abi.NlotProblem()
+        p.dynamics = _abi.DYNAMICS[self.dynamics]
+        p.shape = _abi.SHAPE_DOT if self.shape == "dot" else _abi.SHAPE_POLYGON
+        p.nx, p.nu = self.nx, self.nu
+        body = self.body
+        p.n_body = len(body)
+        for i, (bx, by) in enumerate(body):
+            p.body[i][0], p.body[i][1] = bx, by
+        p.N = int(self.N)
+        p.wheelbase = float(self.wheelbase)
+        p.dt = float(self.dt)
+        p.use_slack = int(bool(self.use_slack))
+        p.use_smooth = int(bool(self.use_smooth))
+        p.slack_penalty = float(self.slack_penalty)
+        p.smooth_weight = float(self.smooth_weight)
+        p.enforce_heading = int(bool(self.enforce_heading))
+        p.sdf_kind = _abi.SDF_MLP if self.sdf == "mlp" else _abi.SDF_ANALYTIC
+        for i, (lo, hi) in enumerate(self.control_bounds):
+            p.umin[i], p.umax[i] = float(lo), float(hi)
+        p.softmin_alpha = float(self.softmin_alpha)
+        p.path_eps = float(self.path_eps)
+        p.n_obs = len(self.obstacles)
+        for i, o in enumerate(self.obstacles):
+            t = o["type"]
+            if t == "circle":
+                p.obs[i].type = _abi.OBS_CIRCLE
+                p.obs[i].size = float(o["radius"])
+            elif t == "square":
+                p.obs[i].type = _abi.OBS_SQUARE
+                p.obs[i].size = float(o["size"])
+            else:
+                raise ValueError(f"obstacle type {t!r} is reached only through the learned SDF "
+                                 "(round-1 analytic kernels: circle, square)")
+            p.obs[i].cx, p.obs[i].cy = map(float, o["center"])
+            p.obs[i].margin = float(o.get("margin", 0.0))
+        return p
+
+
+def _circle(c, r, m=0.0):
+    return {"type": "circle", "center": tuple(c), "radius": r, "margin": m}
+
+
+def _square(c, s, m=0.0):
+    return {"type": "square", "center": tuple(c), "size": s, "margin": m}
+
+
+# Restated scenario parameters (benchmarks/benchmark_*.yaml).  start/goal are the YAML's.
+BENCHMARKS = {
+    # benchmark_1_dot_circle.yaml:1-45
+    "b1": dict(problem=Problem(dynamics="point_2nd", shape="dot", N=40, dt=0.1, use_slack=True,
+                               slack_penalty=50, use_smooth=False, smooth_weight=0.2,
+                               enforce_heading=False, control_bounds=((-1, 1), (-1, 1)),
+                               obstacles=[_circle((0.5, 0.5), 0.2, 0.05)]),
+               start=[0.0, 0.0, 0.0, 0.0], goal=[1.0, 1.0, 0.0, 0.0]),
+    # benchmark_2_unicycle_circle.yaml:1-50
+    "b2": dict(problem=Problem(dynamics="unicycle_2nd", shape="rectangle", length=0.2, width=0.1,
+                               N=50, dt=0.1, use_slack=True, slack_penalty=50, use_smooth=False,
+                               smooth_weight=0.2, enforce_heading=False,
+                               control_bounds=((-2, 2), (-2, 2)),
+                               obstacles=[_circle((0.5, 0.5), 0.2, 0.05)]),
+               start=[0.0, 0.0, 0.785, 0.0, 0.0], goal=[1.0, 1.0, 0.785, 0.0, 0.0]),
+    # benchmark_3_unicycle_convex.yaml:1-54 (mode l4casadi; analytic scene kept for reference)
+    "b3": dict(problem=Problem(dynamics="unicycle_2nd", shape="rectangle", length=0.2, width=0.08,
+                               N=40, dt=0.1, use_slack=True, slack_penalty=10, use_smooth=False,
+                               smooth_weight=0.2, enforce_heading=False,
+                               control_bounds=((-1, 1), (-1, 1)),
+                               obstacles=[_circle((0.6, 0.6), 0.15), _square((0.8, 0.2), 0.35),
+                                          _square((0.0, 0.3), 0.1)]),
+               start=[0.0, 0.0, 0.785, 0.0, 0.0], goal=[1.0, 1.0, 0.785, 0.0, 0.0]),
+    # benchmark_5_ackermann_circle.yaml:1-60
+    "b5": dict(problem=Problem(dynamics="ackermann_2nd", shape="rectangle", length=0.1, width=0.1,
+                               wheelbase=0.1, N=30, dt=0.1, use_slack=True, slack_penalty=1,
+                               use_smooth=False, smooth_weight=0.2, enforce_heading=False,
+                               control_bounds=((-1, 1), (-2, 2)),
+                               obstacles=[_circle((0.5, 0.5), 0.2, 0.01), _square((1.2, 0.37), 0.1, 0.01),
+                                          _square((1.1, 0.7), 0.2, 0.01), _square((0.2, 0.9), 0.1, 0.01)]),
+               start=[0, 0, 0, 0.0, 0.0, 0.0, 0.0], goal=[1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0]),
+}
+
+# The metric configuration (BASELINE.json metric): benchmark_3's body,
+# bounds and slack penalty, N = 50 knots, learned SDF = the artefact FourierMLP weights.
+METRIC_PROBLEM = Problem(dynamics="unicycle_2nd", shape="rectangle", length=0.2, width=0.08, N=50,
+                         dt=0.1, use_slack=True, slack_penalty=10, use_smooth=False,
+                         enforce_heading=False, control_bounds=((-1, 1), (-1, 1)), sdf="mlp")
+
+
+def heading(start_xy, goal_xy) -> float:
+    return math.atan2(goal_xy[1] - start_xy[1], goal_xy[0] - start_xy[0])

@@ -1,0 +1,1732 @@
+/*
+ * nlot_oracle.c — CPU restatement of the reference's NLP hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library (as the
+ * checker / the timed CPU baseline).  The product (libnlot.so, nlotrajectories_amd/) never links
+ * or calls it.
+ *
+ * What is restated (file:line under /root/reference):
+ *   - NLP definition of RunBenchmark.run                      src/nlotrajectories/core/runner.py:44-108
+ *       decision variables X, U, slack                         runner.py:46-47, 66-69
+ *       start / terminal equalities (enforce_heading)          runner.py:50-56
+ *       explicit-Euler dynamics defects                        runner.py:59-64
+ *       per-knot SDF constraints                               runner.py:73-77 -> geometry.py:63-67,107-117
+ *       cost: path length + slack + smooth penalties           runner.py:80-98
+ *       control bounds                                          runner.py:101-103
+ *   - dynamics f(x,u), 6 models                                core/dynamics.py:33-148
+ *   - footprint corners + soft-min                              core/geometry.py:78-83,125-144; core/utils.py:18-33
+ *   - analytic SDFs (circle, smooth square, union)              core/sdf/casadi.py:33-41,69-118,385-386
+ *   - learned SDF (FourierMLP / naive MLP, fp32 like libtorch)  core/nn_architectures.py:30-72; gen/nn_sdf.cpp:57-104
+ *   - IPOPT (external dependency, CasADi 3.7.0's bundled IPOPT, poetry.lock:90-91) is restated from its
+ *     published algorithm (Waechter & Biegler 2006): primal-dual barrier method, monotone mu update,
+ *     fraction-to-boundary rule, inertia-corrected Newton step, filter line search.  Deviations are
+ *     listed in DESIGN.md §4 (no SOC / restoration / adaptive mu oracle).
+ *
+ * Derivatives use a small second-order forward-mode "jet" (value, gradient, Hessian), so this file is
+ * an independent derivation from the hand-written derivatives of the HIP kernels.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/nlot.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ============================================================================================ */
+/* Second-order jets                                                                           */
+/* ============================================================================================ */
+#define JD 10
+#define JH (JD * (JD + 1) / 2)
+typedef struct {
+    int n;
+    double v;
+    double g[JD];
+    double h[JH]; /* lower triangle, row i col j<=i at i*(i+1)/2+j */
+} jet;
+
+static inline int hix(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+static jet jconst(int n, double c) {
+    jet r;
+    memset(&r, 0, sizeof r);
+    r.n = n;
+    r.v = c;
+    return r;
+}
+static jet jvar(int n, double v, int i) {
+    jet r = jconst(n, v);
+    r.g[i] = 1.0;
+    return r;
+}
+static jet jadd(jet a, jet b) {
+    jet r = a;
+    r.v += b.v;
+    for (int i = 0; i < a.n; ++i) r.g[i] += b.g[i];
+    for (int i = 0; i < a.n * (a.n + 1) / 2; ++i) r.h[i] += b.h[i];
+    return r;
+}
+static jet jscale(jet a, double c) {
+    jet r = a;
+    r.v *= c;
+    for (int i = 0; i < a.n; ++i) r.g[i] *= c;
+    for (int i = 0; i < a.n * (a.n + 1) / 2; ++i) r.h[i] *= c;
+    return r;
+}
+static jet jsub(jet a, jet b) { return jadd(a, jscale(b, -1.0)); }
+static jet jaddc(jet a, double c) {
+    a.v += c;
+    return a;
+}
+static jet jmul(jet a, jet b) {
+    jet r = jconst(a.n, a.v * b.v);
+    for (int i = 0; i < a.n; ++i) r.g[i] = a.g[i] * b.v + a.v * b.g[i];
+    for (int i = 0; i < a.n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            int q = hix(i, j);
+            r.h[q] = a.h[q] * b.v + a.v * b.h[q] + a.g[i] * b.g[j] + a.g[j] * b.g[i];
+        }
+    return r;
+}
+/* r = f(a) with f(a.v)=f0, f'=f1, f''=f2 */
+static jet junary(jet a, double f0, double f1, double f2) {
+    jet r = jconst(a.n, f0);
+    for (int i = 0; i < a.n; ++i) r.g[i] = f1 * a.g[i];
+    for (int i = 0; i < a.n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            int q = hix(i, j);
+            r.h[q] = f1 * a.h[q] + f2 * a.g[i] * a.g[j];
+        }
+    return r;
+}
+static jet jsin(jet a) { return junary(a, sin(a.v), cos(a.v), -sin(a.v)); }
+static jet jcos(jet a) { return junary(a, cos(a.v), -sin(a.v), -cos(a.v)); }
+static jet jtan(jet a) {
+    double t = tan(a.v), s2 = 1.0 + t * t;
+    return junary(a, t, s2, 2.0 * t * s2);
+}
+static jet jexp(jet a) {
+    double e = exp(a.v);
+    return junary(a, e, e, e);
+}
+static jet jlog(jet a) { return junary(a, log(a.v), 1.0 / a.v, -1.0 / (a.v * a.v)); }
+static jet jsqrt(jet a) {
+    double s = sqrt(a.v);
+    return junary(a, s, 0.5 / s, -0.25 / (s * a.v));
+}
+static jet jrecip(jet a) { return junary(a, 1.0 / a.v, -1.0 / (a.v * a.v), 2.0 / (a.v * a.v * a.v)); }
+static jet jdiv(jet a, jet b) { return jmul(a, jrecip(b)); }
+static jet jsq(jet a) { return jmul(a, a); }
+/* phi(cx(z), cy(z)) given phi's value / gradient / Hessian in (cx, cy) */
+static jet jcompose2(double f, const double g[2], const double H[3] /*xx,xy,yy*/, jet cx, jet cy) {
+    jet r = jconst(cx.n, f);
+    for (int i = 0; i < cx.n; ++i) r.g[i] = g[0] * cx.g[i] + g[1] * cy.g[i];
+    for (int i = 0; i < cx.n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            int q = hix(i, j);
+            r.h[q] = g[0] * cx.h[q] + g[1] * cy.h[q] + H[0] * cx.g[i] * cx.g[j] +
+                     H[1] * (cx.g[i] * cy.g[j] + cy.g[i] * cx.g[j]) + H[2] * cy.g[i] * cy.g[j];
+        }
+    return r;
+}
+
+/* ============================================================================================ */
+/* Learned SDF — fp32 like the reference's libtorch evaluation (gen/nn_sdf.cpp:57-104)           */
+/* ============================================================================================ */
+/* out: [0]=f [1..2]=lam*grad [3..5]=lam*hess (xx,xy,yy).  lam scales the adjoint seed
+ * (adj1 / jac_adj1, gen/nn_sdf.cpp:79-104); lam = 1 gives jac_nn_sdf.  want = 0: value only. */
+void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
+    enum { HM = 256, LM = 8 };
+    const int H = m->hidden;
+    float z0[HM], h[HM], hn[HM];
+    unsigned char mask[LM + 1][HM];
+    for (int k = 0; k < H; ++k) {
+        /* p @ A + b0  (torch.mm then add, graph ___torch_mangle_0.py) */
+        float z = fmaf(py, m->A[H + k], px * m->A[k]) + m->b0[k];
+        z0[k] = z;
+        if (m->in_kind == NLOT_MLP_IN_FOURIER) {
+            h[k] = cosf(z) * m->fourier_scale; /* nn_architectures.py:38 */
+            mask[0][k] = 1;
+        } else {
+            mask[0][k] = z > 0.f;
+            h[k] = z > 0.f ? z : 0.f;
+        }
+    }
+    for (int l = 0; l < m->n_hidden; ++l) {
+        const float* W = m->W + (size_t)l * H * H;
+        const float* b = m->b + (size_t)l * H;
+        for (int j = 0; j < H; ++j) {
+            float a = 0.f;
+            for (int k = 0; k < H; ++k) a = fmaf(W[(size_t)j * H + k], h[k], a);
+            a += b[j];
+            mask[l + 1][j] = a > 0.f;
+            hn[j] = a > 0.f ? a : 0.f;
+        }
+        memcpy(h, hn, sizeof(float) * H);
+    }
+    float f = 0.f;
+    for (int j = 0; j < H; ++j) f = fmaf(m->w_out[j], h[j], f);
+    out[0] = f + m->b_out;
+    out[1] = out[2] = out[3] = out[4] = out[5] = 0.f;
+    if (!want) return;
+    /* reverse sweep: delta = d f / d h_l */
+    float d[HM], dn[HM];
+    for (int j = 0; j < H; ++j) d[j] = lam * m->w_out[j];
+    for (int l = m->n_hidden - 1; l >= 0; --l) {
+        const float* W = m->W + (size_t)l * H * H;
+        for (int j = 0; j < H; ++j) d[j] = mask[l + 1][j] ? d[j] : 0.f;
+        for (int k = 0; k < H; ++k) dn[k] = 0.f;
+        for (int j = 0; j < H; ++j)
+            for (int k = 0; k < H; ++k) dn[k] = fmaf(W[(size_t)j * H + k], d[j], dn[k]);
+        memcpy(d, dn, sizeof(float) * H);
+    }
+    float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+    for (int k = 0; k < H; ++k) {
+        float ax = m->A[k], ay = m->A[H + k], dz, c2;
+        if (m->in_kind == NLOT_MLP_IN_FOURIER) {
+            dz = d[k] * (-m->fourier_scale * sinf(z0[k]));
+            c2 = d[k] * (-m->fourier_scale * cosf(z0[k]));
+        } else {
+            dz = mask[0][k] ? d[k] : 0.f;
+            c2 = 0.f; /* ReLU input layer: piecewise linear, Hessian 0 a.e. */
+        }
+        gx = fmaf(ax, dz, gx);
+        gy = fmaf(ay, dz, gy);
+        hxx = fmaf(ax * ax, c2, hxx);
+        hxy = fmaf(ax * ay, c2, hxy);
+        hyy = fmaf(ay * ay, c2, hyy);
+    }
+    out[1] = gx;
+    out[2] = gy;
+    out[3] = hxx;
+    out[4] = hxy;
+    out[5] = hyy;
+}
+
+/* Batched form of the nn_sdf family (same argument meaning as nlot_sdf_mlp_eval, host buffers). */
+void oracle_mlp_eval(const NlotMlpDesc* m, const float* pts, long P, float* val, float* grad,
+                     const float* lam, float* hess) {
+    int want = (grad != NULL) || (hess != NULL);
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < P; ++i) {
+        float o[6];
+        oracle_mlp_point(m, pts[2 * i], pts[2 * i + 1], lam ? lam[i] : 1.f, want, o);
+        val[i] = o[0];
+        if (grad) {
+            grad[2 * i] = o[1];
+            grad[2 * i + 1] = o[2];
+        }
+        if (hess) {
+            hess[4 * i + 0] = o[3];
+            hess[4 * i + 1] = o[4];
+            hess[4 * i + 2] = o[4];
+            hess[4 * i + 3] = o[5];
+        }
+    }
+}
+
+/* ============================================================================================ */
+/* Analytic SDFs (core/sdf/casadi.py)                                                           */
+/* ============================================================================================ */
+static jet sdf_circle(const NlotObstacle* o, jet x, jet y) { /* casadi.py:33-41 */
+    jet dx = jaddc(x, -o->cx), dy = jaddc(y, -o->cy);
+    return jaddc(jsqrt(jadd(jsq(dx), jsq(dy))), -(o->size + o->margin));
+}
+static jet soft_abs6(jet v) { return jsqrt(jaddc(jsq(v), 1e-6)); }          /* casadi.py:81-85 */
+static jet smax6(jet a, jet b) {                                              /* casadi.py:95-99 */
+    return jscale(jadd(jadd(a, b), jsqrt(jaddc(jsq(jsub(a, b)), 1e-6))), 0.5);
+}
+static jet smin6(jet a, jet b) {                                              /* casadi.py:101-105 */
+    return jscale(jsub(jadd(a, b), jsqrt(jaddc(jsq(jsub(a, b)), 1e-6))), 0.5);
+}
+static jet sdf_square(const NlotObstacle* o, jet x, jet y) { /* casadi.py:69-118 */
+    double half = o->size / 2 + o->margin;
+    jet dx = soft_abs6(jaddc(x, -o->cx)), dy = soft_abs6(jaddc(y, -o->cy));
+    jet d_x = jaddc(dx, -half), d_y = jaddc(dy, -half);
+    jet zero = jconst(x.n, 0.0);
+    jet dxo = smax6(d_x, zero), dyo = smax6(d_y, zero);
+    jet outside = jsqrt(jadd(jsq(dxo), jsq(dyo)));
+    jet inside = smin6(smax6(d_x, d_y), zero);
+    return jadd(outside, inside);
+}
+/* soft_min, core/utils.py:18-33 (no max-shift, exactly as written) */
+static jet soft_min_j(const jet* a, int n, double alpha) {
+    jet s = jconst(a[0].n, 0.0);
+    for (int i = 0; i < n; ++i) s = jadd(s, jexp(jscale(a[i], -alpha)));
+    return jscale(jlog(s), -1.0 / alpha);
+}
+/* MultiObstacle.approximated_sdf casadi.py:385-386 — soft_min even for one obstacle */
+static jet sdf_analytic(const NlotProblem* p, jet x, jet y) {
+    jet v[NLOT_MAX_OBS];
+    for (int i = 0; i < p->n_obs; ++i)
+        v[i] = p->obs[i].type == NLOT_OBS_CIRCLE ? sdf_circle(&p->obs[i], x, y) : sdf_square(&p->obs[i], x, y);
+    return soft_min_j(v, p->n_obs, p->softmin_alpha);
+}
+
+/* SDF of the scene at world point (cx, cy) given as jets (any dimension). */
+static jet sdf_point(const NlotProblem* p, const NlotMlpDesc* m, jet cx, jet cy, int want) {
+    if (p->sdf_kind == NLOT_SDF_ANALYTIC) return sdf_analytic(p, cx, cy);
+    float o[6];
+    /* NNObstacle.approximated_sdf -> l4casadi forward: CasADi double cast to float (gen/nn_sdf.cpp) */
+    oracle_mlp_point(m, (float)cx.v, (float)cy.v, 1.f, want, o);
+    double g[2] = {o[1], o[2]}, H[3] = {o[3], o[4], o[5]};
+    if (!want) return jconst(cx.n, (double)o[0]);
+    return jcompose2((double)o[0], g, H, cx, cy);
+}
+
+/* Batched scene SDF at points (value, gradient, Hessian); out [P][6]. */
+void oracle_sdf_eval(const NlotProblem* p, const NlotMlpDesc* m, const double* pts, long P, double* out) {
+    for (long i = 0; i < P; ++i) {
+        jet x = jvar(2, pts[2 * i], 0), y = jvar(2, pts[2 * i + 1], 1);
+        jet s = sdf_point(p, m, x, y, 1);
+        out[6 * i + 0] = s.v;
+        out[6 * i + 1] = s.g[0];
+        out[6 * i + 2] = s.g[1];
+        out[6 * i + 3] = s.h[hix(0, 0)];
+        out[6 * i + 4] = s.h[hix(1, 0)];
+        out[6 * i + 5] = s.h[hix(1, 1)];
+    }
+}
+
+double oracle_soft_min(const double* v, int n, double alpha) {
+    jet a[64];
+    for (int i = 0; i < n; ++i) a[i] = jconst(1, v[i]);
+    return soft_min_j(a, n, alpha).v;
+}
+
+/* ============================================================================================ */
+/* Dynamics (core/dynamics.py)                                                                  */
+/* ============================================================================================ */
+/* f(x, u) as jets over z = (x, u); n = nx + nu */
+static void dyn_f(const NlotProblem* p, const jet* x, const jet* u, jet* f) {
+    int n = x[0].n;
+    switch (p->dynamics) {
+    case NLOT_POINT_1ST: /* dynamics.py:40-41 */
+        f[0] = u[0];
+        f[1] = u[1];
+        f[2] = jconst(n, 0.0);
+        f[3] = jconst(n, 0.0);
+        break;
+    case NLOT_POINT_2ND: /* dynamics.py:51-56 */
+        f[0] = x[2];
+        f[1] = x[3];
+        f[2] = u[0];
+        f[3] = u[1];
+        break;
+    case NLOT_UNICYCLE: /* dynamics.py:66-73 */
+        f[0] = jmul(u[0], jcos(x[2]));
+        f[1] = jmul(u[0], jsin(x[2]));
+        f[2] = u[1];
+        break;
+    case NLOT_UNICYCLE_2ND: /* dynamics.py:83-96 */
+        f[0] = jmul(x[3], jcos(x[2]));
+        f[1] = jmul(x[3], jsin(x[2]));
+        f[2] = x[4];
+        f[3] = u[0];
+        f[4] = u[1];
+        break;
+    case NLOT_ACKERMANN: /* dynamics.py:109-118 */
+        f[0] = jmul(u[0], jcos(x[2]));
+        f[1] = jmul(u[0], jsin(x[2]));
+        f[2] = jscale(jmul(u[0], jtan(x[3])), 1.0 / p->wheelbase);
+        f[3] = u[1];
+        break;
+    case NLOT_ACKERMANN_2ND: { /* dynamics.py:131-148, vector order reproduced as written */
+        jet th = x[2], psi = x[3], v = x[4], psid = x[6], a = u[0], al = u[1];
+        f[0] = jmul(v, jcos(th));
+        f[1] = jmul(v, jsin(th));
+        f[2] = jscale(jmul(v, jtan(psi)), 1.0 / p->wheelbase);
+        f[3] = psid;
+        /* domega = 1/L * (dpsi / (1 + psi^2) * v + tan(psi) * a) */
+        f[4] = jscale(jadd(jmul(jdiv(psid, jaddc(jsq(psi), 1.0)), v), jmul(jtan(psi), a)), 1.0 / p->wheelbase);
+        f[5] = a;
+        f[6] = al;
+        break;
+    }
+    default:
+        for (int i = 0; i < p->nx; ++i) f[i] = jconst(n, NAN);
+    }
+}
+
+void oracle_dynamics(const NlotProblem* p, const double* x, const double* u, double* f) {
+    int n = p->nx + p->nu;
+    jet xj[8], uj[4], fj[8];
+    for (int i = 0; i < p->nx; ++i) xj[i] = jconst(n, x[i]);
+    for (int i = 0; i < p->nu; ++i) uj[i] = jconst(n, u[i]);
+    dyn_f(p, xj, uj, fj);
+    for (int i = 0; i < p->nx; ++i) f[i] = fj[i].v;
+}
+
+/* F = x + dt f(x,u) (runner.py:62-63): value, A = dF/dx, B = dF/du, Hl = sum_i lam_i d2F_i/dz2 */
+static void dyn_eval(const NlotProblem* p, const double* x, const double* u, const double* lam, double* F,
+                     double* A, double* B, double* Hl) {
+    int nx = p->nx, nu = p->nu, n = nx + nu;
+    jet xj[8], uj[4], fj[8];
+    for (int i = 0; i < nx; ++i) xj[i] = jvar(n, x[i], i);
+    for (int i = 0; i < nu; ++i) uj[i] = jvar(n, u[i], nx + i);
+    dyn_f(p, xj, uj, fj);
+    for (int i = 0; i < nx; ++i) {
+        F[i] = x[i] + p->dt * fj[i].v;
+        if (A)
+            for (int j = 0; j < nx; ++j) A[i * nx + j] = (i == j ? 1.0 : 0.0) + p->dt * fj[i].g[j];
+        if (B)
+            for (int j = 0; j < nu; ++j) B[i * nu + j] = p->dt * fj[i].g[nx + j];
+    }
+    if (Hl) {
+        for (int a = 0; a < n; ++a)
+            for (int b = 0; b < n; ++b) {
+                double s = 0;
+                for (int i = 0; i < nx; ++i) s += lam[i] * fj[i].h[hix(a, b)];
+                Hl[a * n + b] = p->dt * s;
+            }
+    }
+}
+
+/* ============================================================================================ */
+/* Geometry: corners and per-knot SDF constraints (core/geometry.py)                            */
+/* ============================================================================================ */
+void oracle_corners(const NlotProblem* p, const double* pose, double* out) { /* geometry.py:78-83 */
+    double c = cos(pose[2]), s = sin(pose[2]);
+    for (int i = 0; i < p->n_body; ++i) {
+        out[2 * i] = pose[0] + c * p->body[i][0] - s * p->body[i][1];
+        out[2 * i + 1] = pose[1] + s * p->body[i][0] + c * p->body[i][1];
+    }
+}
+
+/* number of inequality constraints per knot */
+static int knot_m(const NlotProblem* p) {
+    if (p->shape == NLOT_SHAPE_DOT) return 1;
+    return p->use_slack ? 1 : p->n_body;
+}
+
+/* Inequality functions at knot k w.r.t. pose (x, y, theta) = state[0..2] (jets, n = 3).
+ * The slack s_k enters linearly with coefficient 1 (geometry.py:116-117) and is added by callers.
+ * dot:      d = sdf(x, y)                                    geometry.py:63-67 (slack ignored, bug F7b)
+ * slack:    d = soft_min_i sdf(c_i) (+ s_k)                  geometry.py:115-117, margin 0 (runner.py:76)
+ * no slack: d_i = sdf(c_i), one per corner                   geometry.py:112-114
+ * (densify_polygon with num_points=0 returns the corners, geometry.py:85-105) */
+static int knot_ineq(const NlotProblem* p, const NlotMlpDesc* m, const double* xk, int want, jet* d) {
+    jet X = jvar(3, xk[0], 0), Y = jvar(3, xk[1], 1);
+    if (p->shape == NLOT_SHAPE_DOT) {
+        d[0] = sdf_point(p, m, X, Y, want);
+        return 1;
+    }
+    jet T = jvar(3, xk[2], 2);
+    jet c = jcos(T), s = jsin(T);
+    jet phi[NLOT_MAX_BODY];
+    for (int i = 0; i < p->n_body; ++i) {
+        double bx = p->body[i][0], by = p->body[i][1];
+        jet cx = jadd(X, jsub(jscale(c, bx), jscale(s, by)));
+        jet cy = jadd(Y, jadd(jscale(s, bx), jscale(c, by)));
+        phi[i] = sdf_point(p, m, cx, cy, want);
+    }
+    if (p->use_slack) {
+        d[0] = soft_min_j(phi, p->n_body, p->softmin_alpha);
+        return 1;
+    }
+    for (int i = 0; i < p->n_body; ++i) d[i] = phi[i];
+    return p->n_body;
+}
+
+/* value of the per-knot inequality functions (including slack) — exported for tests */
+int oracle_knot_constraints(const NlotProblem* p, const NlotMlpDesc* m, const double* xk, double sk, double* d,
+                            double* grad3) {
+    jet dj[NLOT_MAX_BODY];
+    int mm = knot_ineq(p, m, xk, 1, dj);
+    for (int j = 0; j < mm; ++j) {
+        d[j] = dj[j].v + ((p->use_slack && p->shape != NLOT_SHAPE_DOT) ? sk : 0.0);
+        if (grad3)
+            for (int i = 0; i < 3; ++i) grad3[3 * j + i] = dj[j].g[i];
+    }
+    return mm;
+}
+
+/* ============================================================================================ */
+/* Small dense linear algebra                                                                   */
+/* ============================================================================================ */
+/* In-place Cholesky of the n x n row-major SPD matrix a (lower factor).  Returns 0 on success,
+ * 1 when a pivot is not safely positive (the inertia test of the Newton system). */
+static int chol(double* a, int n) {
+    double scale = 1.0;
+    for (int i = 0; i < n; ++i) scale = fmax(scale, fabs(a[i * n + i]));
+    for (int j = 0; j < n; ++j) {
+        double d = a[j * n + j];
+        for (int k = 0; k < j; ++k) d -= a[j * n + k] * a[j * n + k];
+        if (!(d > 1e-13 * scale) || !isfinite(d)) return 1;
+        d = sqrt(d);
+        a[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = a[i * n + j];
+            for (int k = 0; k < j; ++k) s -= a[i * n + k] * a[j * n + k];
+            a[i * n + j] = s / d;
+        }
+    }
+    return 0;
+}
+/* solve (L L^T) X = Bm for X (n x m, row-major), in place */
+static void chol_solve(const double* L, int n, double* Bm, int m) {
+    for (int c = 0; c < m; ++c) {
+        for (int i = 0; i < n; ++i) {
+            double s = Bm[i * m + c];
+            for (int k = 0; k < i; ++k) s -= L[i * n + k] * Bm[k * m + c];
+            Bm[i * m + c] = s / L[i * n + i];
+        }
+        for (int i = n - 1; i >= 0; --i) {
+            double s = Bm[i * m + c];
+            for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * Bm[k * m + c];
+            Bm[i * m + c] = s / L[i * n + i];
+        }
+    }
+}
+
+/* Symmetric indefinite LDL^T with diagonal (1x1) pivoting on the largest remaining |a_ii|.
+ * a: n x n row-major, overwritten by unit-lower L (strict lower) and D (diagonal); perm: pivot order.
+ * Returns 0 and sets *nneg, or 2 when a pivot is numerically zero (singular). */
+static int ldl(double* a, int n, int* perm, int* nneg) {
+    double scale = 1e-300;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) scale = fmax(scale, fabs(a[i * n + j]));
+    for (int i = 0; i < n; ++i) perm[i] = i;
+    *nneg = 0;
+    for (int j = 0; j < n; ++j) {
+        int pv = j;
+        for (int i = j + 1; i < n; ++i)
+            if (fabs(a[i * n + i]) > fabs(a[pv * n + pv])) pv = i;
+        if (pv != j) { /* symmetric swap of rows/cols j and pv */
+            for (int c = 0; c < n; ++c) {
+                double t = a[j * n + c];
+                a[j * n + c] = a[pv * n + c];
+                a[pv * n + c] = t;
+            }
+            for (int r = 0; r < n; ++r) {
+                double t = a[r * n + j];
+                a[r * n + j] = a[r * n + pv];
+                a[r * n + pv] = t;
+            }
+            int t = perm[j];
+            perm[j] = perm[pv];
+            perm[pv] = t;
+        }
+        double d = a[j * n + j];
+        if (!(fabs(d) > 1e-13 * scale) || !isfinite(d)) return 2;
+        if (d < 0) (*nneg)++;
+        double col[16];
+        for (int i = j + 1; i < n; ++i) col[i] = a[i * n + j];
+        for (int i = j + 1; i < n; ++i) {
+            for (int k = j + 1; k <= i; ++k) a[i * n + k] -= col[i] * col[k] / d;
+            a[i * n + j] = col[i] / d;
+        }
+        for (int i = j + 1; i < n; ++i) /* keep the trailing block symmetric (upper mirrors lower) */
+            for (int k = i + 1; k < n; ++k) a[i * n + k] = a[k * n + i];
+    }
+    return 0;
+}
+/* Solve (P' L D L' P) X = Bm in place, X n x m */
+static void ldl_solve(const double* a, int n, const int* perm, double* Bm, int m);
+int oracle_ldl_test(double* a, int n, double* b, int* nneg) {
+    int perm[16];
+    int st = ldl(a, n, perm, nneg);
+    if (!st) ldl_solve(a, n, perm, b, 1);
+    return st;
+}
+static void ldl_solve(const double* a, int n, const int* perm, double* Bm, int m) {
+    double t[16];
+    for (int c = 0; c < m; ++c) {
+        for (int i = 0; i < n; ++i) t[i] = Bm[perm[i] * m + c];
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < i; ++k) t[i] -= a[i * n + k] * t[k];
+        for (int i = 0; i < n; ++i) t[i] /= a[i * n + i];
+        for (int i = n - 1; i >= 0; --i)
+            for (int k = i + 1; k < n; ++k) t[i] -= a[k * n + i] * t[k];
+        for (int i = 0; i < n; ++i) Bm[perm[i] * m + c] = t[i];
+    }
+}
+
+/* ============================================================================================ */
+/* Solver state                                                                                 */
+/* ============================================================================================ */
+#define FILT_MAX 128
+#define XMAX 8
+#define VMAX 5
+#define ZMAX (XMAX + VMAX)
+#define CMAX 8
+
+typedef struct {
+    const NlotProblem* p;
+    const NlotMlpDesc* m;
+    const NlotSolverOptions* o;
+    int nx, nu, ns, N, M, nc, sd; /* sd: slack enters d (polygon + slack) */
+    int tidx[CMAX];
+    double x0[XMAX], xg[XMAX];
+    /* iterate */
+    double *X, *U, *S, *T;
+    double *yi, *yk, *yt, *yd;
+    double *zl, *zu, *zs, *vt;
+    /* evaluation at current iterate */
+    double f;
+    double *gX, *gU, *gS;
+    double *F, *A, *B, *Hdyn;
+    double *dv, *Jd, *Hd;
+    double *Gs; /* path-length Hessian per segment, 2x2 */
+    /* Newton system (stage-wise) */
+    double *H, *g; /* (N+1) * ZMAX*ZMAX, (N+1) * ZMAX — condensed, unsubstituted */
+    double *Kf, *kf, *Kn; /* (N+1) * VMAX*XMAX, VMAX, VMAX*CMAX */
+    double *Pm, *pv, *Gm; /* (N+1) * XMAX*XMAX, XMAX, XMAX*CMAX */
+    double dx0[XMAX], rN[CMAX];
+    double *cdef; /* N * nx dynamics offsets */
+    /* equality residuals c(x) in IPOPT sign: x0-x0bar | x_{k+1}-F_k | C x_N - xg | d - t (the RHS) */
+    double *rci, *rcd, *rct, *rcq;
+    /* step */
+    double *dX, *dU, *dS, *dT;
+    double *yi_n, *yk_n, *yt_n, *yd_n;
+    double *dzl, *dzu, *dzs, *dvt;
+    /* scalars */
+    double mu, tau, dw_last, theta_max, theta_min;
+    int nfilt;
+    double filt_theta[FILT_MAX], filt_phi[FILT_MAX];
+    double lin_resid; /* debug: max residual of the linear KKT system */
+    double dc_used;   /* delta_c applied to the terminal block in the last solve */
+    double *arena;
+} Sol;
+
+static int nv_of(const Sol* s, int k) { return (k < s->N ? s->nu : 0) + s->ns; }
+
+static int sol_alloc(Sol* s) {
+    int N = s->N, nx = s->nx, nu = s->nu, M = s->M;
+    size_t n = 0;
+#define TAKE(ptr, cnt) n += (size_t)(cnt);
+#define ALLOCS                                                                                   \
+    TAKE(X, (N + 1) * nx) TAKE(U, N * nu) TAKE(S, (N + 1)) TAKE(T, (N + 1) * M) TAKE(yi, nx)     \
+    TAKE(yk, N * nx) TAKE(yt, CMAX) TAKE(yd, (N + 1) * M) TAKE(zl, N * nu) TAKE(zu, N * nu)       \
+    TAKE(zs, (N + 1)) TAKE(vt, (N + 1) * M) TAKE(gX, (N + 1) * nx) TAKE(gU, N * nu)               \
+    TAKE(gS, (N + 1)) TAKE(F, N * nx) TAKE(A, N * nx * nx) TAKE(B, N * nx * nu)                   \
+    TAKE(Hdyn, N * (nx + nu) * (nx + nu)) TAKE(dv, (N + 1) * M) TAKE(Jd, (N + 1) * M * 3)         \
+    TAKE(Hd, (N + 1) * 9) TAKE(Gs, N * 4) TAKE(H, (N + 1) * ZMAX * ZMAX) TAKE(g, (N + 1) * ZMAX)  \
+    TAKE(Kf, (N + 1) * VMAX * XMAX) TAKE(kf, (N + 1) * VMAX) TAKE(Kn, (N + 1) * VMAX * CMAX)      \
+    TAKE(Pm, (N + 1) * XMAX * XMAX) TAKE(pv, (N + 1) * XMAX) TAKE(Gm, (N + 1) * XMAX * CMAX)      \
+    TAKE(cdef, N * nx) TAKE(dX, (N + 1) * nx) TAKE(dU, N * nu) TAKE(dS, (N + 1))                 \
+    TAKE(dT, (N + 1) * M) TAKE(yi_n, nx) TAKE(yk_n, N * nx) TAKE(yt_n, CMAX)                     \
+    TAKE(yd_n, (N + 1) * M) TAKE(dzl, N * nu) TAKE(dzu, N * nu) TAKE(dzs, (N + 1))               \
+    TAKE(dvt, (N + 1) * M) TAKE(rci, XMAX) TAKE(rcd, N * nx) TAKE(rct, CMAX) TAKE(rcq, (N + 1) * M)
+    ALLOCS
+#undef TAKE
+    s->arena = (double*)calloc(n, sizeof(double));
+    if (!s->arena) return 1;
+    double* q = s->arena;
+#define TAKE(ptr, cnt) s->ptr = q; q += (size_t)(cnt);
+    ALLOCS
+#undef TAKE
+    return 0;
+}
+
+/* ============================================================================================ */
+/* NLP evaluation (runner.py:44-108)                                                            */
+/* ============================================================================================ */
+/* objective value at (X, U, S)  — runner.py:80-96 */
+static double objective(const Sol* s, const double* X, const double* U, const double* S) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N;
+    double f = 0;
+    for (int k = 0; k < N; ++k) {
+        double dx = X[(k + 1) * nx] - X[k * nx], dy = X[(k + 1) * nx + 1] - X[k * nx + 1];
+        f += sqrt(dx * dx + dy * dy + p->path_eps);
+    }
+    if (p->use_slack) {
+        double q = 0;
+        for (int k = 0; k <= N; ++k) q += S[k] * S[k];
+        f += p->slack_penalty * q;
+    }
+    if (p->use_smooth) {
+        double q = 0;
+        for (int k = 0; k < N - 1; ++k) /* sum_{k < N-1} ||u_k||^2, runner.py:92-95 (bug F7c kept) */
+            for (int i = 0; i < nu; ++i) q += U[k * nu + i] * U[k * nu + i];
+        f += p->smooth_weight * q;
+    }
+    return f;
+}
+
+/* Equality residuals c(x) (IPOPT sign) at a point; any output may be NULL. */
+static void residuals(const Sol* s, const double* X, const double* U, const double* S, const double* T, double* rci,
+                      double* rcd, double* rct, double* rcq) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    for (int i = 0; i < nx; ++i) rci[i] = X[i] - s->x0[i];
+    for (int j = 0; j < s->nc; ++j) rct[j] = X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]];
+    for (int k = 0; k < N; ++k) {
+        double Fk[XMAX];
+        dyn_eval(p, X + k * nx, U + k * nu, NULL, Fk, NULL, NULL, NULL);
+        for (int i = 0; i < nx; ++i) rcd[k * nx + i] = X[(k + 1) * nx + i] - Fk[i];
+    }
+    for (int k = 0; k <= N; ++k) {
+        jet d[NLOT_MAX_BODY];
+        knot_ineq(p, s->m, X + k * nx, 0, d);
+        for (int j = 0; j < M; ++j) rcq[k * M + j] = d[j].v + (s->sd ? S[k] : 0.0) - T[k * M + j];
+    }
+}
+
+/* Constraint violation theta = ||c||_1 (incl. d - t) and barrier value phi_mu at a point;
+ * the residual arrays (may be NULL) receive c(x). */
+static void merit_r(const Sol* s, const double* X, const double* U, const double* S, const double* T, double mu,
+                    double* theta, double* phi, double* rci, double* rcd, double* rct, double* rcq) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double bi[XMAX], bt[CMAX];
+    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* bq = bd + N * nx;
+    if (!rci) rci = bi;
+    if (!rct) rct = bt;
+    if (!rcd) rcd = bd;
+    if (!rcq) rcq = bq;
+    residuals(s, X, U, S, T, rci, rcd, rct, rcq);
+    double th = 0, bar = 0, lin = 0;
+    for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
+    for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
+    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        th += fabs(rcq[q]);
+        bar += log(T[q]);
+        lin += T[q];
+    }
+    free(bd);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) {
+            bar += log(S[k]);
+            lin += S[k];
+        }
+    const double kappa_d = 1e-5;
+    *theta = th;
+    *phi = objective(s, X, U, S) - mu * bar + kappa_d * mu * lin;
+}
+static void merit(const Sol* s, const double* X, const double* U, const double* S, const double* T, double mu,
+                  double* theta, double* phi, double* fout) {
+    merit_r(s, X, U, S, T, mu, theta, phi, NULL, NULL, NULL, NULL);
+    if (fout) *fout = objective(s, X, U, S);
+}
+
+/* Full evaluation at the current iterate: gradients, Jacobians, Lagrangian-Hessian pieces. */
+static void eval_full(Sol* s) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M, nz = nx + nu;
+    s->f = objective(s, s->X, s->U, s->S);
+    memset(s->gX, 0, sizeof(double) * (N + 1) * nx);
+    memset(s->gU, 0, sizeof(double) * N * nu);
+    memset(s->gS, 0, sizeof(double) * (N + 1));
+    for (int k = 0; k < N; ++k) { /* path length, runner.py:82-86 */
+        double dx = s->X[(k + 1) * nx] - s->X[k * nx], dy = s->X[(k + 1) * nx + 1] - s->X[k * nx + 1];
+        double r2 = dx * dx + dy * dy + p->path_eps, r = sqrt(r2), r3 = r2 * r;
+        s->gX[(k + 1) * nx] += dx / r;
+        s->gX[(k + 1) * nx + 1] += dy / r;
+        s->gX[k * nx] -= dx / r;
+        s->gX[k * nx + 1] -= dy / r;
+        s->Gs[4 * k + 0] = (r2 - dx * dx) / r3;
+        s->Gs[4 * k + 1] = -dx * dy / r3;
+        s->Gs[4 * k + 2] = -dx * dy / r3;
+        s->Gs[4 * k + 3] = (r2 - dy * dy) / r3;
+    }
+    if (p->use_slack)
+        for (int k = 0; k <= N; ++k) s->gS[k] = 2.0 * p->slack_penalty * s->S[k];
+    if (p->use_smooth)
+        for (int k = 0; k < N - 1; ++k)
+            for (int i = 0; i < nu; ++i) s->gU[k * nu + i] = 2.0 * p->smooth_weight * s->U[k * nu + i];
+    for (int k = 0; k < N; ++k) {
+        double Fk[XMAX];
+        dyn_eval(p, s->X + k * nx, s->U + k * nu, s->yk + k * nx, Fk, s->A + k * nx * nx, s->B + k * nx * nu,
+                 s->Hdyn + k * nz * nz);
+        for (int i = 0; i < nx; ++i) {
+            s->F[k * nx + i] = Fk[i];
+            s->rcd[k * nx + i] = s->X[(k + 1) * nx + i] - Fk[i];
+        }
+    }
+    for (int i = 0; i < nx; ++i) s->rci[i] = s->X[i] - s->x0[i];
+    for (int j = 0; j < s->nc; ++j) s->rct[j] = s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]];
+    for (int k = 0; k <= N; ++k) {
+        jet d[NLOT_MAX_BODY];
+        knot_ineq(p, s->m, s->X + k * nx, 1, d);
+        double* Hd = s->Hd + 9 * k;
+        memset(Hd, 0, sizeof(double) * 9);
+        for (int j = 0; j < M; ++j) {
+            s->dv[k * M + j] = d[j].v + (s->sd ? s->S[k] : 0.0);
+            s->rcq[k * M + j] = s->dv[k * M + j] - s->T[k * M + j];
+            for (int a = 0; a < 3; ++a) s->Jd[(k * M + j) * 3 + a] = d[j].g[a];
+            double w = s->yd[k * M + j];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) Hd[a * 3 + b] += w * d[j].h[hix(a, b)];
+        }
+    }
+}
+
+/* Optimality measures (IPOPT's OptimalityErrorConvergenceCheck / curr_barrier_error). */
+typedef struct {
+    double dual, primal, compl0, complmu, sd, sc, cviol;
+} Errs;
+
+static void errors(const Sol* s, Errs* e) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0;
+    int ny = 0, nzc = 0;
+    /* dual infeasibility: grad L over x, u, s, t */
+    for (int k = 0; k <= N; ++k) {
+        double r[XMAX];
+        for (int i = 0; i < nx; ++i) r[i] = s->gX[k * nx + i];
+        if (k > 0)
+            for (int i = 0; i < nx; ++i) r[i] += s->yk[(k - 1) * nx + i];
+        if (k < N)
+            for (int j = 0; j < nx; ++j) {
+                double t = 0;
+                for (int i = 0; i < nx; ++i) t += s->A[k * nx * nx + i * nx + j] * s->yk[k * nx + i];
+                r[j] -= t;
+            }
+        if (k == 0)
+            for (int i = 0; i < nx; ++i) r[i] += s->yi[i];
+        if (k == N)
+            for (int j = 0; j < s->nc; ++j) r[s->tidx[j]] += s->yt[j];
+        for (int j = 0; j < M; ++j)
+            for (int a = 0; a < 3; ++a) r[a] += s->Jd[(k * M + j) * 3 + a] * s->yd[k * M + j];
+        for (int i = 0; i < nx; ++i) dual = fmax(dual, fabs(r[i]));
+        if (k < N)
+            for (int i = 0; i < nu; ++i) {
+                double t = s->gU[k * nu + i] - s->zl[k * nu + i] + s->zu[k * nu + i];
+                for (int a = 0; a < nx; ++a) t -= s->B[k * nx * nu + a * nu + i] * s->yk[k * nx + a];
+                dual = fmax(dual, fabs(t));
+            }
+        if (s->ns) {
+            double t = s->gS[k] - s->zs[k];
+            if (s->sd)
+                for (int j = 0; j < M; ++j) t += s->yd[k * M + j];
+            dual = fmax(dual, fabs(t));
+        }
+        for (int j = 0; j < M; ++j) dual = fmax(dual, fabs(-s->yd[k * M + j] - s->vt[k * M + j]));
+    }
+    /* primal infeasibility (c, d - t) and unscaled constraint violation */
+    for (int i = 0; i < nx; ++i) primal = fmax(primal, fabs(s->X[i] - s->x0[i]));
+    for (int j = 0; j < s->nc; ++j) primal = fmax(primal, fabs(s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]]));
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nx; ++i) primal = fmax(primal, fabs(s->X[(k + 1) * nx + i] - s->F[k * nx + i]));
+    cviol = primal;
+    for (int k = 0; k <= N; ++k)
+        for (int j = 0; j < M; ++j) {
+            primal = fmax(primal, fabs(s->dv[k * M + j] - s->T[k * M + j]));
+            cviol = fmax(cviol, fmax(0.0, -s->dv[k * M + j]));
+        }
+    /* complementarity */
+#define COMPL(z, sl)                                                                             \
+    do {                                                                                         \
+        double zz = (z), ss = (sl);                                                              \
+        c0 = fmax(c0, fabs(zz * ss));                                                            \
+        cmu = fmax(cmu, fabs(zz * ss - s->mu));                                                  \
+        zsum += fabs(zz);                                                                        \
+        nzc++;                                                                                   \
+    } while (0)
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            COMPL(s->zl[k * nu + i], s->U[k * nu + i] - p->umin[i]);
+            COMPL(s->zu[k * nu + i], p->umax[i] - s->U[k * nu + i]);
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k]);
+    for (int k = 0; k <= N; ++k)
+        for (int j = 0; j < M; ++j) COMPL(s->vt[k * M + j], s->T[k * M + j]);
+#undef COMPL
+    for (int i = 0; i < nx; ++i) ysum += fabs(s->yi[i]);
+    for (int i = 0; i < N * nx; ++i) ysum += fabs(s->yk[i]);
+    for (int j = 0; j < s->nc; ++j) ysum += fabs(s->yt[j]);
+    for (int i = 0; i < (N + 1) * M; ++i) ysum += fabs(s->yd[i]);
+    ny = nx + N * nx + s->nc + (N + 1) * M;
+    const double smax = 100.0;
+    e->sd = fmax(smax, (ysum + zsum) / (double)(ny + nzc)) / smax;
+    e->sc = fmax(smax, zsum / (double)nzc) / smax;
+    e->dual = dual;
+    e->primal = primal;
+    e->compl0 = c0;
+    e->complmu = cmu;
+    e->cviol = cviol;
+}
+
+/* ============================================================================================ */
+/* Newton system: stage matrices + Riccati recursion                                            */
+/* ============================================================================================ */
+enum { MODE_NEWTON = 0, MODE_LSQ = 1 };
+
+/* Build the condensed stage-wise system:
+ *   min sum_k 1/2 z_k' H_k z_k + g_k' z_k + sum_k dx_k' M_k dx_{k+1}
+ *   s.t. dx_0 = dx0, dx_{k+1} = A_k dx_k + B_k dv_k + c_k, C dx_N = rN
+ * H_k includes W_kk + Sigma + dw I + J_d' D J_d (IPOPT slacks t and their duals eliminated). */
+static void build(Sol* s, int mode, double dw) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M, nzd = nx + nu;
+    const double kappa_d = 1e-5;
+    double mu = s->mu;
+    for (int k = 0; k <= N; ++k) {
+        int nvk = nv_of(s, k), nzk = nx + nvk, iu = nx, is = nx + (k < N ? nu : 0);
+        double* H = s->H + (size_t)k * ZMAX * ZMAX;
+        double* g = s->g + (size_t)k * ZMAX;
+        memset(H, 0, sizeof(double) * ZMAX * ZMAX);
+        memset(g, 0, sizeof(double) * ZMAX);
+#define HH(i, j) H[(i)*nzk + (j)]
+        for (int i = 0; i < nx; ++i) g[i] = s->gX[k * nx + i];
+        if (k < N)
+            for (int i = 0; i < nu; ++i) g[iu + i] = s->gU[k * nu + i];
+        if (s->ns) g[is] = s->gS[k];
+        if (mode == MODE_NEWTON) {
+            /* objective Hessian */
+            for (int a = 0; a < 2; ++a)
+                for (int b = 0; b < 2; ++b) {
+                    if (k < N) HH(a, b) += s->Gs[4 * k + 2 * a + b];
+                    if (k > 0) HH(a, b) += s->Gs[4 * (k - 1) + 2 * a + b];
+                }
+            if (p->use_slack) HH(is, is) += 2.0 * p->slack_penalty;
+            if (p->use_smooth && k < N - 1)
+                for (int i = 0; i < nu; ++i) HH(iu + i, iu + i) += 2.0 * p->smooth_weight;
+            /* dynamics constraint c_k = x_{k+1} - F_k: W += -sum_i y_i d2F_i */
+            if (k < N)
+                for (int a = 0; a < nzd; ++a)
+                    for (int b = 0; b < nzd; ++b) HH(a, b) -= s->Hdyn[(size_t)k * nzd * nzd + a * nzd + b];
+            /* knot inequality curvature  sum_j yd_j d2 d_j (pose block) */
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b)
+                    if (a < nx && b < nx) HH(a, b) += s->Hd[9 * k + a * 3 + b];
+            /* bound barriers Sigma and barrier gradient */
+            if (k < N)
+                for (int i = 0; i < nu; ++i) {
+                    double sl = s->U[k * nu + i] - p->umin[i], su = p->umax[i] - s->U[k * nu + i];
+                    HH(iu + i, iu + i) += s->zl[k * nu + i] / sl + s->zu[k * nu + i] / su;
+                    g[iu + i] += -mu / sl + mu / su;
+                }
+            if (s->ns) {
+                HH(is, is) += s->zs[k] / s->S[k];
+                g[is] += -mu / s->S[k] + kappa_d * mu;
+            }
+            for (int i = 0; i < nzk; ++i) HH(i, i) += dw;
+        } else {
+            for (int i = 0; i < nzk; ++i) HH(i, i) = 1.0;
+            if (k < N)
+                for (int i = 0; i < nu; ++i) g[iu + i] += -s->zl[k * nu + i] + s->zu[k * nu + i];
+            if (s->ns) g[is] += -s->zs[k];
+        }
+        /* eliminated inequality slacks t (IPOPT d(x) - t = 0, t >= 0) */
+        for (int j = 0; j < M; ++j) {
+            double J[ZMAX];
+            memset(J, 0, sizeof J);
+            for (int a = 0; a < 3 && a < nx; ++a) J[a] = s->Jd[(k * M + j) * 3 + a];
+            if (s->sd) J[is] = 1.0;
+            double D, rhs;
+            double t = s->T[k * M + j], v = s->vt[k * M + j];
+            if (mode == MODE_NEWTON) {
+                D = v / t + dw;
+                rhs = D * s->rcq[k * M + j] + (-mu / t + kappa_d * mu);
+            } else {
+                D = 1.0;
+                rhs = -v;
+            }
+            for (int a = 0; a < nzk; ++a) {
+                g[a] += J[a] * rhs;
+                for (int b = 0; b < nzk; ++b) HH(a, b) += D * J[a] * J[b];
+            }
+        }
+#undef HH
+    }
+    if (mode == MODE_NEWTON) {
+        for (int i = 0; i < nx; ++i) s->dx0[i] = -s->rci[i];
+        for (int j = 0; j < s->nc; ++j) s->rN[j] = -s->rct[j];
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nx; ++i) s->cdef[k * nx + i] = -s->rcd[k * nx + i];
+    } else {
+        memset(s->dx0, 0, sizeof s->dx0);
+        memset(s->rN, 0, sizeof s->rN);
+        memset(s->cdef, 0, sizeof(double) * N * nx);
+    }
+}
+
+/* Cross block M_k between positions of x_k and x_{k+1} (path length), Newton mode only. */
+static void cross(const Sol* s, int mode, int k, double* Mk) {
+    int nx = s->nx;
+    memset(Mk, 0, sizeof(double) * XMAX * XMAX);
+    if (mode != MODE_NEWTON) return;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) Mk[a * nx + b] = -s->Gs[4 * k + 2 * a + b];
+}
+
+/* Backward Riccati + terminal multiplier + forward sweep.  Returns 0, or 1 for wrong inertia. */
+static int riccati(Sol* s, int mode) {
+    int nx = s->nx, nu = s->nu, N = s->N, nc = s->nc, negsum = 0;
+    double Pn[XMAX * XMAX], pn[XMAX], Gn[XMAX * CMAX], Psi[CMAX * CMAX], psi[CMAX];
+    memset(Pn, 0, sizeof Pn);
+    memset(pn, 0, sizeof pn);
+    memset(Gn, 0, sizeof Gn);
+    memset(Psi, 0, sizeof Psi);
+    memset(psi, 0, sizeof psi);
+    for (int k = N; k >= 0; --k) {
+        int nv = nv_of(s, k), nz = nx + nv;
+        double Hp[ZMAX * ZMAX], gp[ZMAX], Ak[XMAX * XMAX], Bk[XMAX * VMAX], ck[XMAX];
+        memcpy(Hp, s->H + (size_t)k * ZMAX * ZMAX, sizeof(double) * nz * nz);
+        memcpy(gp, s->g + (size_t)k * ZMAX, sizeof(double) * nz);
+        memset(Ak, 0, sizeof Ak);
+        memset(Bk, 0, sizeof Bk);
+        memset(ck, 0, sizeof ck);
+        if (k < N) {
+            memcpy(Ak, s->A + (size_t)k * nx * nx, sizeof(double) * nx * nx);
+            for (int i = 0; i < nx; ++i)
+                for (int j = 0; j < nu; ++j) Bk[i * nv + j] = s->B[(size_t)k * nx * nu + i * nu + j];
+            memcpy(ck, s->cdef + (size_t)k * nx, sizeof(double) * nx);
+            /* substitute dx_{k+1} = A dx + B dv + c into the cross term dx_k' M_k dx_{k+1} */
+            double Mk[XMAX * XMAX];
+            cross(s, mode, k, Mk);
+            double MA[XMAX * XMAX], MB[XMAX * VMAX], Mc[XMAX];
+            for (int i = 0; i < nx; ++i) {
+                for (int j = 0; j < nx; ++j) {
+                    double t = 0;
+                    for (int q = 0; q < nx; ++q) t += Mk[i * nx + q] * Ak[q * nx + j];
+                    MA[i * nx + j] = t;
+                }
+                for (int j = 0; j < nv; ++j) {
+                    double t = 0;
+                    for (int q = 0; q < nx; ++q) t += Mk[i * nx + q] * Bk[q * nv + j];
+                    MB[i * nv + j] = t;
+                }
+                double t = 0;
+                for (int q = 0; q < nx; ++q) t += Mk[i * nx + q] * ck[q];
+                Mc[i] = t;
+            }
+            for (int i = 0; i < nx; ++i) {
+                for (int j = 0; j < nx; ++j) Hp[i * nz + j] += MA[i * nx + j] + MA[j * nx + i];
+                for (int j = 0; j < nv; ++j) {
+                    Hp[i * nz + nx + j] += MB[i * nv + j];
+                    Hp[(nx + j) * nz + i] += MB[i * nv + j];
+                }
+                gp[i] += Mc[i];
+            }
+        }
+        /* Q = H' + [A B]' P [A B] ; q = g' + [A B]'(P c + p) */
+        double AB[XMAX * ZMAX], PAB[XMAX * ZMAX], Pcp[XMAX];
+        for (int i = 0; i < nx; ++i) {
+            for (int j = 0; j < nx; ++j) AB[i * nz + j] = Ak[i * nx + j];
+            for (int j = 0; j < nv; ++j) AB[i * nz + nx + j] = Bk[i * nv + j];
+        }
+        for (int i = 0; i < nx; ++i) {
+            for (int j = 0; j < nz; ++j) {
+                double t = 0;
+                for (int q = 0; q < nx; ++q) t += Pn[i * nx + q] * AB[q * nz + j];
+                PAB[i * nz + j] = t;
+            }
+            double t = pn[i];
+            for (int q = 0; q < nx; ++q) t += Pn[i * nx + q] * ck[q];
+            Pcp[i] = t;
+        }
+        double Q[ZMAX * ZMAX], q[ZMAX], QN[ZMAX * CMAX];
+        for (int i = 0; i < nz; ++i) {
+            for (int j = 0; j < nz; ++j) {
+                double t = Hp[i * nz + j];
+                for (int r = 0; r < nx; ++r) t += AB[r * nz + i] * PAB[r * nz + j];
+                Q[i * nz + j] = t;
+            }
+            double t = gp[i];
+            for (int r = 0; r < nx; ++r) t += AB[r * nz + i] * Pcp[r];
+            q[i] = t;
+            for (int c = 0; c < nc; ++c) {
+                double u = 0;
+                for (int r = 0; r < nx; ++r) u += AB[r * nz + i] * Gn[r * nc + c];
+                QN[i * nc + c] = u;
+            }
+        }
+        /* factor Q_vv, feedback gains */
+        double L[VMAX * VMAX], Kk[VMAX * XMAX], kk[VMAX], Knk[VMAX * CMAX];
+        if (nv > 0) {
+            for (int i = 0; i < nv; ++i)
+                for (int j = 0; j < nv; ++j) L[i * nv + j] = Q[(nx + i) * nz + nx + j];
+            /* inertia: pivoted LDL^T counts the negative eigenvalues of each
+             * stage block; with Psi_0 below this gives the exact inertia of the Newton matrix. */
+            int perm[VMAX], nneg;
+            if (ldl(L, nv, perm, &nneg)) return 1; /* singular stage block */
+            negsum += nneg;
+            if (negsum > nc) return 1; /* more negatives than the terminal block can absorb */
+            for (int i = 0; i < nv; ++i) {
+                for (int j = 0; j < nx; ++j) Kk[i * nx + j] = -Q[(nx + i) * nz + j];
+                kk[i] = -q[nx + i];
+                for (int c = 0; c < nc; ++c) Knk[i * nc + c] = -QN[(nx + i) * nc + c];
+            }
+            ldl_solve(L, nv, perm, Kk, nx);
+            ldl_solve(L, nv, perm, kk, 1);
+            if (nc) ldl_solve(L, nv, perm, Knk, nc);
+        }
+        memcpy(s->Kf + (size_t)k * VMAX * XMAX, Kk, sizeof(double) * VMAX * XMAX);
+        memcpy(s->kf + (size_t)k * VMAX, kk, sizeof(double) * VMAX);
+        memcpy(s->Kn + (size_t)k * VMAX * CMAX, Knk, sizeof(double) * VMAX * CMAX);
+        /* value function of stage k */
+        double P[XMAX * XMAX], pp[XMAX], G[XMAX * CMAX];
+        for (int i = 0; i < nx; ++i) {
+            for (int j = 0; j < nx; ++j) {
+                double t = Q[i * nz + j];
+                for (int v = 0; v < nv; ++v) t += Q[i * nz + nx + v] * Kk[v * nx + j];
+                P[i * nx + j] = t;
+            }
+            double t = q[i];
+            for (int v = 0; v < nv; ++v) t += Q[i * nz + nx + v] * kk[v];
+            pp[i] = t;
+            for (int c = 0; c < nc; ++c) {
+                double u = QN[i * nc + c];
+                for (int v = 0; v < nv; ++v) u += Q[i * nz + nx + v] * Knk[v * nc + c];
+                G[i * nc + c] = u;
+            }
+        }
+        for (int i = 0; i < nx; ++i)
+            for (int j = 0; j < i; ++j) {
+                double a = 0.5 * (P[i * nx + j] + P[j * nx + i]);
+                P[i * nx + j] = P[j * nx + i] = a;
+            }
+        for (int a = 0; a < nc; ++a) {
+            for (int b = 0; b < nc; ++b) {
+                double t = 0;
+                for (int v = 0; v < nv; ++v) t += QN[(nx + v) * nc + a] * Knk[v * nc + b];
+                Psi[a * nc + b] += t;
+            }
+            double t = 0;
+            for (int r = 0; r < nx; ++r) t += Gn[r * nc + a] * ck[r];
+            for (int v = 0; v < nv; ++v) t += QN[(nx + v) * nc + a] * kk[v];
+            psi[a] += t;
+        }
+        if (k == N) { /* terminal equality C x_N = xg_sel enters here */
+            memset(G, 0, sizeof G);
+            for (int c = 0; c < nc; ++c) {
+                G[s->tidx[c] * nc + c] = 1.0;
+                psi[c] = -s->rN[c];
+            }
+        }
+        memcpy(s->Pm + (size_t)k * XMAX * XMAX, P, sizeof P);
+        memcpy(s->pv + (size_t)k * XMAX, pp, sizeof pp);
+        memcpy(s->Gm + (size_t)k * XMAX * CMAX, G, sizeof G);
+        memcpy(Pn, P, sizeof P);
+        memcpy(pn, pp, sizeof pp);
+        memcpy(Gn, G, sizeof G);
+    }
+    /* terminal multiplier: -Psi_0 nu = Gamma_0' dx0 + psi_0 (IPOPT delta_c if singular) */
+    double nu_[CMAX];
+    s->dc_used = 0.0;
+    if (nc) {
+        /* inertia (Sylvester over the Riccati eliminations): the Newton matrix has the wanted
+         * inertia iff #neg(Psi_0) = nc - sum_k #neg(Q_vv,k) and Psi_0 is nonsingular. */
+        double L[CMAX * CMAX];
+        int perm[CMAX], nneg;
+        for (int i = 0; i < nc * nc; ++i) L[i] = -Psi[i];
+        int st = ldl(L, nc, perm, &nneg); /* nneg counts negatives of -Psi = positives of Psi */
+        if (st == 2 || nneg != negsum) {
+            /* (near-)rank-deficient terminal block (e.g. no lateral motion of a unicycle at v = 0):
+             * IPOPT's delta_c on those rows; a genuine inertia defect survives it. */
+            double dc = 1e-8 * pow(s->mu, 0.25);
+            for (int i = 0; i < nc * nc; ++i) L[i] = -Psi[i];
+            for (int i = 0; i < nc; ++i) L[i * nc + i] += dc;
+            if (ldl(L, nc, perm, &nneg)) return 1;
+            if (nneg != negsum) return 1; /* wrong inertia */
+            s->dc_used = dc;
+        }
+        for (int c = 0; c < nc; ++c) {
+            double t = psi[c];
+            for (int r = 0; r < nx; ++r) t += Gn[r * nc + c] * s->dx0[r];
+            nu_[c] = t;
+        }
+        ldl_solve(L, nc, perm, nu_, 1);
+    } else if (negsum) {
+        return 1;
+    }
+    /* forward sweep */
+    double dx[XMAX];
+    memcpy(dx, s->dx0, sizeof(double) * nx);
+    for (int k = 0; k <= N; ++k) {
+        int nv = nv_of(s, k);
+        const double *Kk = s->Kf + (size_t)k * VMAX * XMAX, *kk = s->kf + (size_t)k * VMAX,
+                     *Knk = s->Kn + (size_t)k * VMAX * CMAX;
+        double dvv[VMAX];
+        for (int v = 0; v < nv; ++v) {
+            double t = kk[v];
+            for (int j = 0; j < nx; ++j) t += Kk[v * nx + j] * dx[j];
+            for (int c = 0; c < nc; ++c) t += Knk[v * nc + c] * nu_[c];
+            dvv[v] = t;
+        }
+        memcpy(s->dX + k * nx, dx, sizeof(double) * nx);
+        if (k < N)
+            for (int i = 0; i < nu; ++i) s->dU[k * nu + i] = dvv[i];
+        if (s->ns) s->dS[k] = dvv[nv - 1];
+        if (k == 0) { /* initial-state multiplier */
+            const double *P = s->Pm, *pp = s->pv, *G = s->Gm;
+            for (int i = 0; i < nx; ++i) {
+                double t = pp[i];
+                for (int j = 0; j < nx; ++j) t += P[i * nx + j] * dx[j];
+                for (int c = 0; c < nc; ++c) t += G[i * nc + c] * nu_[c];
+                s->yi_n[i] = -t;
+            }
+        }
+        if (k < N) {
+            double dn[XMAX];
+            const double* Ak = s->A + (size_t)k * nx * nx;
+            for (int i = 0; i < nx; ++i) {
+                double t = s->cdef[k * nx + i];
+                for (int j = 0; j < nx; ++j) t += Ak[i * nx + j] * dx[j];
+                for (int j = 0; j < nu; ++j) t += s->B[(size_t)k * nx * nu + i * nu + j] * dvv[j];
+                dn[i] = t;
+            }
+            /* dynamics multiplier y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k */
+            const double *P = s->Pm + (size_t)(k + 1) * XMAX * XMAX, *pp = s->pv + (size_t)(k + 1) * XMAX,
+                         *G = s->Gm + (size_t)(k + 1) * XMAX * CMAX;
+            double Mk[XMAX * XMAX];
+            cross(s, mode, k, Mk);
+            for (int i = 0; i < nx; ++i) {
+                double t = pp[i];
+                for (int j = 0; j < nx; ++j) t += P[i * nx + j] * dn[j];
+                for (int c = 0; c < nc; ++c) t += G[i * nc + c] * nu_[c];
+                double mt = 0;
+                for (int j = 0; j < nx; ++j) mt += Mk[j * nx + i] * dx[j];
+                s->yk_n[k * nx + i] = -t - mt;
+            }
+            memcpy(dx, dn, sizeof(double) * nx);
+        }
+    }
+    for (int c = 0; c < nc; ++c) s->yt_n[c] = nu_[c];
+    return 0;
+}
+
+/* Max residual of the full (unsubstituted) linear KKT system for the computed step (debug). */
+static double linear_residual(Sol* s, int mode) {
+    int nx = s->nx, nu = s->nu, N = s->N, nc = s->nc;
+    double res = 0;
+    for (int k = 0; k <= N; ++k) {
+        int nv = nv_of(s, k), nz = nx + nv;
+        double z[ZMAX], r[ZMAX];
+        for (int i = 0; i < nx; ++i) z[i] = s->dX[k * nx + i];
+        if (k < N)
+            for (int i = 0; i < nu; ++i) z[nx + i] = s->dU[k * nu + i];
+        if (s->ns) z[nz - 1] = s->dS[k];
+        const double* H = s->H + (size_t)k * ZMAX * ZMAX;
+        for (int i = 0; i < nz; ++i) {
+            double t = s->g[(size_t)k * ZMAX + i];
+            for (int j = 0; j < nz; ++j) t += H[i * nz + j] * z[j];
+            r[i] = t;
+        }
+        double Mk[XMAX * XMAX];
+        if (k < N) {
+            cross(s, mode, k, Mk);
+            for (int i = 0; i < nx; ++i)
+                for (int j = 0; j < nx; ++j) r[i] += Mk[i * nx + j] * s->dX[(k + 1) * nx + j];
+        }
+        if (k > 0) {
+            cross(s, mode, k - 1, Mk);
+            for (int i = 0; i < nx; ++i)
+                for (int j = 0; j < nx; ++j) r[i] += Mk[j * nx + i] * s->dX[(k - 1) * nx + j];
+            for (int i = 0; i < nx; ++i) r[i] += s->yk_n[(k - 1) * nx + i];
+        }
+        if (k < N) {
+            for (int j = 0; j < nx; ++j)
+                for (int i = 0; i < nx; ++i) r[j] -= s->A[(size_t)k * nx * nx + i * nx + j] * s->yk_n[k * nx + i];
+            for (int j = 0; j < nu; ++j)
+                for (int i = 0; i < nx; ++i) r[nx + j] -= s->B[(size_t)k * nx * nu + i * nu + j] * s->yk_n[k * nx + i];
+        }
+        if (k == 0)
+            for (int i = 0; i < nx; ++i) r[i] += s->yi_n[i];
+        if (k == N)
+            for (int c = 0; c < nc; ++c) r[s->tidx[c]] += s->yt_n[c];
+        for (int i = 0; i < nz; ++i) res = fmax(res, fabs(r[i]));
+    }
+    for (int i = 0; i < nx; ++i) res = fmax(res, fabs(s->dX[i] - s->dx0[i]));
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            double t = s->dX[(k + 1) * nx + i] - s->cdef[k * nx + i];
+            for (int j = 0; j < nx; ++j) t -= s->A[(size_t)k * nx * nx + i * nx + j] * s->dX[k * nx + j];
+            for (int j = 0; j < nu; ++j) t -= s->B[(size_t)k * nx * nu + i * nu + j] * s->dU[k * nu + j];
+            res = fmax(res, fabs(t));
+        }
+    for (int c = 0; c < nc; ++c) /* regularised row: C dx - dc nu = rN */
+        res = fmax(res, fabs(s->dX[N * nx + s->tidx[c]] - s->dc_used * s->yt_n[c] - s->rN[c]));
+    return res;
+}
+
+/* Recover dt, yd+, dz from the primal step (Newton mode). */
+static void recover(Sol* s, double dw) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    const double kappa_d = 1e-5;
+    double mu = s->mu;
+    for (int k = 0; k <= N; ++k)
+        for (int j = 0; j < M; ++j) {
+            int q = k * M + j;
+            double Jdz = 0;
+            for (int a = 0; a < 3 && a < nx; ++a) Jdz += s->Jd[q * 3 + a] * s->dX[k * nx + a];
+            if (s->sd) Jdz += s->dS[k];
+            double t = s->T[q], v = s->vt[q];
+            double dt = Jdz + s->rcq[q];
+            s->dT[q] = dt;
+            s->yd_n[q] = (v / t + dw) * dt + (-mu / t + kappa_d * mu);
+            s->dvt[q] = mu / t - v - (v / t) * dt;
+        }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int q = k * nu + i;
+            double sl = s->U[q] - p->umin[i], su = p->umax[i] - s->U[q], du = s->dU[q];
+            s->dzl[q] = mu / sl - s->zl[q] - (s->zl[q] / sl) * du;
+            s->dzu[q] = mu / su - s->zu[q] + (s->zu[q] / su) * du;
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) s->dzs[k] = mu / s->S[k] - s->zs[k] - (s->zs[k] / s->S[k]) * s->dS[k];
+}
+
+/* ============================================================================================ */
+/* IPOPT main loop (restated)                                                                   */
+/* ============================================================================================ */
+static double frac_to_bound(double sl, double dsl, double tau, double amax) {
+    if (dsl < 0) {
+        double a = -tau * sl / dsl;
+        if (a < amax) return a;
+    }
+    return amax;
+}
+
+static int cmp_le(double lhs, double rhs, double bas) { /* IPOPT Compare_le */
+    return lhs - rhs <= 10.0 * DBL_EPSILON * fabs(bas);
+}
+
+static void filter_add(Sol* s, double theta, double phi) {
+    const double gt = 1e-5, gp = 1e-8;
+    double nt = (1.0 - gt) * theta, np = phi - gp * theta;
+    int w = 0;
+    for (int i = 0; i < s->nfilt; ++i) /* drop entries dominated by the new one */
+        if (!(s->filt_theta[i] >= nt && s->filt_phi[i] >= np)) {
+            s->filt_theta[w] = s->filt_theta[i];
+            s->filt_phi[w] = s->filt_phi[i];
+            ++w;
+        }
+    s->nfilt = w;
+    if (s->nfilt == FILT_MAX) { /* capacity: forget the oldest entry */
+        memmove(s->filt_theta, s->filt_theta + 1, sizeof(double) * (FILT_MAX - 1));
+        memmove(s->filt_phi, s->filt_phi + 1, sizeof(double) * (FILT_MAX - 1));
+        s->nfilt--;
+    }
+    s->filt_theta[s->nfilt] = nt;
+    s->filt_phi[s->nfilt] = np;
+    s->nfilt++;
+}
+static int filter_ok(const Sol* s, double theta, double phi) {
+    for (int i = 0; i < s->nfilt; ++i)
+        if (!(theta <= s->filt_theta[i] || phi <= s->filt_phi[i])) return 0;
+    return 1;
+}
+
+/* IPOPT filter acceptance of a trial point (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint). */
+static int ls_accept(const Sol* s, double theta, double phi, double gd, double alpha, double tht, double pht,
+                     int* armijo_ftype) {
+    const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
+    if (!(isfinite(tht) && isfinite(pht)) || tht > s->theta_max) return 0;
+    int ftype = gd < 0 && alpha * pow(-gd, sph) > delta * pow(theta, sth);
+    int armijo = cmp_le(pht - phi, eta * alpha * gd, phi);
+    int ok;
+    if (ftype && theta <= s->theta_min) {
+        ok = armijo;
+    } else {
+        ok = cmp_le(tht, (1.0 - gt) * theta, theta) || cmp_le(pht - phi, -gp * theta, phi);
+        if (ok && pht > phi) { /* obj_max_inc = 5 */
+            double bas = fabs(phi) > 10.0 ? log10(fabs(phi)) : 1.0;
+            if (log10(pht - phi) > 5.0 + bas) ok = 0;
+        }
+    }
+    if (ok) ok = filter_ok(s, tht, pht);
+    if (ok) *armijo_ftype = ftype && armijo;
+    return ok;
+}
+
+static double primal_frac(const Sol* s, double tau) {
+    const NlotProblem* p = s->p;
+    int nu = s->nu, N = s->N, M = s->M;
+    double a = 1.0;
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int q = k * nu + i;
+            a = frac_to_bound(s->U[q] - p->umin[i], s->dU[q], tau, a);
+            a = frac_to_bound(p->umax[i] - s->U[q], -s->dU[q], tau, a);
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) a = frac_to_bound(s->S[k], s->dS[k], tau, a);
+    for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->T[q], s->dT[q], tau, a);
+    return a;
+}
+static double dual_frac(const Sol* s, double tau) {
+    int nu = s->nu, N = s->N, M = s->M;
+    double a = 1.0;
+    for (int q = 0; q < N * nu; ++q) {
+        a = frac_to_bound(s->zl[q], s->dzl[q], tau, a);
+        a = frac_to_bound(s->zu[q], s->dzu[q], tau, a);
+    }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) a = frac_to_bound(s->zs[k], s->dzs[k], tau, a);
+    for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->vt[q], s->dvt[q], tau, a);
+    return a;
+}
+/* save (dir=0) / restore (dir=1) the full step */
+static void step_save(Sol* s, double* buf, int dir) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double* arrs[] = {s->dX, s->dU, s->dS, s->dT, s->yi_n, s->yk_n, s->yt_n, s->yd_n, s->dzl, s->dzu, s->dzs, s->dvt};
+    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1, (N + 1) * M};
+    for (int i = 0; i < 12; ++i) {
+        if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
+        else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
+        buf += lens[i];
+    }
+}
+static void res_save(Sol* s, double* buf, int dir) {
+    int nx = s->nx, N = s->N, M = s->M;
+    double* arrs[] = {s->rci, s->rcd, s->rct, s->rcq};
+    int lens[] = {XMAX, N * nx, CMAX, (N + 1) * M};
+    for (int i = 0; i < 4; ++i) {
+        if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
+        else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
+        buf += lens[i];
+    }
+}
+
+/* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
+ * seen, [4] = final mu, [5] = E_0 (scaled overall error) */
+int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                     const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
+                     int* iters_out, double* info) {
+    Sol sol, *s = &sol;
+    memset(s, 0, sizeof sol);
+    s->p = p;
+    s->m = m;
+    s->o = o;
+    s->nx = p->nx;
+    s->nu = p->nu;
+    s->ns = p->use_slack ? 1 : 0;
+    s->N = p->N;
+    s->M = knot_m(p);
+    s->sd = (p->shape == NLOT_SHAPE_POLYGON && p->use_slack) ? 1 : 0;
+    s->nc = 0;
+    for (int i = 0; i < p->nx; ++i) /* runner.py:51-56 */
+        if (p->enforce_heading || i != 2) s->tidx[s->nc++] = i;
+    memcpy(s->x0, x0, sizeof(double) * p->nx);
+    memcpy(s->xg, xg, sizeof(double) * p->nx);
+    if (sol_alloc(s)) return NLOT_NUMERIC;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    const double k1 = o->bound_push, k2 = o->bound_frac;
+    const int nsave = (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX;
+    const int nres = XMAX + N * nx + CMAX + (N + 1) * M;
+    int n_soc = 0;
+    double lin_resid = 0;
+    /* ---- initial point: LinearInitializer (trajectory_initialization.py:54-55), U = S = 0 ---- */
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < nx; ++i)
+            s->X[k * nx + i] = Xinit ? Xinit[k * nx + i] : x0[i] + (xg[i] - x0[i]) * ((double)k / (double)N);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            double lo = p->umin[i], hi = p->umax[i];
+            double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+            double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+            s->U[k * nu + i] = fmin(fmax(0.0, lo + pl), hi - pu);
+        }
+    for (int k = 0; k <= N; ++k) s->S[k] = s->ns ? fmax(0.0, k1) : 0.0;
+    for (int k = 0; k <= N; ++k) {
+        jet d[NLOT_MAX_BODY];
+        knot_ineq(p, m, s->X + k * nx, 0, d);
+        for (int j = 0; j < M; ++j) s->T[k * M + j] = fmax(d[j].v + (s->sd ? s->S[k] : 0.0), k1);
+    }
+    for (int i = 0; i < N * nu; ++i) s->zl[i] = s->zu[i] = 1.0;
+    for (int k = 0; k <= N; ++k) s->zs[k] = 1.0;
+    for (int i = 0; i < (N + 1) * M; ++i) s->vt[i] = 1.0;
+    s->mu = o->mu_init;
+    s->tau = fmax(0.99, 1.0 - s->mu);
+    /* ---- least-squares equality multipliers (IPOPT LeastSquareMultipliers) ---- */
+    eval_full(s);
+    build(s, MODE_LSQ, 0.0);
+    if (riccati(s, MODE_LSQ) == 0) {
+        double ymax = 0;
+        for (int k = 0; k <= N; ++k)
+            for (int j = 0; j < M; ++j) {
+                int q = k * M + j;
+                double w = 0;
+                for (int a = 0; a < 3 && a < nx; ++a) w += s->Jd[q * 3 + a] * s->dX[k * nx + a];
+                if (s->sd) w += s->dS[k];
+                s->yd[q] = w - s->vt[q];
+                ymax = fmax(ymax, fabs(s->yd[q]));
+            }
+        memcpy(s->yi, s->yi_n, sizeof(double) * nx);
+        memcpy(s->yk, s->yk_n, sizeof(double) * N * nx);
+        memcpy(s->yt, s->yt_n, sizeof(double) * s->nc);
+        for (int i = 0; i < nx; ++i) ymax = fmax(ymax, fabs(s->yi[i]));
+        for (int i = 0; i < N * nx; ++i) ymax = fmax(ymax, fabs(s->yk[i]));
+        for (int i = 0; i < s->nc; ++i) ymax = fmax(ymax, fabs(s->yt[i]));
+        if (ymax > o->constr_mult_init_max) {
+            memset(s->yi, 0, sizeof(double) * nx);
+            memset(s->yk, 0, sizeof(double) * N * nx);
+            memset(s->yt, 0, sizeof(double) * CMAX);
+            memset(s->yd, 0, sizeof(double) * (N + 1) * M);
+        }
+    }
+    {
+        double th0, ph0;
+        merit(s, s->X, s->U, s->S, s->T, s->mu, &th0, &ph0, NULL);
+        s->theta_max = 1e4 * fmax(1.0, th0);
+        s->theta_min = 1e-4 * fmax(1.0, th0);
+    }
+    s->nfilt = 0;
+    s->dw_last = 0;
+    int status = NLOT_MAXITER, iter = 0;
+    Errs e;
+    double* Xt = (double*)malloc(sizeof(double) * ((N + 1) * nx + N * nu + (N + 1) + (N + 1) * M));
+    double *Ut = Xt + (N + 1) * nx, *St = Ut + N * nu, *Tt = St + (N + 1);
+    for (;;) {
+        eval_full(s);
+        errors(s, &e);
+        double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
+        if (info) info[5] = E0;
+        if (!isfinite(E0)) {
+            status = NLOT_NUMERIC;
+            break;
+        }
+        if (E0 <= o->tol && e.dual <= o->dual_inf_tol && e.cviol <= o->constr_viol_tol &&
+            e.compl0 <= o->compl_inf_tol) {
+            status = NLOT_SOLVED;
+            break;
+        }
+        if (iter >= o->max_iter) {
+            status = NLOT_MAXITER;
+            break;
+        }
+        /* ---- monotone barrier update (IPOPT MonotoneMuUpdate, fast decrease allowed) ---- */
+        if (iter > 0) {
+            double kap = o->barrier_tol_factor;
+            for (;;) {
+                double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+                if (Emu > kap * s->mu) break;
+                double nm = fmin(0.2 * s->mu, pow(s->mu, 1.5));
+                nm = fmax(nm, fmin(o->tol, o->compl_inf_tol) / (kap + 1.0));
+                if (nm >= s->mu) break;
+                s->mu = nm;
+                s->tau = fmax(0.99, 1.0 - s->mu);
+                s->nfilt = 0;
+                errors(s, &e); /* complmu depends on mu */
+            }
+        }
+        /* ---- search direction with inertia correction ---- */
+        double dw = 0.0;
+        build(s, MODE_NEWTON, dw);
+        if (riccati(s, MODE_NEWTON)) {
+            dw = s->dw_last == 0.0 ? 1e-4 : fmax(1e-20, s->dw_last / 3.0);
+            for (;;) {
+                build(s, MODE_NEWTON, dw);
+                if (!riccati(s, MODE_NEWTON)) break;
+                dw *= (s->dw_last == 0.0) ? 100.0 : 8.0;
+                if (dw > 1e40) break;
+            }
+            if (dw > 1e40) {
+                status = NLOT_NUMERIC;
+                break;
+            }
+            s->dw_last = dw;
+        }
+        lin_resid = fmax(lin_resid, linear_residual(s, MODE_NEWTON));
+        recover(s, dw);
+        /* ---- step sizes: fraction to the boundary ---- */
+        double amax = 1.0, az = 1.0, tau = s->tau;
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i) {
+                int q = k * nu + i;
+                amax = frac_to_bound(s->U[q] - p->umin[i], s->dU[q], tau, amax);
+                amax = frac_to_bound(p->umax[i] - s->U[q], -s->dU[q], tau, amax);
+                az = frac_to_bound(s->zl[q], s->dzl[q], tau, az);
+                az = frac_to_bound(s->zu[q], s->dzu[q], tau, az);
+            }
+        if (s->ns)
+            for (int k = 0; k <= N; ++k) {
+                amax = frac_to_bound(s->S[k], s->dS[k], tau, amax);
+                az = frac_to_bound(s->zs[k], s->dzs[k], tau, az);
+            }
+        for (int q = 0; q < (N + 1) * M; ++q) {
+            amax = frac_to_bound(s->T[q], s->dT[q], tau, amax);
+            az = frac_to_bound(s->vt[q], s->dvt[q], tau, az);
+        }
+        /* ---- filter line search ---- */
+        double theta, phi;
+        merit(s, s->X, s->U, s->S, s->T, s->mu, &theta, &phi, NULL);
+        const double kappa_d = 1e-5, mu = s->mu;
+        double gd = 0; /* grad phi_mu . d */
+        for (int i = 0; i < (N + 1) * nx; ++i) gd += s->gX[i] * s->dX[i];
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i) {
+                int q = k * nu + i;
+                gd += (s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
+            }
+        if (s->ns)
+            for (int k = 0; k <= N; ++k) gd += (s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
+        for (int q = 0; q < (N + 1) * M; ++q) gd += (-mu / s->T[q] + kappa_d * mu) * s->dT[q];
+        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3;
+        double amin = gt;
+        if (gd < 0) {
+            amin = fmin(gt, gp * theta / (-gd));
+            if (theta <= s->theta_min) amin = fmin(amin, delta * pow(theta, sth) / pow(-gd, sph));
+        }
+        amin *= 0.05;
+        double alpha = amax;
+        int accepted = 0, armijo_ftype = 0, trials = 0;
+        double *rci_t = s->rci, *rcd_t = NULL, *rct_t = NULL, *rcq_t = NULL;
+        (void)rci_t;
+        double tri[XMAX], trt[CMAX];
+        double* trd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+        double* trq = trd + N * nx;
+        rcd_t = trd;
+        rct_t = trt;
+        rcq_t = trq;
+        for (;;) {
+            ++trials;
+            for (int i = 0; i < (N + 1) * nx; ++i) Xt[i] = s->X[i] + alpha * s->dX[i];
+            for (int i = 0; i < N * nu; ++i) Ut[i] = s->U[i] + alpha * s->dU[i];
+            for (int k = 0; k <= N; ++k) St[k] = s->S[k] + alpha * s->dS[k];
+            for (int q = 0; q < (N + 1) * M; ++q) Tt[q] = s->T[q] + alpha * s->dT[q];
+            double tht, pht;
+            merit_r(s, Xt, Ut, St, Tt, mu, &tht, &pht, tri, rcd_t, rct_t, rcq_t);
+            if (ls_accept(s, theta, phi, gd, alpha, tht, pht, &armijo_ftype)) {
+                accepted = 1;
+                break;
+            }
+            /* ---- second-order correction on the first trial (IPOPT max_soc = 4, kappa_soc = 0.99) ---- */
+            if (trials == 1 && o->max_soc > 0 && tht >= theta) {
+                int soc_ok = 0;
+                double* save = (double*)malloc(sizeof(double) * nsave);
+                step_save(s, save, 0);
+                /* c_soc = alpha_max c(x) + c(x + alpha_max d) */
+                double *ci = s->rci, *cd = s->rcd, *ct = s->rct, *cq = s->rcq;
+                double* c0 = (double*)malloc(sizeof(double) * nres);
+                res_save(s, c0, 0);
+                for (int i = 0; i < nx; ++i) ci[i] = alpha * ci[i] + tri[i];
+                for (int i = 0; i < N * nx; ++i) cd[i] = alpha * cd[i] + trd[i];
+                for (int i = 0; i < s->nc; ++i) ct[i] = alpha * ct[i] + trt[i];
+                for (int i = 0; i < (N + 1) * M; ++i) cq[i] = alpha * cq[i] + trq[i];
+                double th_old = tht, a_test = alpha;
+                for (int pcount = 0; pcount < o->max_soc; ++pcount) {
+                    build(s, MODE_NEWTON, dw);
+                    if (riccati(s, MODE_NEWTON)) break; /* same matrix: cannot fail, but be safe */
+                    recover(s, dw);
+                    double asoc = primal_frac(s, tau);
+                    for (int i = 0; i < (N + 1) * nx; ++i) Xt[i] = s->X[i] + asoc * s->dX[i];
+                    for (int i = 0; i < N * nu; ++i) Ut[i] = s->U[i] + asoc * s->dU[i];
+                    for (int k = 0; k <= N; ++k) St[k] = s->S[k] + asoc * s->dS[k];
+                    for (int q = 0; q < (N + 1) * M; ++q) Tt[q] = s->T[q] + asoc * s->dT[q];
+                    double ths, phs;
+                    merit_r(s, Xt, Ut, St, Tt, mu, &ths, &phs, tri, rcd_t, rct_t, rcq_t);
+                    if (ls_accept(s, theta, phi, gd, a_test, ths, phs, &armijo_ftype)) {
+                        soc_ok = 1;
+                        alpha = asoc;
+                        az = dual_frac(s, tau);
+                        break;
+                    }
+                    if (ths > 0.99 * th_old) break;
+                    th_old = ths;
+                    for (int i = 0; i < nx; ++i) ci[i] = asoc * ci[i] + tri[i];
+                    for (int i = 0; i < N * nx; ++i) cd[i] = asoc * cd[i] + trd[i];
+                    for (int i = 0; i < s->nc; ++i) ct[i] = asoc * ct[i] + trt[i];
+                    for (int i = 0; i < (N + 1) * M; ++i) cq[i] = asoc * cq[i] + trq[i];
+                }
+                res_save(s, c0, 1); /* restore the current residuals */
+                free(c0);
+                if (!soc_ok) step_save(s, save, 1);
+                free(save);
+                if (soc_ok) {
+                    accepted = 1;
+                    n_soc++;
+                    break;
+                }
+            }
+            alpha *= 0.5;
+            if (alpha < amin) break;
+        }
+        free(trd);
+        if (getenv("NLOT_VERBOSE"))
+            fprintf(stderr, "it %3d mu %.2e f %.6f th %.2e E0 %.2e dual %.2e dw %.1e amax %.2e a %.2e az %.2e tr %d nf %d soc %d\n", iter, mu,
+                    s->f, theta, E0, e.dual, dw, amax, alpha, az, trials, s->nfilt, n_soc);
+        if (!accepted) {
+            status = NLOT_LS_FAILED;
+            break;
+        }
+        if (!armijo_ftype) filter_add(s, theta, phi);
+        /* ---- accept trial point ---- */
+        memcpy(s->X, Xt, sizeof(double) * (N + 1) * nx);
+        memcpy(s->U, Ut, sizeof(double) * N * nu);
+        memcpy(s->S, St, sizeof(double) * (N + 1));
+        memcpy(s->T, Tt, sizeof(double) * (N + 1) * M);
+        for (int i = 0; i < nx; ++i) s->yi[i] += alpha * (s->yi_n[i] - s->yi[i]);
+        for (int i = 0; i < N * nx; ++i) s->yk[i] += alpha * (s->yk_n[i] - s->yk[i]);
+        for (int i = 0; i < s->nc; ++i) s->yt[i] += alpha * (s->yt_n[i] - s->yt[i]);
+        for (int i = 0; i < (N + 1) * M; ++i) s->yd[i] += alpha * (s->yd_n[i] - s->yd[i]);
+        const double ks = 1e10; /* kappa_Sigma bound-multiplier safeguard */
+#define ZUPD(z, dz, sl)                                                                          \
+    do {                                                                                         \
+        double zn = (z) + az * (dz), sv = (sl);                                                  \
+        zn = fmax(fmin(zn, ks * mu / sv), mu / (ks * sv));                                       \
+        (z) = zn;                                                                                \
+    } while (0)
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i) {
+                int q = k * nu + i;
+                ZUPD(s->zl[q], s->dzl[q], s->U[q] - p->umin[i]);
+                ZUPD(s->zu[q], s->dzu[q], p->umax[i] - s->U[q]);
+            }
+        if (s->ns)
+            for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k]);
+        for (int q = 0; q < (N + 1) * M; ++q) ZUPD(s->vt[q], s->dvt[q], s->T[q]);
+#undef ZUPD
+        ++iter;
+    }
+    free(Xt);
+    memcpy(Xout, s->X, sizeof(double) * (N + 1) * nx);
+    memcpy(Uout, s->U, sizeof(double) * N * nu);
+    if (Sout) memcpy(Sout, s->S, sizeof(double) * (N + 1));
+    *cost = objective(s, s->X, s->U, s->S);
+    *iters_out = iter;
+    if (info) {
+        info[0] = *cost;
+        info[1] = e.dual;
+        info[2] = e.cviol;
+        info[3] = lin_resid;
+        info[4] = s->mu;
+    }
+    free(s->arena);
+    return status;
+}
+
+/* Batch of B independent instances, OpenMP over instances (the CPU baseline). */
+int oracle_solve_batch(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                       const double* xg, const double* Xinit, double* X, double* U, double* S, double* cost,
+                       int* status, int* iters, long B, int nthreads) {
+    int nx = p->nx, nu = p->nu, N = p->N;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (long b = 0; b < B; ++b) {
+        status[b] = oracle_solve_one(p, o, m, x0 + b * nx, xg + b * nx, Xinit ? Xinit + b * (N + 1) * nx : NULL,
+                                     X + b * (N + 1) * nx, U + b * N * nu, S ? S + b * (N + 1) : NULL, cost + b,
+                                     iters + b, NULL);
+    }
+    (void)nthreads;
+    return 0;
+}
+
+void oracle_default_options(NlotSolverOptions* o) {
+    memset(o, 0, sizeof *o);
+    o->tol = 1e-4;
+    o->max_iter = 1000;
+    o->mu_strategy = 0;
+    o->mu_init = 0.1;
+    o->barrier_tol_factor = 10.0;
+    o->dual_inf_tol = 1.0;
+    o->constr_viol_tol = 1e-4;
+    o->compl_inf_tol = 1e-4;
+    o->constr_mult_init_max = 1e3;
+    o->bound_push = 1e-2;
+    o->bound_frac = 1e-2;
+    o->max_soc = 0; /* IPOPT default 4; 0 measured better here */
+}
+
+int oracle_sizeof_problem(void) { return (int)sizeof(NlotProblem); }
+int oracle_sizeof_options(void) { return (int)sizeof(NlotSolverOptions); }
+int oracle_sizeof_mlpdesc(void) { return (int)sizeof(NlotMlpDesc); }
