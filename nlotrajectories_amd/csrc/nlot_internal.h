@@ -1,0 +1,62 @@
+// Internal declarations shared by the HIP translation units of libnlot.so (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/nlot.h"
+
+namespace nlot {
+
+// thread-local last error (nlot_last_error)
+void set_error(const std::string& msg);
+
+#define NLOT_HIP_CHECK(expr)                                                                        \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            ::nlot::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+            return NLOT_ERR_HIP;                                                                   \
+        }                                                                                          \
+    } while (0)
+
+// Device-resident learned-SDF weights (opaque NlotMlp of the ABI).
+struct MlpDev {
+    int in_kind;     // NLOT_MLP_IN_*
+    int H;           // hidden width
+    int n_hidden;    // HxH layers
+    float scale;     // fourier scale
+    float b_out;
+    const float* A;     // [2][H]
+    const float* b0;    // [H]
+    const float* W;     // [n_hidden][H][H] (out, in)
+    const float* b;     // [n_hidden][H]
+    const float* w_out; // [H]
+};
+
+// Output addressing of the MLP kernel: element q of point i goes to ptr_q[i * stride_q].
+struct MlpOut {
+    float* val;
+    float* gx;
+    float* gy;
+    float* hxx;
+    float* hxy;
+    float* hyx;  // may alias hxy (SoA) or be the [1][0] slot of an AoS 2x2
+    float* hyy;
+    int sv, sg, sh;
+};
+
+// Launch the MFMA SDF-MLP kernel on cnt * P_per points, cnt = *n_dev if n_dev else n (n = upper bound
+// that sizes the persistent grid).  Point g lives at (g % cnt) + (g / cnt) * ld of pts/lam/out.
+// full = value + lam*grad + lam*hess; else value only.
+int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                       const float* lam, const MlpOut& out, bool full, hipStream_t stream);
+
+}  // namespace nlot
+
+struct NlotMlp {
+    nlot::MlpDev dev;
+    void* block;  // single device allocation holding all arrays
+};

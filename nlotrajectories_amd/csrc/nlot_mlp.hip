@@ -1,0 +1,385 @@
+// Batched learned-SDF MLP: value, lambda*gradient and lambda*Hessian at P points (gfx950).
+//
+// Replaces the per-point CasADi externals nn_sdf / jac_nn_sdf / adj1_nn_sdf / jac_adj1_nn_sdf
+// (/root/reference/_l4c_generated/nn_sdf.cpp:57-104), whose TorchScript graphs evaluate
+//   f(p) = w_out . relu(W_l ... relu(W_0 h0 + b_0) ...) + b_out,   h0 = scale*cos(p A + b0)  (FourierMLP,
+//   core/nn_architectures.py:30-72)  or  h0 = relu(p A + b0)  (l4casadi naive MLP)
+// in fp32, one 1x2 point per call.  Here one launch evaluates every corner of every knot of every
+// active problem.
+//
+// Mapping (MI355X, wave64, f32-input MFMA v_mfma_f32_32x32x2_f32 = exact k-ordered fp32 FMA chain):
+//   * a wave owns 32 points; a 256-thread block owns 128 points per tile and loops over tiles
+//     (persistent grid: the weights are staged into LDS once per block);
+//   * forward GEMM:  Z^T[hidden j][point i] = W[j][:] . h[:][i]  — A operand = W from LDS
+//     (row stride H+1 floats: the 32 rows a ds_read_b32 touches land in 32 distinct banks),
+//     B operand = the hidden activations of the point held by the lane;  the input layer h0 is
+//     computed on the fly per k-step (1 cos per lane per MFMA k-step, hidden under the MFMA);
+//   * the accumulator layout (hidden unit in registers, point in lanes) is exactly the B-operand
+//     layout of the next product, so every further hidden layer and the whole reverse sweep
+//     (G^T = W^T (lam*w_out .* mask)) chain register-to-register with no LDS transpose;
+//   * the gradient / Hessian w.r.t. the 2-D input are contractions over the hidden units of the
+//     input layer: per-lane partial sums + one cross-half shuffle.  For a Fourier input layer
+//     lam*d2f/dp2 = A diag(g .* (-scale cos z)) A^T (g = df/dh0), for a ReLU input layer it is 0.
+#include <hip/hip_runtime.h>
+
+#include "nlot_internal.h"
+
+namespace nlot {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxResidentLayers = 2;
+
+// row index (hidden unit) held by register r of a 32x32 accumulator on lane-half hl
+__device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
+
+template <int H, int L, bool FULL>
+// Point g of the launch lives at address (g % cnt) + (g / cnt) * ld of pts / lam / out: a [P_per][ld] list
+// whose first `cnt` columns are valid (cnt = *cnt_dev when given: the solver's compacted instances).
+__global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+                                                      const int* __restrict__ cnt_dev, int P_per, int64_t ld,
+                                                      const float* __restrict__ lam, MlpOut out) {
+    constexpr int HP = H + 1;   // padded LDS row
+    constexpr int NT = H / 32;  // 32x32 tiles along the hidden dimension
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sW = smem;                                   // [L][H][HP]
+    float* sA0 = sW + (size_t)L * H * HP;               // [H]
+    float* sA1 = sA0 + H;                               // [H]
+    float* sb0 = sA1 + H;                               // [H]
+    float* sb = sb0 + H;                                // [L][H]
+    float* sw = sb + L * H;                             // [H]
+
+    for (int idx = threadIdx.x; idx < L * H * H; idx += blockDim.x) {
+        int l = idx / (H * H), rem = idx - l * H * H, j = rem / H, k = rem - j * H;
+        sW[(size_t)l * H * HP + j * HP + k] = w.W[idx];
+    }
+    for (int idx = threadIdx.x; idx < H; idx += blockDim.x) {
+        sA0[idx] = w.A[idx];
+        sA1[idx] = w.A[H + idx];
+        sb0[idx] = w.b0[idx];
+        sw[idx] = w.w_out[idx];
+    }
+    for (int idx = threadIdx.x; idx < L * H; idx += blockDim.x) sb[idx] = w.b[idx];
+    __syncthreads();
+
+    const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
+    const int64_t npts = cnt * P_per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int il = lane & 31, hl = lane >> 5;
+    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
+    const float scale = w.scale;
+
+    for (int64_t tile = blockIdx.x; tile * 128 < npts; tile += gridDim.x) {
+        const int64_t gi = tile * 128 + wave * 32 + il;
+        const bool valid = gi < npts;
+        const int64_t pi = valid ? (gi % cnt) + (gi / cnt) * ld : 0;
+        float px = 0.f, py = 0.f;
+        if (valid) {
+            px = pts[2 * pi];
+            py = pts[2 * pi + 1];
+        }
+        // ---------------- input layer + first hidden GEMM ----------------
+        f32x16 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll 4
+        for (int s = 0; s < H / 2; ++s) {
+            const int k = 2 * s + hl;
+            const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
+            const float h0 = fourier ? cosf(z) * scale : (z > 0.f ? z : 0.f);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float a = sW[(t * 32 + il) * HP + k];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, h0, acc[t], 0, 0, 0);
+            }
+        }
+        uint64_t mask[L];
+        // bias + ReLU of layer 0
+        {
+            uint64_t m = 0;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[t][r] + sb[t * 32 + acc_row(r, hl)];
+                    const bool on = v > 0.f;
+                    acc[t][r] = on ? v : 0.f;
+                    m |= (uint64_t)on << (t * 16 + r);
+                }
+            mask[0] = m;
+        }
+        // ---------------- further hidden layers (register-chained) ----------------
+#pragma unroll
+        for (int l = 1; l < L; ++l) {
+            const float* Wl = sW + (size_t)l * H * HP;
+            f32x16 nacc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) nacc[t] = f32x16{};
+#pragma unroll
+            for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int kk = ti * 32 + acc_row(r, hl);
+                    const float bv = acc[ti][r];
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        const float a = Wl[(t * 32 + il) * HP + kk];
+                        nacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, nacc[t], 0, 0, 0);
+                    }
+                }
+            uint64_t m = 0;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = nacc[t][r] + sb[l * H + t * 32 + acc_row(r, hl)];
+                    const bool on = v > 0.f;
+                    acc[t][r] = on ? v : 0.f;
+                    m |= (uint64_t)on << (t * 16 + r);
+                }
+            mask[l] = m;
+        }
+        // ---------------- output layer ----------------
+        float fpart = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) fpart = fmaf(sw[t * 32 + acc_row(r, hl)], acc[t][r], fpart);
+        const float f = fpart + __shfl_xor(fpart, 32) + w.b_out;
+
+        if constexpr (!FULL) {
+            if (valid && hl == 0) out.val[pi * out.sv] = f;
+            continue;
+        } else {
+            // ---------------- reverse sweep ----------------
+            const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
+            // e = lam * w_out .* mask_top  (in place, accumulator layout)
+            {
+                const uint64_t m = mask[L - 1];
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        acc[t][r] = ((m >> (t * 16 + r)) & 1) ? lm * sw[t * 32 + acc_row(r, hl)] : 0.f;
+            }
+#pragma unroll
+            for (int l = L - 1; l >= 0; --l) {
+                const float* Wl = sW + (size_t)l * H * HP;
+                f32x16 g[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) g[t] = f32x16{};
+#pragma unroll
+                for (int tj = 0; tj < NT; ++tj)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int jj = tj * 32 + acc_row(r, hl);
+                        const float bv = acc[tj][r];
+#pragma unroll
+                        for (int t = 0; t < NT; ++t) {
+                            const float a = Wl[jj * HP + t * 32 + il];
+                            g[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, g[t], 0, 0, 0);
+                        }
+                    }
+                if (l > 0) {
+                    const uint64_t m = mask[l - 1];
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[t][r] = ((m >> (t * 16 + r)) & 1) ? g[t][r] : 0.f;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) acc[t] = g[t];
+                }
+            }
+            // acc = df/dh0 (x lam); contract with the input layer's derivatives
+            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = t * 32 + acc_row(r, hl);
+                    const float ax = sA0[k], ay = sA1[k];
+                    const float z = fmaf(py, ay, px * ax) + sb0[k];
+                    const float d = acc[t][r];
+                    float dz, c2;
+                    if (fourier) {
+                        float sn, cs;
+                        sincosf(z, &sn, &cs);
+                        dz = d * (-scale * sn);
+                        c2 = d * (-scale * cs);
+                    } else {
+                        dz = z > 0.f ? d : 0.f;
+                        c2 = 0.f;
+                    }
+                    gx = fmaf(ax, dz, gx);
+                    gy = fmaf(ay, dz, gy);
+                    hxx = fmaf(ax * ax, c2, hxx);
+                    hxy = fmaf(ax * ay, c2, hxy);
+                    hyy = fmaf(ay * ay, c2, hyy);
+                }
+            gx += __shfl_xor(gx, 32);
+            gy += __shfl_xor(gy, 32);
+            hxx += __shfl_xor(hxx, 32);
+            hxy += __shfl_xor(hxy, 32);
+            hyy += __shfl_xor(hyy, 32);
+            if (valid && hl == 0) {
+                out.val[pi * out.sv] = f;
+                if (out.gx) {
+                    out.gx[pi * out.sg] = gx;
+                    out.gy[pi * out.sg] = gy;
+                }
+                if (out.hxx) {
+                    out.hxx[pi * out.sh] = hxx;
+                    out.hxy[pi * out.sh] = hxy;
+                    if (out.hyx != out.hxy) out.hyx[pi * out.sh] = hxy;
+                    out.hyy[pi * out.sh] = hyy;
+                }
+            }
+        }
+    }
+}
+
+static int g_num_cus = 0;
+
+static int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+        g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    }
+    return g_num_cus;
+}
+
+template <int H, int L, bool FULL>
+static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                    const float* lam, const MlpOut& out, hipStream_t stream) {
+    const size_t lds = sizeof(float) * ((size_t)w.n_hidden * H * (H + 1) + 4 * H + (size_t)w.n_hidden * H);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_kernel<H, L, FULL>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    int64_t tiles = (n * P_per + 127) / 128;
+    // resident blocks per CU: VGPR-limited (FULL: 1 wave/SIMD) and LDS-limited
+    int64_t cap = (int64_t)num_cus() * ((!FULL && L == 1 && lds <= 80 * 1024) ? 2 : 1);
+    int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
+    hipLaunchKernelGGL((mlp_kernel<H, L, FULL>), dim3(grid), dim3(256), lds, stream, w, pts, n, n_dev, P_per, ld, lam, out);
+    NLOT_HIP_CHECK(hipGetLastError());
+    return NLOT_OK;
+}
+
+int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                       const float* lam, const MlpOut& out, bool full, hipStream_t stream) {
+    if (n <= 0) return NLOT_OK;
+    if (w.n_hidden < 1 || w.n_hidden > kMaxResidentLayers) {
+        set_error("MLP kernel: 1 or 2 hidden HxH layers are supported (DESIGN.md §7)");
+        return NLOT_ERR_INVALID;
+    }
+#define NLOT_MLP_CASE(HH, LL)                                                                      \
+    if (w.H == HH && w.n_hidden == LL)                                                             \
+        return full ? launch_t<HH, LL, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream)        \
+                    : launch_t<HH, LL, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+    NLOT_MLP_CASE(64, 1)
+    NLOT_MLP_CASE(64, 2)
+    NLOT_MLP_CASE(128, 1)
+    NLOT_MLP_CASE(128, 2)
+#undef NLOT_MLP_CASE
+    {
+        set_error("MLP kernel: hidden width must be 64 or 128 (DESIGN.md §7)");
+        return NLOT_ERR_INVALID;
+    }
+}
+
+}  // namespace nlot
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
+    using namespace nlot;
+    if (!d || !d->A || !d->b0 || !d->w_out || (d->n_hidden > 0 && (!d->W || !d->b))) {
+        set_error("nlot_mlp_create: null descriptor or weight pointer");
+        return nullptr;
+    }
+    if (d->act != 0 || (d->in_kind != NLOT_MLP_IN_FOURIER && d->in_kind != NLOT_MLP_IN_LINEAR_RELU)) {
+        set_error("nlot_mlp_create: only ReLU hidden layers with a Fourier or Linear+ReLU input layer");
+        return nullptr;
+    }
+    if ((d->hidden != 64 && d->hidden != 128) || d->n_hidden < 1 || d->n_hidden > kMaxResidentLayers) {
+        set_error("nlot_mlp_create: hidden width 64/128 with 1-2 hidden layers supported (DESIGN.md §7)");
+        return nullptr;
+    }
+    const int H = d->hidden, L = d->n_hidden;
+    const size_t nA = 2 * H, nb0 = H, nW = (size_t)L * H * H, nb = (size_t)L * H, nw = H;
+    const size_t total = nA + nb0 + nW + nb + nw;
+    float* blk = nullptr;
+    if (hipMalloc(&blk, total * sizeof(float)) != hipSuccess) {
+        set_error("nlot_mlp_create: hipMalloc failed");
+        return nullptr;
+    }
+    float* p = blk;
+    auto put = [&](const float* src, size_t cnt) -> float* {
+        float* dst = p;
+        hipMemcpy(dst, src, cnt * sizeof(float), hipMemcpyHostToDevice);
+        p += cnt;
+        return dst;
+    };
+    NlotMlp* m = new NlotMlp;
+    m->block = blk;
+    m->dev.in_kind = d->in_kind;
+    m->dev.H = H;
+    m->dev.n_hidden = L;
+    m->dev.scale = d->fourier_scale;
+    m->dev.b_out = d->b_out;
+    m->dev.A = put(d->A, nA);
+    m->dev.b0 = put(d->b0, nb0);
+    m->dev.W = put(d->W, nW);
+    m->dev.b = put(d->b, nb);
+    m->dev.w_out = put(d->w_out, nw);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        set_error("nlot_mlp_create: copy failed");
+        hipFree(blk);
+        delete m;
+        return nullptr;
+    }
+    return m;
+}
+
+extern "C" void nlot_mlp_destroy(NlotMlp* m) {
+    if (!m) return;
+    hipFree(m->block);
+    delete m;
+}
+
+extern "C" int32_t nlot_sdf_mlp_eval(const NlotMlp* mlp, const float* pts, int64_t P, float* val, float* grad,
+                                     const float* lam, float* hess, void* stream) {
+    using namespace nlot;
+    if (!mlp || !pts || !val || P < 0) {
+        set_error("nlot_sdf_mlp_eval: null argument");
+        return NLOT_ERR_INVALID;
+    }
+    MlpOut o{};
+    o.val = val;
+    o.sv = 1;
+    if (grad) {
+        o.gx = grad;
+        o.gy = grad + 1;
+        o.sg = 2;
+    }
+    if (hess) {
+        o.hxx = hess;
+        o.hxy = hess + 1;
+        o.hyx = hess + 2;
+        o.hyy = hess + 3;
+        o.sh = 4;
+    }
+    const bool full = grad || hess;
+    if (full && !grad) {  // kernel writes grad and hess together: route grad to a scratch-free path
+        set_error("nlot_sdf_mlp_eval: hess requires grad (jac_adj1 is evaluated with adj1)");
+        return NLOT_ERR_INVALID;
+    }
+    return launch_mlp_strided(mlp->dev, pts, P, nullptr, 1, P, lam, o, full, (hipStream_t)stream);
+}

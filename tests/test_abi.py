@@ -1,0 +1,56 @@
+"""The C-ABI library loads, exports exactly what include/nlot.h declares, and the ctypes struct
+layouts agree with the C compiler's (checked through the oracle, which includes the same header)."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "nlot.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", src))
+    return {n for n in names if n not in {"if", "return", "sizeof"}}
+
+
+def test_header_lists_all_symbols():
+    from nlotrajectories_amd._lib import EXPORTED
+
+    assert header_functions() == set(EXPORTED)
+
+
+def test_library_exports_every_symbol():
+    import ctypes as C
+
+    from nlotrajectories_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    L = C.CDLL(_lib.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(L, name), name
+    assert _lib.lib().nlot_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    import ctypes as C
+
+    import oracle as O
+    from nlotrajectories_amd import _abi
+
+    L = O.lib()
+    assert L.oracle_sizeof_problem() == C.sizeof(_abi.NlotProblem)
+    assert L.oracle_sizeof_options() == C.sizeof(_abi.NlotSolverOptions)
+    assert L.oracle_sizeof_mlpdesc() == C.sizeof(_abi.NlotMlpDesc)
+
+
+def test_default_options_agree():
+    import ctypes as C
+
+    from nlotrajectories_amd import _abi, _lib
+
+    o = _abi.NlotSolverOptions()
+    _lib.lib().nlot_default_options(C.byref(o))
+    d = _abi.default_options()
+    for k, _ in o._fields_:
+        assert getattr(o, k) == getattr(d, k), k

@@ -1,0 +1,69 @@
+"""GPU parity of the batched SDF-MLP kernel (nn_sdf / jac_nn_sdf / adj1_nn_sdf / jac_adj1_nn_sdf)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dmlp(artefact):
+    from nlotrajectories_amd.ops import DeviceMlp
+
+    return DeviceMlp(artefact)
+
+
+def test_mlp_matches_reference_golden(dmlp, golden):
+    """Against the reference module's fp32 autograd values (tests/golden/make_golden.py)."""
+    from nlotrajectories_amd.ops import sdf_mlp_eval
+
+    p = torch.tensor(golden["p"], device="cuda")
+    lam = torch.tensor(golden["lam"], device="cuda")
+    v, g, h = sdf_mlp_eval(dmlp, p)
+    _, ga, ha = sdf_mlp_eval(dmlp, p, lam=lam)
+    v, g, h, ga, ha = (t.cpu().numpy() for t in (v, g, h, ga, ha))
+    f64 = golden["f_f64"]
+    # fp32 forward of a 2-128-128-1 net with |W| sums ~ 1e2: absolute tolerance 2e-5 on f (|f| <~ 2)
+    np.testing.assert_allclose(v, f64, atol=2e-5, rtol=0)
+    gs = np.abs(golden["grad_f64"]).max()
+    np.testing.assert_allclose(g, golden["grad_f64"], atol=2e-5 * max(gs, 1), rtol=0)
+    np.testing.assert_allclose(ga, golden["adj1_f64"], atol=5e-5 * max(gs, 1), rtol=0)
+    hs = np.abs(golden["jac_adj1_f64"]).max()
+    np.testing.assert_allclose(ha, golden["jac_adj1_f64"], atol=2e-5 * hs, rtol=0)
+    np.testing.assert_allclose(h[:, 0, 1], h[:, 1, 0])
+
+
+def test_mlp_matches_oracle_and_value_path(dmlp, artefact):
+    import oracle as O
+    from nlotrajectories_amd.ops import sdf_mlp_eval
+
+    rng = np.random.default_rng(3)
+    for P in (1, 31, 32, 33, 127, 128, 129, 4097):
+        pts = rng.uniform(-0.6, 1.6, size=(P, 2)).astype(np.float32)
+        lam = rng.uniform(-1, 1, size=P).astype(np.float32)
+        hm = O.HostMlp(artefact)
+        ov, og, oh = O.mlp_eval(hm, pts, lam)
+        t = torch.tensor(pts, device="cuda")
+        v, g, h = (x.cpu().numpy() for x in sdf_mlp_eval(dmlp, t, lam=torch.tensor(lam, device="cuda")))
+        vv, _, _ = sdf_mlp_eval(dmlp, t, derivatives=False)
+        np.testing.assert_allclose(v, ov, atol=1e-5)
+        np.testing.assert_array_equal(vv.cpu().numpy(), v)  # value-only kernel == full kernel's value
+        np.testing.assert_allclose(g, og, atol=5e-5 * max(1, np.abs(og).max()))
+        np.testing.assert_allclose(h, oh, atol=5e-5 * max(1, np.abs(oh).max()))
+
+
+def test_mlp_relu_two_layer_vs_torch():
+    """l4casadi naive MLP (ReLU input layer, 2 hidden layers): value & grad vs torch fp64; hess = 0."""
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    w = MlpWeights.random_relu_mlp(hidden=64, n_hidden=2, seed=1)
+    m = w.torch_module().double()
+    pts = torch.rand(1000, 2, dtype=torch.float64) * 2 - 0.5
+    pts.requires_grad_(True)
+    f = m(pts)[:, 0]
+    (g,) = torch.autograd.grad(f.sum(), pts)
+    v, gg, hh = sdf_mlp_eval(DeviceMlp(w), pts.detach().float().cuda())
+    np.testing.assert_allclose(v.cpu().numpy(), f.detach().numpy(), atol=1e-4 * max(1, f.abs().max().item()))
+    np.testing.assert_allclose(gg.cpu().numpy(), g.numpy(), atol=1e-4 * max(1, g.abs().max().item()))
+    assert float(hh.abs().max()) == 0.0

@@ -1,0 +1,66 @@
+"""CPU oracle solver: converges on the restated benchmarks; Newton steps solve the full KKT system."""
+import numpy as np
+import pytest
+
+
+def test_b2_converges_in_trust_constr_basin():
+    """benchmark_2 from the linear initial guess: the restated IPOPT converges (tol 1e-4) to the basin the
+    survey's independent scipy trust-constr solve found (cost 1.656058 at KKT 6.9e-9)."""
+    import oracle as O
+    from nlotrajectories_amd.problem import BENCHMARKS
+
+    b = BENCHMARKS["b2"]
+    r = O.solve_one(b["problem"], b["start"], b["goal"])
+    assert r["status"] == 0
+    assert abs(r["cost"] - 1.656058) < 2e-3
+    assert r["constr_viol"] < 1e-4 and r["dual_inf"] < 1e-3
+    assert r["lin_resid"] < 1e-6  # Riccati step satisfies the unsubstituted KKT system
+
+
+def test_b2_tight_tolerance_reaches_trust_constr_cost():
+    import oracle as O
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.problem import BENCHMARKS
+
+    b = BENCHMARKS["b2"]
+    r = O.solve_one(b["problem"], b["start"], b["goal"], opt=_abi.default_options(tol=1e-8, constr_viol_tol=1e-8,
+                                                                                  compl_inf_tol=1e-8))
+    assert r["status"] == 0
+    assert abs(r["cost"] - 1.656058) < 5e-5
+
+
+def test_b3_analytic_and_batch_equals_single():
+    import oracle as O
+    from nlotrajectories_amd.problem import BENCHMARKS
+
+    b = BENCHMARKS["b3"]
+    r = O.solve_one(b["problem"], b["start"], b["goal"])
+    assert r["status"] == 0
+    rb = O.solve_batch(b["problem"], np.array([b["start"]] * 3), np.array([b["goal"]] * 3), threads=2)
+    assert (rb["status"] == 0).all()
+    np.testing.assert_array_equal(rb["cost"], r["cost"])
+    np.testing.assert_array_equal(rb["X"][1], r["X"])
+
+
+def test_metric_learned_sdf_instance(artefact):
+    import oracle as O
+    from nlotrajectories_amd.problem import METRIC_PROBLEM
+
+    r = O.solve_one(METRIC_PROBLEM, [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0], O.HostMlp(artefact))
+    assert r["status"] == 0
+    assert r["constr_viol"] < 1e-4
+    assert r["lin_resid"] < 1e-6
+
+
+def test_status_for_invalid_derivative_start():
+    """benchmark_1's straight line passes through the circle centre where the reference's sqrt SDF has no
+    derivative: IPOPT stops with an invalid-number error; the restatement reports NUMERIC."""
+    import oracle as O
+    from nlotrajectories_amd.problem import BENCHMARKS
+
+    b = BENCHMARKS["b1"]
+    r = O.solve_one(b["problem"], b["start"], b["goal"])
+    assert r["status"] == 3
+    # off-centre start converges
+    r = O.solve_one(b["problem"], [0.0, 0.2, 0, 0], [1.0, 0.9, 0, 0])
+    assert r["status"] == 0
