@@ -89,7 +89,8 @@ def main():
         step()
     set_timing(True)
     agg = dict(mlp_full_ms=0.0, mlp_full_launches=0, mlp_points_full=0, mlp_value_ms=0.0,
-               mlp_value_launches=0, mlp_points_value=0, iterations=0)
+               mlp_value_launches=0, mlp_points_value=0, iterations=0, iterate_ms=0.0)
+    slots_in_lds = None
     iters_all, solved_total = [], 0
     if world > 1:
         dist.barrier()
@@ -101,6 +102,7 @@ def main():
         st = last_stats()
         for k in agg:
             agg[k] += st[k]
+        slots_in_lds = bool(st["slots_in_lds"])
         iters_all.append(r["iters"][r["status"] == 0].float().mean().item() if ns else 0.0)
     torch.cuda.synchronize()
     if world > 1:
@@ -160,6 +162,9 @@ def main():
                 "status_counts_rank0": status_counts,
                 "mean_iters_solved": float(np.mean(iters_all)),
                 "lockstep_global_steps": agg["iterations"] // max(a.steps, 1),
+                "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
+                "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) / max(a.steps, 1),
+                "riccati_slots": "lds" if slots_in_lds else "hbm",
             },
             "roofline": {
                 "kernel": "mlp_kernel<128,1,full> (SDF-MLP value+grad+Hessian, v_mfma_f32_32x32x2_f32)",

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 1
+#define NLOT_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -198,6 +198,9 @@ typedef struct NlotSolveStats {
     double mlp_value_ms;       /* summed device time of the value-only MLP launches */
     int32_t mlp_full_launches;
     int32_t mlp_value_launches;
+    double iterate_ms;         /* summed device time of the solver-step (k_iterate) launches */
+    int32_t slots_in_lds;      /* 1: Riccati stage slots held in LDS, 0: in the HBM workspace */
+    int32_t pad_;
 } NlotSolveStats;
 /* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
 void nlot_set_timing(int32_t enabled);

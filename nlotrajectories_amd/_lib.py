@@ -12,7 +12,8 @@ import subprocess
 from . import _abi
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libnlot.so")
+# NLOT_LIB selects an alternative in-tree build (e.g. the phase-timer build libnlot_prof.so)
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("NLOT_LIB", "libnlot.so"))
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 # symbols include/nlot.h declares (checked by tests/test_abi.py)
@@ -69,7 +70,7 @@ def lib():
     L.nlot_last_stats.argtypes = [C.POINTER(_abi.NlotSolveStats)]
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 1:
+    if L.nlot_abi_version() != 2:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

@@ -17,41 +17,41 @@ template <int DYN> struct Dyn;
 
 template <> struct Dyn<NLOT_POINT_1ST> {  // dynamics.py:33-41  f = (u0, u1, 0, 0)
     static constexpr int NX = 4, NU = 2;
-    __device__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
         o[0] = u[0]; o[1] = u[1]; o[2] = 0; o[3] = 0; (void)x;
     }
-    __device__ static void jac(const double* x, const double* u, double dt, double, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double* x, const double* u, double dt, double, double (*A)[NX], double (*B)[NU]) {
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
         B[0][0] = dt; B[1][1] = dt; (void)x; (void)u;
     }
-    __device__ static void hess(const double*, const double*, const double*, double, double, double (*)[NX + NU]) {}
+    __device__ __forceinline__ static void hess(const double*, const double*, const double*, double, double, double (*)[NX + NU]) {}
 };
 
 template <> struct Dyn<NLOT_POINT_2ND> {  // dynamics.py:44-56  f = (vx, vy, ax, ay)
     static constexpr int NX = 4, NU = 2;
-    __device__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
         o[0] = x[2]; o[1] = x[3]; o[2] = u[0]; o[3] = u[1];
     }
-    __device__ static void jac(const double*, const double*, double dt, double, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double*, const double*, double dt, double, double (*A)[NX], double (*B)[NU]) {
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
         A[0][2] = dt; A[1][3] = dt; B[2][0] = dt; B[3][1] = dt;
     }
-    __device__ static void hess(const double*, const double*, const double*, double, double, double (*)[NX + NU]) {}
+    __device__ __forceinline__ static void hess(const double*, const double*, const double*, double, double, double (*)[NX + NU]) {}
 };
 
 template <> struct Dyn<NLOT_UNICYCLE> {  // dynamics.py:59-73  f = (v c, v s, w), u = (v, w)
     static constexpr int NX = 3, NU = 2;
-    __device__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = u[0] * c; o[1] = u[0] * s; o[2] = u[1];
     }
-    __device__ static void jac(const double* x, const double* u, double dt, double, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double* x, const double* u, double dt, double, double (*A)[NX], double (*B)[NU]) {
         double s, c; sincos(x[2], &s, &c);
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
         A[0][2] = -dt * u[0] * s; A[1][2] = dt * u[0] * c;
         B[0][0] = dt * c; B[1][0] = dt * s; B[2][1] = dt;
     }
-    __device__ static void hess(const double* x, const double* u, const double* l, double dt, double, double (*H)[NX + NU]) {
+    __device__ __forceinline__ static void hess(const double* x, const double* u, const double* l, double dt, double, double (*H)[NX + NU]) {
         double s, c; sincos(x[2], &s, &c);
         H[2][2] += dt * (-l[0] * u[0] * c - l[1] * u[0] * s);
         double t = dt * (-l[0] * s + l[1] * c);
@@ -61,11 +61,11 @@ template <> struct Dyn<NLOT_UNICYCLE> {  // dynamics.py:59-73  f = (v c, v s, w)
 
 template <> struct Dyn<NLOT_UNICYCLE_2ND> {  // dynamics.py:76-96  f = (v c, v s, w, a, alpha)
     static constexpr int NX = 5, NU = 2;
-    __device__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = x[3] * c; o[1] = x[3] * s; o[2] = x[4]; o[3] = u[0]; o[4] = u[1];
     }
-    __device__ static void jac(const double* x, const double*, double dt, double, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double* x, const double*, double dt, double, double (*A)[NX], double (*B)[NU]) {
         double s, c; sincos(x[2], &s, &c);
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
         A[0][2] = -dt * x[3] * s; A[0][3] = dt * c;
@@ -73,7 +73,7 @@ template <> struct Dyn<NLOT_UNICYCLE_2ND> {  // dynamics.py:76-96  f = (v c, v s
         A[2][4] = dt;
         B[3][0] = dt; B[4][1] = dt;
     }
-    __device__ static void hess(const double* x, const double*, const double* l, double dt, double, double (*H)[NX + NU]) {
+    __device__ __forceinline__ static void hess(const double* x, const double*, const double* l, double dt, double, double (*H)[NX + NU]) {
         double s, c; sincos(x[2], &s, &c);
         H[2][2] += dt * (-l[0] * x[3] * c - l[1] * x[3] * s);
         double t = dt * (-l[0] * s + l[1] * c);
@@ -83,18 +83,18 @@ template <> struct Dyn<NLOT_UNICYCLE_2ND> {  // dynamics.py:76-96  f = (v c, v s
 
 template <> struct Dyn<NLOT_ACKERMANN> {  // dynamics.py:99-118  f = (v c, v s, v tan(psi)/L, psidot)
     static constexpr int NX = 4, NU = 2;
-    __device__ static void f(const double* x, const double* u, double L, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = u[0] * c; o[1] = u[0] * s; o[2] = u[0] * tan(x[3]) / L; o[3] = u[1];
     }
-    __device__ static void jac(const double* x, const double* u, double dt, double L, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double* x, const double* u, double dt, double L, double (*A)[NX], double (*B)[NU]) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), sec2 = 1 + tp * tp;
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
         A[0][2] = -dt * u[0] * s; A[1][2] = dt * u[0] * c; A[2][3] = dt * u[0] * sec2 / L;
         B[0][0] = dt * c; B[1][0] = dt * s; B[2][0] = dt * tp / L; B[3][1] = dt;
     }
-    __device__ static void hess(const double* x, const double* u, const double* l, double dt, double L, double (*H)[NX + NU]) {
+    __device__ __forceinline__ static void hess(const double* x, const double* u, const double* l, double dt, double L, double (*H)[NX + NU]) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), sec2 = 1 + tp * tp;
         H[2][2] += dt * (-l[0] * u[0] * c - l[1] * u[0] * s);
@@ -108,14 +108,14 @@ template <> struct Dyn<NLOT_ACKERMANN> {  // dynamics.py:99-118  f = (v c, v s, 
 
 template <> struct Dyn<NLOT_ACKERMANN_2ND> {  // dynamics.py:121-148, output order reproduced as written
     static constexpr int NX = 7, NU = 2;
-    __device__ static void f(const double* x, const double* u, double L, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), q = 1 + x[3] * x[3];
         o[0] = x[4] * c; o[1] = x[4] * s; o[2] = x[4] * tp / L; o[3] = x[6];
         o[4] = (x[6] / q * x[4] + tp * u[0]) / L;  // "domega" lands in the v slot (bug F7a kept)
         o[5] = u[0]; o[6] = u[1];
     }
-    __device__ static void jac(const double* x, const double* u, double dt, double L, double (*A)[NX], double (*B)[NU]) {
+    __device__ __forceinline__ static void jac(const double* x, const double* u, double dt, double L, double (*A)[NX], double (*B)[NU]) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), sec2 = 1 + tp * tp, q = 1 + x[3] * x[3], dq = -2 * x[3] / (q * q);
         for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) A[i][j] = i == j; B[i][0] = B[i][1] = 0; }
@@ -128,7 +128,7 @@ template <> struct Dyn<NLOT_ACKERMANN_2ND> {  // dynamics.py:121-148, output ord
         A[4][6] = dt * x[4] / q / L;
         B[4][0] = dt * tp / L; B[5][0] = dt; B[6][1] = dt;
     }
-    __device__ static void hess(const double* x, const double* u, const double* l, double dt, double L, double (*H)[NX + NU]) {
+    __device__ __forceinline__ static void hess(const double* x, const double* u, const double* l, double dt, double L, double (*H)[NX + NU]) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), sec2 = 1 + tp * tp, q = 1 + x[3] * x[3];
         double dq = -2 * x[3] / (q * q), d2q = (6 * x[3] * x[3] - 2) / (q * q * q);  // d(1/q), d2(1/q)
@@ -154,35 +154,35 @@ template <> struct Dyn<NLOT_ACKERMANN_2ND> {  // dynamics.py:121-148, output ord
 struct HD {
     double v, gx, gy, hxx, hxy, hyy;
 };
-__device__ inline HD hd_var_x(double x) { return {x, 1, 0, 0, 0, 0}; }
-__device__ inline HD hd_var_y(double y) { return {y, 0, 1, 0, 0, 0}; }
-__device__ inline HD hd_const(double c) { return {c, 0, 0, 0, 0, 0}; }
-__device__ inline HD operator+(HD a, HD b) { return {a.v + b.v, a.gx + b.gx, a.gy + b.gy, a.hxx + b.hxx, a.hxy + b.hxy, a.hyy + b.hyy}; }
-__device__ inline HD operator-(HD a, HD b) { return {a.v - b.v, a.gx - b.gx, a.gy - b.gy, a.hxx - b.hxx, a.hxy - b.hxy, a.hyy - b.hyy}; }
-__device__ inline HD operator+(HD a, double c) { a.v += c; return a; }
-__device__ inline HD operator*(double c, HD a) { return {c * a.v, c * a.gx, c * a.gy, c * a.hxx, c * a.hxy, c * a.hyy}; }
-__device__ inline HD operator*(HD a, HD b) {
+__device__ __forceinline__ HD hd_var_x(double x) { return {x, 1, 0, 0, 0, 0}; }
+__device__ __forceinline__ HD hd_var_y(double y) { return {y, 0, 1, 0, 0, 0}; }
+__device__ __forceinline__ HD hd_const(double c) { return {c, 0, 0, 0, 0, 0}; }
+__device__ __forceinline__ HD operator+(HD a, HD b) { return {a.v + b.v, a.gx + b.gx, a.gy + b.gy, a.hxx + b.hxx, a.hxy + b.hxy, a.hyy + b.hyy}; }
+__device__ __forceinline__ HD operator-(HD a, HD b) { return {a.v - b.v, a.gx - b.gx, a.gy - b.gy, a.hxx - b.hxx, a.hxy - b.hxy, a.hyy - b.hyy}; }
+__device__ __forceinline__ HD operator+(HD a, double c) { a.v += c; return a; }
+__device__ __forceinline__ HD operator*(double c, HD a) { return {c * a.v, c * a.gx, c * a.gy, c * a.hxx, c * a.hxy, c * a.hyy}; }
+__device__ __forceinline__ HD operator*(HD a, HD b) {
     return {a.v * b.v, a.gx * b.v + a.v * b.gx, a.gy * b.v + a.v * b.gy,
             a.hxx * b.v + a.v * b.hxx + 2 * a.gx * b.gx,
             a.hxy * b.v + a.v * b.hxy + a.gx * b.gy + a.gy * b.gx,
             a.hyy * b.v + a.v * b.hyy + 2 * a.gy * b.gy};
 }
-__device__ inline HD hd_chain(HD a, double f0, double f1, double f2) {
+__device__ __forceinline__ HD hd_chain(HD a, double f0, double f1, double f2) {
     return {f0, f1 * a.gx, f1 * a.gy, f1 * a.hxx + f2 * a.gx * a.gx, f1 * a.hxy + f2 * a.gx * a.gy,
             f1 * a.hyy + f2 * a.gy * a.gy};
 }
-__device__ inline HD hd_sqrt(HD a) { double s = sqrt(a.v); return hd_chain(a, s, 0.5 / s, -0.25 / (s * a.v)); }
-__device__ inline HD hd_exp(HD a) { double e = exp(a.v); return hd_chain(a, e, e, e); }
-__device__ inline HD hd_log(HD a) { return hd_chain(a, log(a.v), 1.0 / a.v, -1.0 / (a.v * a.v)); }
+__device__ __forceinline__ HD hd_sqrt(HD a) { double s = sqrt(a.v); return hd_chain(a, s, 0.5 / s, -0.25 / (s * a.v)); }
+__device__ __forceinline__ HD hd_exp(HD a) { double e = exp(a.v); return hd_chain(a, e, e, e); }
+__device__ __forceinline__ HD hd_log(HD a) { return hd_chain(a, log(a.v), 1.0 / a.v, -1.0 / (a.v * a.v)); }
 
 // CircleObstacle.approximated_sdf (core/sdf/casadi.py:33-41): |p - c| - (r + m)
-__device__ inline HD sdf_circle(double cx, double cy, double r, double m, double x, double y) {
+__device__ __forceinline__ HD sdf_circle(double cx, double cy, double r, double m, double x, double y) {
     double dx = x - cx, dy = y - cy, rr = sqrt(dx * dx + dy * dy);
     double nx = dx / rr, ny = dy / rr;
     return {rr - (r + m), nx, ny, (1 - nx * nx) / rr, -nx * ny / rr, (1 - ny * ny) / rr};
 }
 // SquareObstacle.approximated_sdf (core/sdf/casadi.py:69-118)
-__device__ inline HD sdf_square(double cx, double cy, double size, double m, double x, double y) {
+__device__ __forceinline__ HD sdf_square(double cx, double cy, double size, double m, double x, double y) {
     const double half = size / 2 + m;
     HD X = hd_var_x(x) + (-cx), Y = hd_var_y(y) + (-cy);
     HD dx = hd_sqrt(X * X + 1e-6), dy = hd_sqrt(Y * Y + 1e-6);
@@ -196,7 +196,7 @@ __device__ inline HD sdf_square(double cx, double cy, double size, double m, dou
     return outside + inside;
 }
 // MultiObstacle.approximated_sdf (casadi.py:385-386): soft_min over obstacles, utils.py:18-33
-__device__ inline HD sdf_scene(const NlotProblem& p, double x, double y, bool derivs) {
+__device__ __forceinline__ HD sdf_scene(const NlotProblem& p, double x, double y, bool derivs) {
     HD sum = hd_const(0.0);
     for (int i = 0; i < p.n_obs; ++i) {
         const NlotObstacle& o = p.obs[i];
@@ -213,7 +213,7 @@ __device__ inline HD sdf_scene(const NlotProblem& p, double x, double y, bool de
 // Returns 0 (nneg = negative pivots) or 2 if numerically singular.  n <= NMAX compile-time.
 // ---------------------------------------------------------------------------------------------
 template <int NMAX>
-__device__ inline int ldl_factor(double (*a)[NMAX], int n, int* perm, int* nneg) {
+__device__ __forceinline__ int ldl_factor(double (*a)[NMAX], int n, int* perm, int* nneg) {
     double scale = 1e-300;
 #pragma unroll
     for (int i = 0; i < NMAX; ++i)
@@ -227,15 +227,44 @@ __device__ inline int ldl_factor(double (*a)[NMAX], int n, int* perm, int* nneg)
     for (int j = 0; j < NMAX; ++j) {
         if (j >= n) break;
         int pv = j;
+        double best = fabs(a[j][j]);
 #pragma unroll
         for (int i = j + 1; i < NMAX; ++i)
-            if (i < n && fabs(a[i][i]) > fabs(a[pv][pv])) pv = i;
-        if (pv != j) {
+            if (i < n && fabs(a[i][i]) > best) {
+                best = fabs(a[i][i]);
+                pv = i;
+            }
+        if (pv != j) {  // symmetric swap j <-> pv with compile-time register indices only
 #pragma unroll
-            for (int c = 0; c < NMAX; ++c) { double t = a[j][c]; a[j][c] = a[pv][c]; a[pv][c] = t; }
+            for (int c = 0; c < NMAX; ++c) {
+                double rowp = 0;
 #pragma unroll
-            for (int r = 0; r < NMAX; ++r) { double t = a[r][j]; a[r][j] = a[r][pv]; a[r][pv] = t; }
-            int t = perm[j]; perm[j] = perm[pv]; perm[pv] = t;
+                for (int r = 0; r < NMAX; ++r)
+                    if (r == pv) rowp = a[r][c];
+#pragma unroll
+                for (int r = 0; r < NMAX; ++r)
+                    if (r == pv) a[r][c] = a[j][c];
+                a[j][c] = rowp;
+            }
+#pragma unroll
+            for (int r = 0; r < NMAX; ++r) {
+                double colp = 0;
+#pragma unroll
+                for (int c = 0; c < NMAX; ++c)
+                    if (c == pv) colp = a[r][c];
+#pragma unroll
+                for (int c = 0; c < NMAX; ++c)
+                    if (c == pv) a[r][c] = a[r][j];
+                a[r][j] = colp;
+            }
+            int pp = 0;
+#pragma unroll
+            for (int r = 0; r < NMAX; ++r)
+                if (r == pv) pp = perm[r];
+#pragma unroll
+            for (int r = 0; r < NMAX; ++r)
+                if (r == pv) perm[r] = perm[j];
+            perm[j] = pp;
         }
         double d = a[j][j];
         if (!(fabs(d) > 1e-13 * scale) || !isfinite(d)) return 2;
@@ -261,7 +290,7 @@ __device__ inline int ldl_factor(double (*a)[NMAX], int n, int* perm, int* nneg)
 }
 // Solve with the factor for one right-hand side (in place).
 template <int NMAX>
-__device__ inline void ldl_solve1(const double (*a)[NMAX], int n, const int* perm, double* x) {
+__device__ __forceinline__ void ldl_solve1(const double (*a)[NMAX], int n, const int* perm, double* x) {
     double t[NMAX];
 #pragma unroll
     for (int i = 0; i < NMAX; ++i) t[i] = 0;

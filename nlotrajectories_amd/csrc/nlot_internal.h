@@ -49,7 +49,7 @@ struct MlpOut {
 };
 
 // Launch the MFMA SDF-MLP kernel on cnt * P_per points, cnt = *n_dev if n_dev else n (n = upper bound
-// that sizes the persistent grid).  Point g lives at (g % cnt) + (g / cnt) * ld of pts/lam/out.
+// that sizes the persistent grid).  Point g lives at g (ld == 0) or (g % cnt) + (g / cnt) * ld.
 // full = value + lam*grad + lam*hess; else value only.
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                        const float* lam, const MlpOut& out, bool full, hipStream_t stream);

@@ -34,8 +34,8 @@ constexpr int kMaxResidentLayers = 2;
 __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
 
 template <int H, int L, bool FULL>
-// Point g of the launch lives at address (g % cnt) + (g / cnt) * ld of pts / lam / out: a [P_per][ld] list
-// whose first `cnt` columns are valid (cnt = *cnt_dev when given: the solver's compacted instances).
+// Point g of the launch (g < cnt * P_per, cnt = *cnt_dev when given: the solver's compacted instances)
+// lives at address g (ld == 0, contiguous rank-major list) or (g % cnt) + (g / cnt) * ld of pts/lam/out.
 __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
                                                       const int* __restrict__ cnt_dev, int P_per, int64_t ld,
                                                       const float* __restrict__ lam, MlpOut out) {
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
     for (int64_t tile = blockIdx.x; tile * 128 < npts; tile += gridDim.x) {
         const int64_t gi = tile * 128 + wave * 32 + il;
         const bool valid = gi < npts;
-        const int64_t pi = valid ? (gi % cnt) + (gi / cnt) * ld : 0;
+        const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
         float px = 0.f, py = 0.f;
         if (valid) {
             px = pts[2 * pi];
@@ -381,5 +381,5 @@ extern "C" int32_t nlot_sdf_mlp_eval(const NlotMlp* mlp, const float* pts, int64
         set_error("nlot_sdf_mlp_eval: hess requires grad (jac_adj1 is evaluated with adj1)");
         return NLOT_ERR_INVALID;
     }
-    return launch_mlp_strided(mlp->dev, pts, P, nullptr, 1, P, lam, o, full, (hipStream_t)stream);
+    return launch_mlp_strided(mlp->dev, pts, P, nullptr, 1, 0, lam, o, full, (hipStream_t)stream);
 }

@@ -3,10 +3,18 @@
 // restatement of IPOPT's primal-dual filter line-search algorithm (runner.py:113-133)
 // whose Newton systems are solved by a stage-wise Riccati recursion.
 //
-// Layout: every per-instance array is structure-of-arrays with the instance index fastest
-// (element i of instance b at [i * cap + b]), so the one-thread-per-instance kernels below read and
-// write whole 256/512-byte lines per wave.  The learned-SDF points of all active instances are
-// compacted into one list per global step and evaluated by the MFMA kernel (nlot_mlp.hip).
+// MI355X mapping: ONE WAVEFRONT PER INSTANCE.
+//   * lanes over knots for everything that is per knot (SDF chain rule + soft-min, dynamics and their
+//     derivatives, condensed stage matrices, residuals, optimality measures); scalars of the
+//     algorithm come from wave reductions (shuffles), broadcast from lane 0 so every lane takes the
+//     same branch;
+//   * the Riccati recursion is sequential in the knot index: lanes go over the entries of the small
+//     stage matrices (P, [A B]'P[A B], gains), with the recursion state in LDS;
+//   * per-instance arrays are instance-major (a wave touches one contiguous block), the stage
+//     matrices of one Newton solve live in a per-instance scratch (L2-resident between passes);
+//   * the learned-SDF corner points of all instances that need them in a step are compacted
+//     (rank-major) into one list and evaluated by the MFMA kernel (nlot_mlp.hip) in a single launch;
+//   * the host launches only the still-active instances (active list rebuilt every step).
 //
 // Per-instance phase machine (one global step = one launch of each kernel):
 //   INIT -> [corners, MLP full, k_iterate: slack push, least-squares multipliers, then EVAL work]
@@ -17,7 +25,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -29,22 +39,11 @@ namespace nlot {
 enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3 };
 enum Scal {
     SC_MU, SC_TAU, SC_DWLAST, SC_THMAX, SC_THMIN, SC_ALPHA, SC_AMAX, SC_AMIN, SC_AZ, SC_THETA, SC_PHI, SC_GD,
-    SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_COUNT
+    SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_NCAND, SC_COUNT
 };
 constexpr int FILT_MAX = 64;
+constexpr int NSPEC = 8;  // step lengths evaluated per line-search round after a first rejection
 constexpr int MMAX = 4;  // inequalities per knot (rectangle without slack)
-
-struct Ws {
-    double *X, *U, *S, *T, *yi, *yk, *yt, *yd, *zl, *zu, *zs, *vt;
-    double *dv, *Jd, *Hd, *rci, *rcd, *rct, *rcq;
-    double *Kf, *kf, *Kn, *Pm, *pv, *Gm;
-    double *dX, *dU, *dS, *dT, *yi_n, *yk_n, *yt_n, *yd_n, *dzl, *dzu, *dzs, *dvt;
-    double *sc, *filt;
-    float* pts;  // [P_per][cap][2]
-    float* mo;   // [6][P_per][cap]
-    int* cnt;    // [0] eval points count, [1] trial count, [2] not-done count
-    int64_t cap;
-};
 
 struct Dims {
     int N, nx, nu, ns, M, nc, nb, nv, sd;  // nv = nu + ns (stage k < N)
@@ -69,19 +68,45 @@ static Dims make_dims(const NlotProblem& p) {
     return d;
 }
 
-// workspace carving (host and device agree on the order)
+// Per-stage slot of one Newton solve: [A | B | c | M | union{ H, g ; Riccati outputs K, k, Kn, P, p, G }]
+// (the condensed H, g of stage k are dead once the backward sweep has consumed them).
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+__host__ __device__ constexpr int rstg_len(int nx, int nu) {
+    return (nu + 1) * nx + (nu + 1) + (nu + 1) * nx + nx * nx + nx + nx * nx;
+}
+__host__ __device__ constexpr int slot_len(int nx, int nu) {
+    return nx * (nx + nu + 1) + nx + 4 + cmax((nx + nu + 1) * (nx + nu + 1) + (nx + nu + 1), rstg_len(nx, nu));
+}
+constexpr size_t kLdsBudget = 150 * 1024;  // slots go to LDS when they fit, else to the global scratch
+
+// instance-major arrays: (name, per-instance length)
 #define NLOT_WS_ARRAYS(X_)                                                                             \
-    X_(X, (N + 1) * nx) X_(U, N * nu) X_(S, N + 1) X_(T, (N + 1) * M) X_(yi, nx) X_(yk, N * nx) X_(yt, nc) \
+    X_(X, (N + 1) * nx) X_(U, N * nu) X_(S, N + 1) X_(T, (N + 1) * M) X_(yi, nx) X_(yk, N * nx) X_(yt, 8) \
     X_(yd, (N + 1) * M) X_(zl, N * nu) X_(zu, N * nu) X_(zs, N + 1) X_(vt, (N + 1) * M)                \
     X_(dv, (N + 1) * M) X_(Jd, (N + 1) * M * 3) X_(Hd, (N + 1) * 6) X_(rci, nx) X_(rcd, N * nx)         \
-    X_(rct, nc) X_(rcq, (N + 1) * M) X_(Kf, (N + 1) * nv * nx) X_(kf, (N + 1) * nv)                     \
-    X_(Kn, (N + 1) * nv * nc) X_(Pm, (N + 1) * nx * nx) X_(pv, (N + 1) * nx) X_(Gm, (N + 1) * nx * nc) \
-    X_(dX, (N + 1) * nx) X_(dU, N * nu) X_(dS, N + 1) X_(dT, (N + 1) * M) X_(yi_n, nx) X_(yk_n, N * nx) \
-    X_(yt_n, nc) X_(yd_n, (N + 1) * M) X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1)                  \
-    X_(dvt, (N + 1) * M) X_(sc, SC_COUNT) X_(filt, 2 * FILT_MAX)
+    X_(rct, 8) X_(rcq, (N + 1) * M) X_(dX, (N + 1) * nx) X_(dU, N * nu) X_(dS, N + 1)                  \
+    X_(dT, (N + 1) * M) X_(yi_n, nx) X_(yk_n, N * nx) X_(yt_n, 8) X_(yd_n, (N + 1) * M)                \
+    X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1) X_(dvt, (N + 1) * M) X_(sc, SC_COUNT)               \
+    X_(filt, 2 * FILT_MAX) X_(stg, (N + 1) * slot_len(nx, nu))
+
+struct Ws {
+#define NLOT_DECL(name, cnt) \
+    double* name;            \
+    int L_##name;
+    NLOT_WS_ARRAYS(NLOT_DECL)
+#undef NLOT_DECL
+    float* pts;  // compacted corner list, rank-major [rank][P][2]
+    float* mo;   // MLP outputs [6][cap * P] (rank-major within a plane)
+    int* cnt;    // [0] eval instances, [1] trial instances, [2] next active count
+    int* act[2]; // active instance lists (ping-pong)
+    int64_t cap;
+    int ppk;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static size_t ws_doubles_per_instance(const Dims& d) {
-    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M, nc = d.nc, nv = d.nv;
+    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M;
     size_t n = 0;
 #define NLOT_CNT(name, cnt) n += (size_t)(cnt);
     NLOT_WS_ARRAYS(NLOT_CNT)
@@ -89,15 +114,18 @@ static size_t ws_doubles_per_instance(const Dims& d) {
     return n;
 }
 
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t kHdr = 8192;  // device copies of NlotProblem, Dims, Ws (kernels read them through pointers:
+                                // a by-value struct argument indexed at run time is copied to scratch)
+constexpr size_t kHdrProblem = 0, kHdrDims = 2048, kHdrWs = 4096;
 
 static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
-    size_t b = align256(ws_doubles_per_instance(d) * (size_t)B * sizeof(double));
-    if (mlp) {
+    size_t b = kHdr + align256(ws_doubles_per_instance(d) * (size_t)B * sizeof(double));
+    if (mlp) {  // corner list and outputs sized for NSPEC line-search candidates per instance
         const size_t P = (size_t)d.ppk * (d.N + 1);
-        b += align256(P * (size_t)B * 2 * sizeof(float));
-        b += align256(6 * P * (size_t)B * sizeof(float));
+        b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
+        b += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
     }
+    b += align256(2 * (size_t)B * sizeof(int));
     b += 256;  // counters
     return b;
 }
@@ -105,10 +133,13 @@ static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
 static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
     Ws w{};
     w.cap = B;
-    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M, nc = d.nc, nv = d.nv;
+    w.ppk = d.ppk;
+    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M;
+    base = (char*)base + kHdr;
     double* q = (double*)base;
-#define NLOT_TAKE(name, cnt)   \
-    w.name = q;                \
+#define NLOT_TAKE(name, cnt)          \
+    w.name = q;                       \
+    w.L_##name = (int)(cnt);          \
     q += (size_t)(cnt) * (size_t)B;
     NLOT_WS_ARRAYS(NLOT_TAKE)
 #undef NLOT_TAKE
@@ -116,30 +147,61 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
     if (mlp) {
         const size_t P = (size_t)d.ppk * (N + 1);
         w.pts = (float*)c;
-        c += align256(P * (size_t)B * 2 * sizeof(float));
+        c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
         w.mo = (float*)c;
-        c += align256(6 * P * (size_t)B * sizeof(float));
+        c += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
     }
+    w.act[0] = (int*)c;
+    w.act[1] = (int*)c + B;
+    c += align256(2 * (size_t)B * sizeof(int));
     w.cnt = (int*)c;
     return w;
 }
 
-#define AT(arr, i) (ws.arr[(size_t)(i) * ws.cap + b])
-#define SC(i) (ws.sc[(size_t)(i) * ws.cap + b])
+// element i of instance b's array (instance-major)
+#define AT(arr, i) (ws.arr[(size_t)b * ws.L_##arr + (i)])
+#define SC(i) AT(sc, i)
+
+// ---- wave-level helpers (64 lanes; results broadcast from lane 0 so every lane branches alike) ----
+__device__ inline double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return __shfl(v, 0);
+}
+__device__ inline double wmax(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return __shfl(v, 0);
+}
+__device__ inline double wmin(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return __shfl(v, 0);
+}
+__device__ inline void wsync() { __syncthreads(); }  // one-wave workgroups: barrier + LDS/global fence
+// LDS-only workgroup sync (s_waitcnt lgkmcnt(0) + s_barrier): outstanding global stores are not waited
+// for.  Used inside the Riccati recursion when its slots live in LDS; the global fallback needs wsync.
+template <bool LDS>
+__device__ __forceinline__ void xsync() {
+    if constexpr (LDS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    } else {
+        __syncthreads();
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // per-corner SDF: learned (MLP output of this step's compacted list) or analytic
 // ---------------------------------------------------------------------------------------------
-__device__ inline HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, int cntv, int pidx, double cx,
-                                double cy) {
+__device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, int pidx, double cx, double cy) {
     if (p.sdf_kind == NLOT_SDF_ANALYTIC) return sdf_scene(p, cx, cy, true);
-    const size_t P = 0;  // unused
-    (void)P;
-    // MLP outputs: [q][pidx * cap + rank]
-    const int64_t stride = (int64_t)ws.cap;
-    const int64_t plane = (int64_t)((p.shape == NLOT_SHAPE_DOT ? 1 : p.n_body) * (p.N + 1)) * stride;
-    const int64_t o = (int64_t)pidx * stride + rank;
-    (void)cntv;
+    // MLP outputs of this step's compacted list, rank-major: quantity q of point pidx of the
+    // instance with compaction rank r at mo[q * plane + r * P + pidx]
+    const int64_t P = (int64_t)ws.ppk * (p.N + 1);
+    const int64_t plane = P * ws.cap * NSPEC;
+    const int64_t o = (int64_t)rank * P + pidx;
     HD h;
     h.v = ws.mo[o];
     h.gx = ws.mo[plane + o];
@@ -152,11 +214,11 @@ __device__ inline HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, in
 
 // Inequality functions at a knot (geometry.py:63-67, 107-117; utils.py:18-33): values d[j]
 // (slack excluded), pose gradients g[j][3], and Hw = sum_j w[j] d2 d_j / dpose2 (if w != null).
-__device__ inline void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
+__device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
                                  const double* xk, double* d, double (*g)[3], const double* w, double* Hw) {
     const double x = xk[0], y = xk[1];
     if (p.shape == NLOT_SHAPE_DOT) {
-        HD f = corner_sdf(p, ws, rank, 0, k, x, y);
+        HD f = corner_sdf(p, ws, rank, k, x, y);
         d[0] = f.v;
         if (g) { g[0][0] = f.gx; g[0][1] = f.gy; g[0][2] = 0; }
         if (Hw) {
@@ -168,11 +230,13 @@ __device__ inline void knot_eval(const NlotProblem& p, const Dims& dm, const Ws&
     double sn, cs;
     sincos(xk[2], &sn, &cs);
     double phi[MMAX], gp[MMAX][3], Hp[MMAX][6];  // Hp: xx xy xt yy yt tt
-    for (int i = 0; i < dm.nb; ++i) {
+#pragma unroll
+    for (int i = 0; i < MMAX; ++i) {
+        if (i >= dm.nb) break;
         const double bx = p.body[i][0], by = p.body[i][1];
         const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
         const double ex = -(cy - y), ey = cx - x;                            // d c / d theta
-        HD f = corner_sdf(p, ws, rank, 0, k * dm.nb + i, cx, cy);
+        HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy);
         phi[i] = f.v;
         gp[i][0] = f.gx;
         gp[i][1] = f.gy;
@@ -187,69 +251,52 @@ __device__ inline void knot_eval(const NlotProblem& p, const Dims& dm, const Ws&
     if (p.use_slack) {  // soft_min over corners (not max-shifted, as utils.py:30-31)
         const double al = p.softmin_alpha;
         double e[MMAX], sum = 0;
-        for (int i = 0; i < dm.nb; ++i) {
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i) {
+            if (i >= dm.nb) break;
             e[i] = exp(-al * phi[i]);
             sum += e[i];
         }
         d[0] = -log(sum) / al;
         double gd[3] = {0, 0, 0};
-        for (int i = 0; i < dm.nb; ++i)
-            for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[i][a];
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i)
+            if (i < dm.nb)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[i][a];
         if (g)
             for (int a = 0; a < 3; ++a) g[0][a] = gd[a];
         if (Hw) {
             double H[6] = {0, 0, 0, 0, 0, 0};
             const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
-            for (int i = 0; i < dm.nb; ++i) {
+#pragma unroll
+            for (int i = 0; i < MMAX; ++i) {
+                if (i >= dm.nb) break;
                 const double wi = e[i] / sum;
+#pragma unroll
                 for (int q = 0; q < 6; ++q) H[q] += wi * (Hp[i][q] - al * gp[i][ia[q]] * gp[i][ib[q]]);
             }
             for (int q = 0; q < 6; ++q) Hw[q] = w[0] * (H[q] + al * gd[ia[q]] * gd[ib[q]]);
         }
     } else {
-        for (int i = 0; i < dm.nb; ++i) {
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i) {
+            if (i >= dm.nb) break;
             d[i] = phi[i];
             if (g)
+#pragma unroll
                 for (int a = 0; a < 3; ++a) g[i][a] = gp[i][a];
         }
         if (Hw) {
+#pragma unroll
             for (int q = 0; q < 6; ++q) Hw[q] = 0;
-            for (int i = 0; i < dm.nb; ++i)
-                for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[i][q];
+#pragma unroll
+            for (int i = 0; i < MMAX; ++i)
+                if (i < dm.nb)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[i][q];
         }
     }
-}
-
-// objective value (runner.py:80-96)
-__device__ inline double objective(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, const double* dXs,
-                                   const double* dUs, const double* dSs, double al) {
-    (void)dXs; (void)dUs; (void)dSs;
-    const int nx = dm.nx, nu = dm.nu, N = dm.N;
-    double f = 0;
-    for (int k = 0; k < N; ++k) {
-        const double dx = (AT(X, (k + 1) * nx) + al * AT(dX, (k + 1) * nx)) - (AT(X, k * nx) + al * AT(dX, k * nx));
-        const double dy = (AT(X, (k + 1) * nx + 1) + al * AT(dX, (k + 1) * nx + 1)) -
-                          (AT(X, k * nx + 1) + al * AT(dX, k * nx + 1));
-        f += sqrt(dx * dx + dy * dy + p.path_eps);
-    }
-    if (p.use_slack) {
-        double q = 0;
-        for (int k = 0; k <= N; ++k) {
-            const double s = AT(S, k) + al * AT(dS, k);
-            q += s * s;
-        }
-        f += p.slack_penalty * q;
-    }
-    if (p.use_smooth) {
-        double q = 0;
-        for (int k = 0; k < N - 1; ++k)
-            for (int i = 0; i < nu; ++i) {
-                const double u = AT(U, k * nu + i) + al * AT(dU, k * nu + i);
-                q += u * u;
-            }
-        f += p.smooth_weight * q;
-    }
-    return f;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -257,26 +304,39 @@ __device__ inline double objective(const NlotProblem& p, const Dims& dm, const W
 // ---------------------------------------------------------------------------------------------
 enum { MODE_NEWTON = 0, MODE_LSQ = 1 };
 
+#ifdef NLOT_PHASE_PROF
+#define PROF_T(v) const long long v = wall_clock64()
+#define PROF_ACC(acc, v0) acc += wall_clock64() - v0
+#else
+#define PROF_T(v)
+#define PROF_ACC(acc, v0)
+#endif
+
 template <int DYN>
 struct Solver {
     using D = Dyn<DYN>;
     static constexpr int NX = D::NX, NU = D::NU, NV = NU + 1, NZ = NX + NV, NC = NX;
 
-    // Condensed stage matrix H (nz x nz) and gradient g (nz) of stage k.
-    __device__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
-                                 double dw, double (*H)[NZ], double* g) {
-        const int N = dm.N, nu = NU, M = dm.M;
-        const int nvk = (k < N ? nu : 0) + dm.ns, nz = NX + nvk, iu = NX, is = NX + (k < N ? nu : 0);
+    // Condensed stage matrix H (nz x nz) and gradient g (nz) of stage k, written to o[0, NZ*NZ) and
+    // o[NZ*NZ, NZ*NZ+NZ).  H is accumulated in its structured blocks (pose 3x3, pose-slack, slack,
+    // control diagonal, dynamics curvature) and emitted dense once, so it never occupies 64 doubles
+    // of registers.
+    __device__ __forceinline__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
+                                                 double dw, double* o) {
+        const int N = dm.N, M = dm.M;
         const double mu = SC(SC_MU), kappa_d = 1e-5;
+        const bool newton = mode == MODE_NEWTON;
+        double Pp[3][3], ps[3], gp[NX], gu[NU], uu[NU], ss = 0, gs = 0;
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) {
-            g[i] = 0;
+        for (int i = 0; i < 3; ++i) {
+            ps[i] = 0;
 #pragma unroll
-            for (int j = 0; j < NZ; ++j) H[i][j] = 0;
+            for (int j = 0; j < 3; ++j) Pp[i][j] = 0;
         }
-        double x[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+        for (int i = 0; i < NX; ++i) gp[i] = 0;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) gu[i] = uu[i] = 0;
         // objective gradient and (Newton) Hessian of the path-length terms
         for (int seg = k - 1; seg <= k; ++seg) {
             if (seg < 0 || seg >= N) continue;
@@ -284,83 +344,75 @@ struct Solver {
             const double dy = AT(X, (seg + 1) * NX + 1) - AT(X, seg * NX + 1);
             const double r2 = dx * dx + dy * dy + p.path_eps, r = sqrt(r2), r3 = r2 * r;
             const double sgn = seg == k ? -1.0 : 1.0;
-            g[0] += sgn * dx / r;
-            g[1] += sgn * dy / r;
-            if (mode == MODE_NEWTON) {
-                H[0][0] += (r2 - dx * dx) / r3;
-                H[0][1] += -dx * dy / r3;
-                H[1][0] += -dx * dy / r3;
-                H[1][1] += (r2 - dy * dy) / r3;
+            gp[0] += sgn * dx / r;
+            gp[1] += sgn * dy / r;
+            if (newton) {
+                Pp[0][0] += (r2 - dx * dx) / r3;
+                Pp[0][1] += -dx * dy / r3;
+                Pp[1][0] += -dx * dy / r3;
+                Pp[1][1] += (r2 - dy * dy) / r3;
             }
         }
-        if (p.use_slack) g[is] += 2.0 * p.slack_penalty * AT(S, k);
+        const double Sk = AT(S, k);
+        if (p.use_slack) gs += 2.0 * p.slack_penalty * Sk;
         if (p.use_smooth && k < N - 1)
 #pragma unroll
-            for (int i = 0; i < NU; ++i) g[iu + i] += 2.0 * p.smooth_weight * AT(U, k * NU + i);
-        if (mode == MODE_NEWTON) {
-            if (p.use_slack) H[is][is] += 2.0 * p.slack_penalty;
+            for (int i = 0; i < NU; ++i) gu[i] += 2.0 * p.smooth_weight * AT(U, k * NU + i);
+        double Hz[NX + NU][NX + NU];  // dynamics curvature: constant sparsity, folds to a few registers
+#pragma unroll
+        for (int i = 0; i < NX + NU; ++i)
+#pragma unroll
+            for (int j = 0; j < NX + NU; ++j) Hz[i][j] = 0;
+        if (newton) {
+            if (p.use_slack) ss += 2.0 * p.slack_penalty;
             if (p.use_smooth && k < N - 1)
 #pragma unroll
-                for (int i = 0; i < NU; ++i) H[iu + i][iu + i] += 2.0 * p.smooth_weight;
+                for (int i = 0; i < NU; ++i) uu[i] += 2.0 * p.smooth_weight;
             if (k < N) {  // dynamics c_k = x_{k+1} - F_k  =>  W -= sum_i y_i d2F_i
-                double u[NU], l[NX], Hz[NX + NU][NX + NU];
+                double x[NX], u[NU], l[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
 #pragma unroll
                 for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) l[i] = AT(yk, k * NX + i);
-#pragma unroll
-                for (int i = 0; i < NX + NU; ++i)
-#pragma unroll
-                    for (int j = 0; j < NX + NU; ++j) Hz[i][j] = 0;
                 D::hess(x, u, l, p.dt, p.wheelbase, Hz);
-#pragma unroll
-                for (int i = 0; i < NX + NU; ++i)
-#pragma unroll
-                    for (int j = 0; j < NX + NU; ++j) H[i][j] -= Hz[i][j];
             }
             // knot inequality curvature sum_j yd_j d2 d_j (pose block x, y, theta)
             {
                 const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
                 for (int q = 0; q < 6; ++q) {
-                    if (ia[q] >= NX || ib[q] >= NX) continue;
                     const double v = AT(Hd, k * 6 + q);
-                    H[ia[q]][ib[q]] += v;
-                    if (ia[q] != ib[q]) H[ib[q]][ia[q]] += v;
+                    Pp[ia[q]][ib[q]] += v;
+                    if (ia[q] != ib[q]) Pp[ib[q]][ia[q]] += v;
                 }
             }
             if (k < N)
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
-                    const double uu = AT(U, k * NU + i), sl = uu - p.umin[i], su = p.umax[i] - uu;
-                    H[iu + i][iu + i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
-                    g[iu + i] += -mu / sl + mu / su;
+                    const double uv = AT(U, k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
+                    uu[i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
+                    gu[i] += -mu / sl + mu / su;
                 }
             if (dm.ns) {
-                const double s = AT(S, k);
-                H[is][is] += AT(zs, k) / s;
-                g[is] += -mu / s + kappa_d * mu;
+                ss += AT(zs, k) / Sk;
+                gs += -mu / Sk + kappa_d * mu;
             }
-            for (int i = 0; i < nz; ++i) H[i][i] += dw;
         } else {
-            for (int i = 0; i < nz; ++i) H[i][i] = 1.0;
             if (k < N)
 #pragma unroll
-                for (int i = 0; i < NU; ++i) g[iu + i] += -AT(zl, k * NU + i) + AT(zu, k * NU + i);
-            if (dm.ns) g[is] += -AT(zs, k);
+                for (int i = 0; i < NU; ++i) gu[i] += -AT(zl, k * NU + i) + AT(zu, k * NU + i);
+            if (dm.ns) gs += -AT(zs, k);
         }
-        // eliminated inequality slacks t
+        // eliminated inequality slacks t:  H += J' D J, g += J' rhs, J = (d d_j/d pose, 1 on the slack)
         for (int j = 0; j < M; ++j) {
-            double J[NZ];
+            double J[3];
 #pragma unroll
-            for (int a = 0; a < NZ; ++a) J[a] = 0;
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-                if (a < NX) J[a] = AT(Jd, (k * M + j) * 3 + a);
-            if (dm.sd) J[is] = 1.0;
+            for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + j) * 3 + a);
             const double t = AT(T, k * M + j), v = AT(vt, k * M + j);
             double Dj, rhs;
-            if (mode == MODE_NEWTON) {
+            if (newton) {
                 Dj = v / t + dw;
                 rhs = Dj * AT(rcq, k * M + j) + (-mu / t + kappa_d * mu);
             } else {
@@ -368,16 +420,53 @@ struct Solver {
                 rhs = -v;
             }
 #pragma unroll
-            for (int a = 0; a < NZ; ++a) {
-                g[a] += J[a] * rhs;
+            for (int a = 0; a < 3; ++a) {
+                gp[a] += J[a] * rhs;
 #pragma unroll
-                for (int c = 0; c < NZ; ++c) H[a][c] += Dj * J[a] * J[c];
+                for (int c = 0; c < 3; ++c) Pp[a][c] += Dj * J[a] * J[c];
+                if (dm.sd) ps[a] += Dj * J[a];
+            }
+            if (dm.sd) {
+                ss += Dj;
+                gs += rhs;
             }
         }
+        // emit dense H, g; the slack column is NX + NU (k < N) or NX (k == N): compile-time per branch
+        const double dg = newton ? dw : 1.0;
+        auto emit = [&](auto has_u) {
+            constexpr bool HU = decltype(has_u)::value;
+            constexpr int is = HU ? NX + NU : NX;
+            const bool hs = dm.ns != 0;
+            const int nz = is + (hs ? 1 : 0);
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+#pragma unroll
+                for (int j = 0; j < NZ; ++j) {
+                    double h = 0;
+                    if (i < 3 && j < 3) h += Pp[i][j];
+                    if (HU && i == j && i >= NX && i < NX + NU) h += uu[i - NX];
+                    if (HU && i < NX + NU && j < NX + NU) h -= Hz[i][j];
+                    if (hs) {
+                        if (i == is && j == is) h += ss;
+                        if (i == is && j < 3) h += ps[j];
+                        if (j == is && i < 3) h += ps[i];
+                    }
+                    if (i == j && i < nz) h += dg;
+                    o[i * NZ + j] = h;
+                }
+                double gi = 0;
+                if (i < NX) gi = gp[i];
+                else if (HU && i < NX + NU) gi = gu[i - NX];
+                if (hs && i == is) gi = gs;
+                o[NZ * NZ + i] = gi;
+            }
+        };
+        if (k < N) emit(std::true_type{});
+        else emit(std::false_type{});
     }
 
     // path-length cross block M_k (positions of x_k vs x_{k+1}) = -G_k
-    __device__ static void cross(const NlotProblem& p, const Ws& ws, int b, int k, int mode, double (*Mk)[2]) {
+    __device__ __forceinline__ static void cross(const NlotProblem& p, const Ws& ws, int b, int k, int mode, double (*Mk)[2]) {
         Mk[0][0] = Mk[0][1] = Mk[1][0] = Mk[1][1] = 0;
         if (mode != MODE_NEWTON) return;
         const double dx = AT(X, (k + 1) * NX) - AT(X, k * NX), dy = AT(X, (k + 1) * NX + 1) - AT(X, k * NX + 1);
@@ -387,42 +476,41 @@ struct Solver {
         Mk[1][1] = -(r2 - dy * dy) / r3;
     }
 
-    // Backward Riccati with the terminal multiplier carried along, then the forward sweep.
-    // Residuals of the right-hand side come from rci/rcd/rct/rcq (zero in LSQ mode).
-    // Returns 0, or 1 when the inertia test fails.
-    __device__ static int riccati(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int mode, double dw) {
-        const int N = dm.N, nc = dm.nc, ns = dm.ns;
-        double P[NX][NX], pp[NX], G[NX][NC], Psi[NC][NC], psi[NC];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            pp[i] = 0;
-#pragma unroll
-            for (int j = 0; j < NX; ++j) P[i][j] = 0;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) G[i][c] = 0;
-        }
-#pragma unroll
-        for (int a = 0; a < NC; ++a) {
-            psi[a] = 0;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) Psi[a][c] = 0;
-        }
-        int negsum = 0;
-        SC(SC_DC) = 0.0;
-        for (int k = N; k >= 0; --k) {
-            const int nv = (k < N ? NU : 0) + ns, nz = NX + nv;
-            double H[NZ][NZ], g[NZ];
-            stage(p, dm, ws, b, k, mode, dw, H, g);
-            double A[NX][NX], Bu[NX][NU], c[NX];
-            // [A B] with the slack column zero;  c = F_k - x_{k+1} = -rcd_k
+    // ---------------- wave-parallel Riccati ----------------
+    // slot layout (see slot_len): [A B 0] (NX x NZ, dense) | c | M | union{ H, g ; K, k, Kn, P, p, G }
+    static constexpr int SLOT = slot_len(NX, NU), RSTG = rstg_len(NX, NU);
+    static constexpr int sAB = 0, sc = NX * NZ, sM = sc + NX, sU = sM + 4;
+    static constexpr int oH = sU, og = sU + NZ * NZ;                       // union: condensed stage
+    static constexpr int rK = sU, rk = rK + NV * NX, rKn = rk + NV, rP = rKn + NV * NC, rp = rP + NX * NX,
+                         rG = rp + NX;                                       // union: Riccati outputs
+    static_assert(rG + NX * NC == sU + RSTG, "slot layout");
+    static constexpr int NCOL = NX + 1 + NC;                               // gain columns: K | k | Kn
+
+    struct Sh {
+        double P[2][NX][NX], pp[2][NX], G[2][NX][NC];  // value function (double-buffered)
+        double Psi[NC][NC], psi[NC];
+        double PAB[NX][NZ], Pcp[NX];
+        double Q[NZ][NZ], q[NZ], QN[NZ][NC];
+        double cols[NCOL][NV];                         // gains, column-major, zero beyond nv / nc
+    };
+
+    // Build every stage's condensed matrices in parallel (lane = knot) into the slots.
+    template <bool LDS>
+    __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
+                                        double dw, double* SL) {
+        const int N = dm.N;
+        for (int k = lane; k <= N; k += 64) {
+            double* o = SL + (size_t)k * SLOT;
+            stage(p, dm, ws, b, k, mode, dw, o + oH);
+            double A[NX][NX], Bu[NX][NU];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                c[i] = 0;
 #pragma unroll
                 for (int j = 0; j < NX; ++j) A[i][j] = 0;
 #pragma unroll
                 for (int j = 0; j < NU; ++j) Bu[i][j] = 0;
             }
+            double Mk[2][2] = {{0, 0}, {0, 0}};
             if (k < N) {
                 double x[NX], u[NU];
 #pragma unroll
@@ -430,402 +518,444 @@ struct Solver {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
                 D::jac(x, u, p.dt, p.wheelbase, A, Bu);
-#pragma unroll
-                for (int i = 0; i < NX; ++i) c[i] = mode == MODE_NEWTON ? -AT(rcd, k * NX + i) : 0.0;
-                double Mk[2][2];
                 cross(p, ws, b, k, mode, Mk);
-                // substitute dx_{k+1} = A dx + B dv + c into dx_k' M dx_{k+1}
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) {
-                        const double ma = Mk[i][0] * A[0][j] + Mk[i][1] * A[1][j];
-                        H[i][j] += ma;
-                        H[j][i] += ma;
-                    }
-#pragma unroll
-                    for (int j = 0; j < NU; ++j) {
-                        const double mb = Mk[i][0] * Bu[0][j] + Mk[i][1] * Bu[1][j];
-                        H[i][NX + j] += mb;
-                        H[NX + j][i] += mb;
-                    }
-                    g[i] += Mk[i][0] * c[0] + Mk[i][1] * c[1];
-                }
             }
-            // AB = [A | B | 0]  (NX x NZ)
-            double AB[NX][NZ];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
 #pragma unroll
-                for (int j = 0; j < NX; ++j) AB[i][j] = A[i][j];
-#pragma unroll
-                for (int j = 0; j < NV; ++j) AB[i][NX + j] = j < NU ? Bu[i][j] : 0.0;
+                for (int j = 0; j < NZ; ++j) o[sAB + i * NZ + j] = j < NX ? A[i][j] : (j < NX + NU ? Bu[i][j - NX] : 0.0);
+                o[sc + i] = (k < N && mode == MODE_NEWTON) ? -AT(rcd, k * NX + i) : 0.0;
             }
-            double PAB[NX][NZ], Pcp[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-#pragma unroll
-                for (int j = 0; j < NZ; ++j) {
+            o[sM + 0] = Mk[0][0];
+            o[sM + 1] = Mk[0][1];
+            o[sM + 2] = Mk[1][0];
+            o[sM + 3] = Mk[1][1];
+        }
+        xsync<LDS>();
+    }
+
+    // Returns 0, or 1 when the inertia test fails (uniform over the wave).  Writes dX, dU, dS, yi_n, yk_n, yt_n.
+    // Per stage: 4 LDS barriers; the Q_vv factorisation is computed redundantly in every lane's
+    // registers (no serial LDS round trips); the forward sweep is barrier-free (every lane carries dx).
+    template <bool LDS>
+    __device__ static int riccati_wave(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
+                                       double dw, Sh& sh, double* SL) {
+        const int N = dm.N, nc = dm.nc, ns = dm.ns;
+#ifdef NLOT_PHASE_PROF
+        long long pa = 0, pb = 0, pc = 0, pd = 0;
+#endif
+        PROF_T(r0);
+        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, SL);
+        PROF_T(r1);
+        int cur = 0, negsum = 0;
+        for (int e = lane; e < NX * NX + NX + NX * NC + NC * NC + NC; e += 64) {
+            if (e < NX * NX) sh.P[0][e / NX][e % NX] = 0;
+            else if (e < NX * NX + NX) sh.pp[0][e - NX * NX] = 0;
+            else if (e < NX * NX + NX + NX * NC) { int f = e - NX * NX - NX; sh.G[0][f / NC][f % NC] = 0; }
+            else if (e < NX * NX + NX + NX * NC + NC * NC) { int f = e - NX * NX - NX - NX * NC; sh.Psi[f / NC][f % NC] = 0; }
+            else sh.psi[e - NX * NX - NX - NX * NC - NC * NC] = 0;
+        }
+        if (mode == MODE_NEWTON && lane == 0) SC(SC_DC) = 0.0;
+        xsync<true>();
+        for (int k = N; k >= 0; --k) {
+            const int nv = (k < N ? NU : 0) + ns, nxt = cur ^ 1;
+            double* slot = SL + (size_t)k * SLOT;
+            const double* AB = slot + sAB;
+            PROF_T(q0);
+            // (1) PAB = P [A B 0],  Pcp = P c + p
+            for (int e = lane; e < NX * NZ + NX; e += 64) {
+                if (e < NX * NZ) {
+                    const int r = e / NZ, j = e % NZ;
                     double t = 0;
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) t += P[i][q] * AB[q][j];
-                    PAB[i][j] = t;
-                }
-                double t = pp[i];
+                    for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * AB[q * NZ + j];
+                    sh.PAB[r][j] = t;
+                } else {
+                    const int r = e - NX * NZ;
+                    double t = sh.pp[cur][r];
 #pragma unroll
-                for (int q = 0; q < NX; ++q) t += P[i][q] * c[q];
-                Pcp[i] = t;
-            }
-            // Q = H' + AB' P AB, q = g' + AB'(P c + p), QN = AB' G
-            double Q[NZ][NZ], q[NZ], QN[NZ][NC];
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) {
-#pragma unroll
-                for (int j = 0; j < NZ; ++j) {
-                    double t = H[i][j];
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r][i] * PAB[r][j];
-                    Q[i][j] = t;
-                }
-                double t = g[i];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) t += AB[r][i] * Pcp[r];
-                q[i] = t;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) {
-                    double u = 0;
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) u += AB[r][i] * G[r][cc];
-                    QN[i][cc] = u;
+                    for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * slot[sc + q];
+                    sh.Pcp[r] = t;
                 }
             }
-            // stage control block: slack at position NX + nv - 1 when k == N (no u at the last knot)
-            int vidx[NV];
+            xsync<true>();
+            PROF_ACC(pa, q0);
+            PROF_T(q1);
+            // (2) Q = H + cross + AB' PAB,  q = g + M c + AB' Pcp,  QN = AB' G   (cross: the path-length
+            //     coupling dx_k' M dx_{k+1} with dx_{k+1} = A dx + B dv + c substituted)
+            for (int e = lane; e < NZ * NZ + NZ + NZ * NC; e += 64) {
+                if (e < NZ * NZ) {
+                    const int i = e / NZ, j = e % NZ;
+                    double t = slot[oH + e];
+                    if (i < 2) t += slot[sM + i * 2] * AB[j] + slot[sM + i * 2 + 1] * AB[NZ + j];
+                    if (j < 2) t += slot[sM + j * 2] * AB[i] + slot[sM + j * 2 + 1] * AB[NZ + i];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) vidx[v] = NX + v;
-            // stage() places the slack at NX + (k < N ? NU : 0): at the last knot it is column NX
-            if (k == N) vidx[0] = NX;
-            double Kk[NV][NX], kk[NV], Kn[NV][NC];
+                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.PAB[r][j];
+                    sh.Q[i][j] = t;
+                } else if (e < NZ * NZ + NZ) {
+                    const int i = e - NZ * NZ;
+                    double t = slot[og + i];
+                    if (i < 2) t += slot[sM + i * 2] * slot[sc + 0] + slot[sM + i * 2 + 1] * slot[sc + 1];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                kk[v] = 0;
+                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.Pcp[r];
+                    sh.q[i] = t;
+                } else {
+                    const int f = e - NZ * NZ - NZ, i = f / NC, cc = f % NC;
+                    double t = 0;
 #pragma unroll
-                for (int j = 0; j < NX; ++j) Kk[v][j] = 0;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) Kn[v][cc] = 0;
+                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.G[cur][r][cc];
+                    sh.QN[i][cc] = t;
+                }
             }
+            xsync<true>();
+            PROF_ACC(pb, q1);
+            PROF_T(q2);
+            // (3) every lane factors Q_vv in registers (identical, uniform inertia decision); lane c
+            //     solves gain column c and stores it (LDS for the value update, slot for the forward sweep)
             if (nv > 0) {
                 double L[NV][NV];
                 int perm[NV], nneg;
 #pragma unroll
                 for (int i = 0; i < NV; ++i)
 #pragma unroll
-                    for (int j = 0; j < NV; ++j) L[i][j] = (i < nv && j < nv) ? Q[vidx[i]][vidx[j]] : 0.0;
+                    for (int j = 0; j < NV; ++j) L[i][j] = (i < nv && j < nv) ? sh.Q[NX + i][NX + j] : 0.0;
                 if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
                 negsum += nneg;
                 if (negsum > nc) return 1;
-                double col[NV];
+                if (lane < NCOL) {
+                    const int c = lane;
+                    double col[NV];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) {
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? -Q[vidx[v]][j] : 0.0;
+                    for (int v = 0; v < NV; ++v) {
+                        double r = 0;
+                        if (v < nv) {
+                            if (c < NX) r = -sh.Q[NX + v][c];
+                            else if (c == NX) r = -sh.q[NX + v];
+                            else if (c - NX - 1 < nc) r = -sh.QN[NX + v][c - NX - 1];
+                        }
+                        col[v] = r;
+                    }
                     ldl_solve1<NV>(L, nv, perm, col);
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) Kk[v][j] = col[v];
+                    for (int v = 0; v < NV; ++v) {
+                        const double r = v < nv ? col[v] : 0.0;
+                        sh.cols[c][v] = r;
+                        if (c < NX) slot[rK + v * NX + c] = r;
+                        else if (c == NX) slot[rk + v] = r;
+                        else slot[rKn + v * NC + (c - NX - 1)] = r;
+                    }
                 }
+            } else if (lane < NCOL) {
 #pragma unroll
-                for (int v = 0; v < NV; ++v) col[v] = v < nv ? -q[vidx[v]] : 0.0;
-                ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) kk[v] = col[v];
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) {
-                    if (cc >= nc) break;
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? -QN[vidx[v]][cc] : 0.0;
-                    ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) Kn[v][cc] = col[v];
-                }
-            }
-            // store gains
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                if (v >= dm.nv) continue;
-                AT(kf, k * dm.nv + v) = kk[v];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) AT(Kf, (k * dm.nv + v) * NX + j) = Kk[v][j];
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc)
-                    if (cc < nc) AT(Kn, (k * dm.nv + v) * nc + cc) = Kn[v][cc];
-            }
-            // value function of stage k
-            double Pn[NX][NX], pn[NX], Gn[NX][NC];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-#pragma unroll
-                for (int j = 0; j < NX; ++j) {
-                    double t = Q[i][j];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v)
-                        if (v < nv) t += Q[i][vidx[v]] * Kk[v][j];
-                    Pn[i][j] = t;
-                }
-                double t = q[i];
-#pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    if (v < nv) t += Q[i][vidx[v]] * kk[v];
-                pn[i] = t;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) {
-                    double u = QN[i][cc];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v)
-                        if (v < nv) u += Q[i][vidx[v]] * Kn[v][cc];
-                    Gn[i][cc] = u;
+                for (int v = 0; v < NV; ++v) {
+                    const int c = lane;
+                    sh.cols[c][v] = 0.0;
+                    if (c < NX) slot[rK + v * NX + c] = 0.0;
+                    else if (c == NX) slot[rk + v] = 0.0;
+                    else slot[rKn + v * NC + (c - NX - 1)] = 0.0;
                 }
             }
+            xsync<true>();
+            PROF_ACC(pc, q2);
+            PROF_T(q3);
+            // (4) value function of stage k (symmetrised P) and the terminal-multiplier system; the
+            //     last knot carries the terminal equality C x_N = xg_sel
+            for (int e = lane; e < NX * NX + NX + NX * NC + NC * NC + NC; e += 64) {
+                if (e < NX * NX) {
+                    const int i = e / NX, j = e % NX;
+                    double t = sh.Q[i][j], t2 = sh.Q[j][i];
 #pragma unroll
-            for (int i = 0; i < NX; ++i)
+                    for (int v = 0; v < NV; ++v) {
+                        t += sh.Q[i][NX + v] * sh.cols[j][v];
+                        t2 += sh.Q[j][NX + v] * sh.cols[i][v];
+                    }
+                    const double r = i == j ? t : 0.5 * (t + t2);
+                    sh.P[nxt][i][j] = r;
+                    slot[rP + e] = r;
+                } else if (e < NX * NX + NX) {
+                    const int i = e - NX * NX;
+                    double t = sh.q[i];
 #pragma unroll
-                for (int j = 0; j < i; ++j) {
-                    const double a = 0.5 * (Pn[i][j] + Pn[j][i]);
-                    Pn[i][j] = Pn[j][i] = a;
-                }
+                    for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX][v];
+                    sh.pp[nxt][i] = t;
+                    slot[rp + i] = t;
+                } else if (e < NX * NX + NX + NX * NC) {
+                    const int f = e - NX * NX - NX, i = f / NC, cc = f % NC;
+                    double t;
+                    if (k == N) {
+                        t = (cc < nc && dm.tidx[cc] == i) ? 1.0 : 0.0;
+                    } else {
+                        t = sh.QN[i][cc];
 #pragma unroll
-            for (int a = 0; a < NC; ++a) {
-                if (a >= nc) continue;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) {
-                    if (cc >= nc) continue;
+                        for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + 1 + cc][v];
+                    }
+                    sh.G[nxt][i][cc] = t;
+                    slot[rG + f] = t;
+                } else if (e < NX * NX + NX + NX * NC + NC * NC) {
+                    const int f = e - NX * NX - NX - NX * NC, a = f / NC, cc = f % NC;
                     double t = 0;
 #pragma unroll
-                    for (int v = 0; v < NV; ++v)
-                        if (v < nv) t += QN[vidx[v]][a] * Kn[v][cc];
-                    Psi[a][cc] += t;
-                }
-                double t = 0;
+                    for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + 1 + cc][v];
+                    sh.Psi[a][cc] += t;
+                } else {
+                    const int a = e - NX * NX - NX - NX * NC - NC * NC;
+                    if (k == N) {
+                        sh.psi[a] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
+                    } else {
+                        double t = 0;
 #pragma unroll
-                for (int r = 0; r < NX; ++r) t += G[r][a] * c[r];
+                        for (int r = 0; r < NX; ++r) t += sh.G[cur][r][a] * slot[sc + r];
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    if (v < nv) t += QN[vidx[v]][a] * kk[v];
-                psi[a] += t;
-            }
-            if (k == N) {  // terminal equality C x_N = xg_sel
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) Gn[i][cc] = 0;
-                for (int cc = 0; cc < nc; ++cc) {
-                    Gn[dm.tidx[cc]][cc] = 1.0;
-                    psi[cc] = mode == MODE_NEWTON ? AT(rct, cc) : 0.0;
+                        for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX][v];
+                        sh.psi[a] += t;
+                    }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                AT(pv, k * NX + i) = pn[i];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) AT(Pm, (k * NX + i) * NX + j) = Pn[i][j];
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc)
-                    if (cc < nc) AT(Gm, (k * NX + i) * nc + cc) = Gn[i][cc];
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                pp[i] = pn[i];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) P[i][j] = Pn[i][j];
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) G[i][cc] = Gn[i][cc];
-            }
+            cur = nxt;
+            xsync<true>();
+            PROF_ACC(pd, q3);
         }
-        // terminal multiplier (Sylvester inertia check, delta_c on the terminal block if needed)
-        double dx0[NX], nu_[NC];
+        xsync<LDS>();  // slot outputs (HBM in the fallback) are read across lanes below
+        PROF_T(r2);
+        // terminal multiplier (every lane, identical): -Psi nu = G0' dx0 + psi, delta_c on the terminal block
+        double dx[NX], nu_[NC];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
+        for (int i = 0; i < NX; ++i) dx[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) nu_[cc] = 0;
+        for (int cc = 0; cc < NC; ++cc) nu_[cc] = 0.0;
         if (nc) {
             double L[NC][NC];
             int perm[NC], nneg;
 #pragma unroll
             for (int i = 0; i < NC; ++i)
 #pragma unroll
-                for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -Psi[i][j] : 0.0;
-            int st = ldl_factor<NC>(L, nc, perm, &nneg);
-            if (st == 2 || nneg != negsum) {
+                for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.Psi[i][j] : 0.0;
+            int f = ldl_factor<NC>(L, nc, perm, &nneg);
+            if (f == 2 || nneg != negsum) {
                 const double dc = 1e-8 * pow(SC(SC_MU), 0.25);
 #pragma unroll
                 for (int i = 0; i < NC; ++i)
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -Psi[i][j] + (i == j ? dc : 0.0) : 0.0;
+                    for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.Psi[i][j] + (i == j ? dc : 0.0) : 0.0;
                 if (ldl_factor<NC>(L, nc, perm, &nneg)) return 1;
                 if (nneg != negsum) return 1;
-                SC(SC_DC) = dc;
+                if (lane == 0) SC(SC_DC) = dc;
             }
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc) {
-                if (cc >= nc) continue;
-                double t = psi[cc];
+                double t = 0;
+                if (cc < nc) {
+                    t = sh.psi[cc];
 #pragma unroll
-                for (int r = 0; r < NX; ++r) t += G[r][cc] * dx0[r];
+                    for (int r = 0; r < NX; ++r) t += sh.G[cur][r][cc] * dx[r];
+                }
                 nu_[cc] = t;
             }
             ldl_solve1<NC>(L, nc, perm, nu_);
         } else if (negsum) {
             return 1;
         }
-        // forward sweep
-        double dx[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dx[i] = dx0[i];
+        PROF_T(r3);
+        // forward sweep (every lane carries dx; no barriers): dv = k + K dx + Kn nu, dx+ = A dx + B dv + c
         for (int k = 0; k <= N; ++k) {
             const int nv = (k < N ? NU : 0) + ns;
-            double dvv[NV];
+            const double* slot = SL + (size_t)k * SLOT;
+            double dv[NV];
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                dvv[v] = 0;
-                if (v >= nv) continue;
-                double t = AT(kf, k * dm.nv + v);
+                double t = slot[rk + v];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) t += AT(Kf, (k * dm.nv + v) * NX + j) * dx[j];
+                for (int j = 0; j < NX; ++j) t += slot[rK + v * NX + j] * dx[j];
 #pragma unroll
-                for (int cc = 0; cc < NC; ++cc)
-                    if (cc < nc) t += AT(Kn, (k * dm.nv + v) * nc + cc) * nu_[cc];
-                dvv[v] = t;
+                for (int cc = 0; cc < NC; ++cc) t += slot[rKn + v * NC + cc] * nu_[cc];
+                dv[v] = t;
             }
+            double mine = 0;
 #pragma unroll
-            for (int i = 0; i < NX; ++i) AT(dX, k * NX + i) = dx[i];
-            if (k < N)
-#pragma unroll
-                for (int i = 0; i < NU; ++i) AT(dU, k * NU + i) = dvv[i];
-            if (ns) AT(dS, k) = dvv[nv - 1];
-            if (k == 0) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double t = AT(pv, i);
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) t += AT(Pm, i * NX + j) * dx[j];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc)
-                        if (cc < nc) t += AT(Gm, i * nc + cc) * nu_[cc];
-                    AT(yi_n, i) = -t;
-                }
-            }
+            for (int i = 0; i < NX; ++i)
+                if (i == lane) mine = dx[i];
+            if (lane < NX) AT(dX, k * NX + lane) = mine;
             if (k < N) {
-                double x[NX], u[NU], A[NX][NX], Bu[NX][NU], dn[NX];
+                double dvl = 0;
 #pragma unroll
-                for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
-#pragma unroll
-                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
-                D::jac(x, u, p.dt, p.wheelbase, A, Bu);
+                for (int v = 0; v < NU; ++v)
+                    if (v == lane) dvl = dv[v];
+                if (lane < NU) AT(dU, k * NU + lane) = dvl;
+            }
+            if (ns && lane == 0) AT(dS, k) = k < N ? dv[NU] : dv[0];
+            if (k < N) {
+                double dn[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    double t = mode == MODE_NEWTON ? -AT(rcd, k * NX + i) : 0.0;
+                    double t = slot[sc + i];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) t += A[i][j] * dx[j];
-#pragma unroll
-                    for (int j = 0; j < NU; ++j) t += Bu[i][j] * dvv[j];
+                    for (int j = 0; j < NZ; ++j) {
+                        const double z = j < NX ? dx[j] : (j - NX < nv ? dv[j - NX] : 0.0);
+                        t += slot[sAB + i * NZ + j] * z;
+                    }
                     dn[i] = t;
-                }
-                double Mk[2][2];
-                cross(p, ws, b, k, mode, Mk);
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double t = AT(pv, (k + 1) * NX + i);
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) t += AT(Pm, ((k + 1) * NX + i) * NX + j) * dn[j];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc)
-                        if (cc < nc) t += AT(Gm, ((k + 1) * NX + i) * nc + cc) * nu_[cc];
-                    double mt = i < 2 ? Mk[0][i] * dx[0] + Mk[1][i] * dx[1] : 0.0;
-                    AT(yk_n, k * NX + i) = -t - mt;
                 }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) dx[i] = dn[i];
             }
         }
+        wsync();  // dX visible to every lane
+        // equality multipliers in parallel over knots: y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k,
+        // y_init = -grad V_0(dx_0)
+        for (int k = lane - 1; k < N; k += 64) {
+            const double* s1 = SL + (size_t)(k + 1) * SLOT;
+            double xn[NX];
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
-            if (cc < nc) AT(yt_n, cc) = nu_[cc];
+            for (int j = 0; j < NX; ++j) xn[j] = AT(dX, (k + 1) * NX + j);
+            double mx0 = 0, mx1 = 0;
+            if (k >= 0) {
+                const double* s0 = SL + (size_t)k * SLOT;
+                const double d0 = AT(dX, k * NX), d1 = AT(dX, k * NX + 1);
+                mx0 = s0[sM + 0] * d0 + s0[sM + 2] * d1;
+                mx1 = s0[sM + 1] * d0 + s0[sM + 3] * d1;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double t = s1[rp + i];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) t += s1[rP + i * NX + j] * xn[j];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += s1[rG + i * NC + cc] * nu_[cc];
+                if (k < 0) {
+                    AT(yi_n, i) = -t;
+                } else {
+                    const double mt = i == 0 ? mx0 : (i == 1 ? mx1 : 0.0);
+                    AT(yk_n, k * NX + i) = -t - mt;
+                }
+            }
+        }
+        if (lane < nc) {
+            double v = 0;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc)
+                if (cc == lane) v = nu_[cc];
+            AT(yt_n, lane) = v;
+        }
+        wsync();
+#ifdef NLOT_PHASE_PROF
+        PROF_T(r4);
+        if (b == 0 && lane == 0 && mode == MODE_NEWTON && SC(SC_ITERS) < 4)
+            printf("RIC build %lld back %lld [PAB %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", r1 - r0,
+                   r2 - r1, pa, pb, pc, pd, r3 - r2, r4 - r3);
+#endif
         return 0;
     }
 };
 
 // ---------------------------------------------------------------------------------------------
-// kernels
+// kernels (one 64-lane workgroup = one instance; grid = active instances)
 // ---------------------------------------------------------------------------------------------
-__global__ void k_init_state(NlotProblem p, Dims dm, NlotSolverOptions o, Ws ws, const double* __restrict__ x0,
-                             const double* __restrict__ xg, const double* __restrict__ Xinit, int B) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+__global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
+                                                   const double* __restrict__ x0, const double* __restrict__ xg,
+                                                   const double* __restrict__ Xinit) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const int b = blockIdx.x, lane = threadIdx.x;
     const int N = dm.N, nx = dm.nx, nu = dm.nu, M = dm.M;
     const double k1 = o.bound_push, k2 = o.bound_frac;
-    for (int k = 0; k <= N; ++k)
-        for (int i = 0; i < nx; ++i) {
-            double v;
-            if (Xinit) v = Xinit[((size_t)b * (N + 1) + k) * nx + i];
-            else v = x0[(size_t)b * nx + i] + (xg[(size_t)b * nx + i] - x0[(size_t)b * nx + i]) * ((double)k / (double)N);
-            AT(X, k * nx + i) = v;  // LinearInitializer (trajectory_initialization.py:54-55)
-        }
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nu; ++i) {
-            const double lo = p.umin[i], hi = p.umax[i];
-            const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
-            const double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
-            AT(U, k * nu + i) = fmin(fmax(0.0, lo + pl), hi - pu);
-            AT(zl, k * nu + i) = 1.0;
-            AT(zu, k * nu + i) = 1.0;
-        }
-    for (int k = 0; k <= N; ++k) {
+    for (int e = lane; e < (N + 1) * nx; e += 64) {
+        const int k = e / nx, i = e % nx;
+        const double v = Xinit ? Xinit[((size_t)b * (N + 1) + k) * nx + i]
+                               : x0[(size_t)b * nx + i] + (xg[(size_t)b * nx + i] - x0[(size_t)b * nx + i]) * ((double)k / (double)N);
+        AT(X, e) = v;  // LinearInitializer (trajectory_initialization.py:54-55)
+        AT(dX, e) = 0.0;
+    }
+    for (int e = lane; e < N * nu; e += 64) {
+        const int i = e % nu;
+        const double lo = p.umin[i], hi = p.umax[i];
+        const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+        const double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+        AT(U, e) = fmin(fmax(0.0, lo + pl), hi - pu);
+        AT(zl, e) = 1.0;
+        AT(zu, e) = 1.0;
+        AT(dU, e) = 0.0;
+    }
+    for (int k = lane; k <= N; k += 64) {
         AT(S, k) = dm.ns ? fmax(0.0, k1) : 0.0;
         AT(zs, k) = 1.0;
         AT(dS, k) = 0.0;
     }
-    for (int i = 0; i < (N + 1) * nx; ++i) AT(dX, i) = 0.0;  // step arrays start defined (0 * garbage = NaN)
-    for (int i = 0; i < N * nu; ++i) AT(dU, i) = 0.0;
-    for (int q = 0; q < (N + 1) * M; ++q) AT(dT, q) = 0.0;
-    for (int q = 0; q < (N + 1) * M; ++q) AT(vt, q) = 1.0;
-    SC(SC_MU) = o.mu_init;
-    SC(SC_TAU) = fmax(0.99, 1.0 - o.mu_init);
-    SC(SC_DWLAST) = 0;
-    SC(SC_STATUS) = -1;
-    SC(SC_ITERS) = 0;
-    SC(SC_PHASE) = PH_INIT;
-    SC(SC_NFILT) = 0;
-    SC(SC_E0) = 0;
+    for (int q = lane; q < (N + 1) * M; q += 64) {
+        AT(vt, q) = 1.0;
+        AT(dT, q) = 0.0;
+    }
+    if (lane == 0) {
+        SC(SC_MU) = o.mu_init;
+        SC(SC_TAU) = fmax(0.99, 1.0 - o.mu_init);
+        SC(SC_DWLAST) = 0;
+        SC(SC_STATUS) = -1;
+        SC(SC_ITERS) = 0;
+        SC(SC_PHASE) = PH_INIT;
+        SC(SC_NFILT) = 0;
+        SC(SC_E0) = 0;
+        ws.act[0][b] = b;
+    }
 }
 
-// corners of X (+ alpha dX) for instances in the given phases, compacted into the MLP point list
-__global__ void k_points(NlotProblem p, Dims dm, Ws ws, int B, int trial) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+// number of step lengths evaluated in this line-search round: alpha_max alone in the first round,
+// afterwards the next NSPEC halvings that stay >= alpha_min (speculative backtracking: the same
+// accepted alpha as sequential halving, because the acceptance test of one candidate does not
+// depend on the others)
+__device__ __forceinline__ int n_candidates(const Ws& ws, int b) {
+    if (SC(SC_TRIALS) == 0) return 1;
+    const double amin = SC(SC_AMIN);
+    double a = SC(SC_ALPHA);
+    int n = 1;
+    for (int j = 1; j < NSPEC; ++j) {
+        a *= 0.5;
+        if (a < amin) break;
+        ++n;
+    }
+    return n;
+}
+
+// corners of X (+ alpha dX) of instances in the wanted phase, appended to the compacted point list
+__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, const int* __restrict__ active, int trial) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const int b = active[blockIdx.x], lane = threadIdx.x;
     const int ph = (int)SC(SC_PHASE);
     const bool want = trial ? ph == PH_LS : (ph == PH_INIT || ph == PH_EVAL);
     if (!want) return;
-    const int rank = atomicAdd(&ws.cnt[trial ? 1 : 0], 1);
-    SC(SC_RANK) = rank;
-    const double al = trial ? SC(SC_ALPHA) : 0.0;
-    const int nx = dm.nx;
-    for (int k = 0; k <= dm.N; ++k) {
+    // trial: the first round evaluates alpha_max; later rounds the next NSPEC halvings that stay
+    // >= alpha_min (speculative backtracking, identical outcome to sequential halving)
+    const int ncand = trial ? n_candidates(ws, b) : 1;
+    const double a0 = trial ? SC(SC_ALPHA) : 0.0;
+    int rank = 0;
+    if (lane == 0) {
+        rank = atomicAdd(&ws.cnt[trial ? 1 : 0], ncand);
+        SC(SC_RANK) = rank;
+        SC(SC_NCAND) = ncand;
+    }
+    rank = __shfl(rank, 0);
+    const int nx = dm.nx, nb = dm.nb;
+    for (int cnd = 0; cnd < ncand; ++cnd) {
+    const double al = trial ? ldexp(a0, -cnd) : 0.0;
+    const size_t base = (size_t)(rank + cnd) * dm.ppk * (dm.N + 1);
+    for (int e = lane; e < (dm.N + 1) * nb; e += 64) {
+        const int k = e / nb, i = e % nb;
         const double x = AT(X, k * nx) + al * AT(dX, k * nx);
         const double y = AT(X, k * nx + 1) + al * AT(dX, k * nx + 1);
+        float px, py;
         if (p.shape == NLOT_SHAPE_DOT) {
-            const size_t o = ((size_t)k * ws.cap + rank) * 2;
-            ws.pts[o] = (float)x;  // CasADi double -> fp32 (gen/nn_sdf.cpp)
-            ws.pts[o + 1] = (float)y;
-            continue;
-        }
-        const double th = AT(X, k * nx + 2) + al * AT(dX, k * nx + 2);
-        double sn, cs;
-        sincos(th, &sn, &cs);
-        for (int i = 0; i < dm.nb; ++i) {
+            px = (float)x;  // CasADi double -> fp32 (gen/nn_sdf.cpp)
+            py = (float)y;
+        } else {
+            const double th = AT(X, k * nx + 2) + al * AT(dX, k * nx + 2);
+            double sn, cs;
+            sincos(th, &sn, &cs);
             const double bx = p.body[i][0], by = p.body[i][1];
-            const size_t o = ((size_t)(k * dm.nb + i) * ws.cap + rank) * 2;
-            ws.pts[o] = (float)(x + cs * bx - sn * by);
-            ws.pts[o + 1] = (float)(y + sn * bx + cs * by);
+            px = (float)(x + cs * bx - sn * by);
+            py = (float)(y + sn * bx + cs * by);
         }
+        ws.pts[(base + e) * 2] = px;
+        ws.pts[(base + e) * 2 + 1] = py;
+    }
     }
 }
 
@@ -836,64 +966,93 @@ __device__ inline double frac_to_bound(double sl, double dsl, double tau, double
     }
     return amax;
 }
+__device__ inline int cmp_le(double lhs, double rhs, double bas) {
+    return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(bas);
+}
 
-template <int DYN>
-__global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolverOptions o, Ws ws, int B,
-                                                const double* __restrict__ x0, const double* __restrict__ xg) {
+// objective at X + al dX (runner.py:80-96), wave-parallel
+__device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, double al) {
+    const int nx = dm.nx, nu = dm.nu, N = dm.N;
+    double f = 0;
+    for (int k = lane; k < N; k += 64) {
+        const double dx = (AT(X, (k + 1) * nx) + al * AT(dX, (k + 1) * nx)) - (AT(X, k * nx) + al * AT(dX, k * nx));
+        const double dy = (AT(X, (k + 1) * nx + 1) + al * AT(dX, (k + 1) * nx + 1)) -
+                          (AT(X, k * nx + 1) + al * AT(dX, k * nx + 1));
+        f += sqrt(dx * dx + dy * dy + p.path_eps);
+    }
+    double sq = 0, uq = 0;
+    if (p.use_slack)
+        for (int k = lane; k <= N; k += 64) {
+            const double s = AT(S, k) + al * AT(dS, k);
+            sq += s * s;
+        }
+    if (p.use_smooth)
+        for (int e = lane; e < (N - 1) * nu; e += 64) {
+            const double u = AT(U, e) + al * AT(dU, e);
+            uq += u * u;
+        }
+    return wsum(f) + p.slack_penalty * wsum(sq) + p.smooth_weight * wsum(uq);
+}
+
+template <int DYN, bool LDS>
+__global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+                                                const int* __restrict__ active, const double* __restrict__ x0,
+                                                const double* __restrict__ xg) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
     using SV = Solver<DYN>;
     constexpr int NX = SV::NX, NU = SV::NU;
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    const int b = active[blockIdx.x], lane = threadIdx.x;
     const int ph = (int)SC(SC_PHASE);
     if (ph != PH_INIT && ph != PH_EVAL) return;
+    __shared__ typename SV::Sh sh;
+    extern __shared__ double lds_slots[];  // (N+1) Riccati stage slots when they fit (LDS), else unused
+    double* SL = LDS ? lds_slots : &AT(stg, 0);
     const int N = dm.N, M = dm.M, nc = dm.nc;
     const int rank = (int)SC(SC_RANK);
     const double k1 = o.bound_push;
     const double* x0b = x0 + (size_t)b * NX;
     const double* xgb = xg + (size_t)b * NX;
 
-    // ---- knot data: d, J_d (y_d-weighted Hessian later) ----
     auto eval_knots = [&](bool with_hess) {
-        for (int k = 0; k <= N; ++k) {
+        for (int k = lane; k <= N; k += 64) {
             double xk[NX], d[MMAX], gk[MMAX][3], w[MMAX], Hw[6];
 #pragma unroll
             for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i);
-            for (int j = 0; j < M; ++j) w[j] = AT(yd, k * M + j);
+#pragma unroll
+            for (int j = 0; j < MMAX; ++j) w[j] = (with_hess && j < M) ? AT(yd, k * M + j) : 0.0;
             knot_eval(p, dm, ws, rank, k, xk, d, gk, w, with_hess ? Hw : nullptr);
-            for (int j = 0; j < M; ++j) {
-                const double dj = d[j] + (dm.sd ? AT(S, k) : 0.0);
-                AT(dv, k * M + j) = dj;
+#pragma unroll
+            for (int j = 0; j < MMAX; ++j) {
+                if (j >= M) break;
+                AT(dv, k * M + j) = d[j] + (dm.sd ? AT(S, k) : 0.0);
+#pragma unroll
                 for (int a = 0; a < 3; ++a) AT(Jd, (k * M + j) * 3 + a) = gk[j][a];
             }
             if (with_hess)
                 for (int q = 0; q < 6; ++q) AT(Hd, k * 6 + q) = Hw[q];
         }
+        wsync();
     };
-    auto residuals = [&]() {  // c(x) at the current point (IPOPT sign)
-#pragma unroll
-        for (int i = 0; i < NX; ++i) AT(rci, i) = AT(X, i) - x0b[i];
-        for (int cc = 0; cc < nc; ++cc) AT(rct, cc) = AT(X, N * NX + dm.tidx[cc]) - xgb[dm.tidx[cc]];
-        for (int k = 0; k < N; ++k) {
-            double x[NX], u[NU], f[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
-            Dyn<DYN>::f(x, u, p.wheelbase, f);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
-        }
-        for (int q = 0; q < (N + 1) * M; ++q) AT(rcq, q) = AT(dv, q) - AT(T, q);
+    auto zero_mults = [&]() {
+        for (int i = lane; i < NX; i += 64) AT(yi, i) = 0;
+        for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0;
+        for (int i = lane; i < nc; i += 64) AT(yt, i) = 0;
+        for (int q = lane; q < (N + 1) * M; q += 64) AT(yd, q) = 0;
     };
 
     if (ph == PH_INIT) {
         eval_knots(false);
-        for (int q = 0; q < (N + 1) * M; ++q) AT(T, q) = fmax(AT(dv, q), k1);  // slack push
-        for (int q = 0; q < (N + 1) * M; ++q) AT(yd, q) = 0.0;
+        for (int q = lane; q < (N + 1) * M; q += 64) {
+            AT(T, q) = fmax(AT(dv, q), k1);  // slack push
+            AT(yd, q) = 0.0;
+        }
+        wsync();
         // least-squares equality multipliers (IPOPT LeastSquareMultipliers)
-        if (SV::riccati(p, dm, ws, b, MODE_LSQ, 0.0) == 0) {
+        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, sh, SL) == 0) {
             double ymax = 0;
-            for (int k = 0; k <= N; ++k)
+            for (int k = lane; k <= N; k += 64)
                 for (int j = 0; j < M; ++j) {
                     double w = 0;
                     for (int a = 0; a < 3 && a < NX; ++a) w += AT(Jd, (k * M + j) * 3 + a) * AT(dX, k * NX + a);
@@ -902,172 +1061,187 @@ __global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolv
                     AT(yd, k * M + j) = v;
                     ymax = fmax(ymax, fabs(v));
                 }
-            for (int i = 0; i < NX; ++i) ymax = fmax(ymax, fabs(AT(yi, i) = AT(yi_n, i)));
-            for (int i = 0; i < N * NX; ++i) ymax = fmax(ymax, fabs(AT(yk, i) = AT(yk_n, i)));
-            for (int cc = 0; cc < nc; ++cc) ymax = fmax(ymax, fabs(AT(yt, cc) = AT(yt_n, cc)));
-            if (ymax > o.constr_mult_init_max) {
-                for (int i = 0; i < NX; ++i) AT(yi, i) = 0;
-                for (int i = 0; i < N * NX; ++i) AT(yk, i) = 0;
-                for (int cc = 0; cc < nc; ++cc) AT(yt, cc) = 0;
-                for (int q = 0; q < (N + 1) * M; ++q) AT(yd, q) = 0;
-            }
+            for (int i = lane; i < NX; i += 64) ymax = fmax(ymax, fabs(AT(yi, i) = AT(yi_n, i)));
+            for (int i = lane; i < N * NX; i += 64) ymax = fmax(ymax, fabs(AT(yk, i) = AT(yk_n, i)));
+            for (int i = lane; i < nc; i += 64) ymax = fmax(ymax, fabs(AT(yt, i) = AT(yt_n, i)));
+            ymax = wmax(ymax);
+            wsync();
+            if (ymax > o.constr_mult_init_max) zero_mults();
         } else {
-            for (int i = 0; i < NX; ++i) AT(yi, i) = 0;
-            for (int i = 0; i < N * NX; ++i) AT(yk, i) = 0;
-            for (int cc = 0; cc < nc; ++cc) AT(yt, cc) = 0;
-            for (int q = 0; q < (N + 1) * M; ++q) AT(yd, q) = 0;
+            zero_mults();
         }
+        wsync();
     }
+    PROF_T(t0);
     eval_knots(true);
-    residuals();
+    // residuals c(x) (IPOPT sign)
+    for (int i = lane; i < NX; i += 64) AT(rci, i) = AT(X, i) - x0b[i];
+    for (int i = lane; i < nc; i += 64) AT(rct, i) = AT(X, N * NX + dm.tidx[i]) - xgb[dm.tidx[i]];
+    for (int k = lane; k < N; k += 64) {
+        double x[NX], u[NU], f[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+        for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+        Dyn<DYN>::f(x, u, p.wheelbase, f);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
+    }
+    for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) = AT(dv, q) - AT(T, q);
+    wsync();
 
-    // ---- theta / phi at the current point ----
-    const double mu0 = SC(SC_MU);
-    auto theta_phi = [&](double mu, double* th, double* ph_) {
+    auto theta_phi = [&](double mu, double* th, double* phv) {
         double t = 0, bar = 0, lin = 0;
-        for (int i = 0; i < NX; ++i) t += fabs(AT(rci, i));
-        for (int cc = 0; cc < nc; ++cc) t += fabs(AT(rct, cc));
-        for (int i = 0; i < N * NX; ++i) t += fabs(AT(rcd, i));
-        for (int q = 0; q < (N + 1) * M; ++q) {
+        for (int i = lane; i < NX; i += 64) t += fabs(AT(rci, i));
+        for (int i = lane; i < nc; i += 64) t += fabs(AT(rct, i));
+        for (int i = lane; i < N * NX; i += 64) t += fabs(AT(rcd, i));
+        for (int q = lane; q < (N + 1) * M; q += 64) {
             t += fabs(AT(rcq, q));
             bar += log(AT(T, q));
             lin += AT(T, q);
         }
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < NU; ++i) {
-                const double u = AT(U, k * NU + i);
-                bar += log(u - p.umin[i]) + log(p.umax[i] - u);
-            }
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
+        }
         if (dm.ns)
-            for (int k = 0; k <= N; ++k) {
+            for (int k = lane; k <= N; k += 64) {
                 bar += log(AT(S, k));
                 lin += AT(S, k);
             }
-        *th = t;
-        *ph_ = objective(p, dm, ws, b, nullptr, nullptr, nullptr, 0.0) - mu * bar + 1e-5 * mu * lin;
+        *th = wsum(t);
+        const double fo = objective_w(p, dm, ws, b, lane, 0.0);
+        *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
     };
+    PROF_T(t1);
+    const double mu0 = SC(SC_MU);
     if (ph == PH_INIT) {
         double th0, p0;
         theta_phi(mu0, &th0, &p0);
-        SC(SC_THMAX) = 1e4 * fmax(1.0, th0);
-        SC(SC_THMIN) = 1e-4 * fmax(1.0, th0);
-        SC(SC_NFILT) = 0;
+        if (lane == 0) {
+            SC(SC_THMAX) = 1e4 * fmax(1.0, th0);
+            SC(SC_THMIN) = 1e-4 * fmax(1.0, th0);
+            SC(SC_NFILT) = 0;
+        }
     }
 
     // ---- optimality measures (IPOPT scaled E_0 / E_mu) ----
-    double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0;
-    int nzc = 0;
-    {
-        for (int k = 0; k <= N; ++k) {
-            double r[NX];
-            // objective gradient w.r.t. x_k (path length)
+    double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0, nzc = 0;
+    for (int k = lane; k <= N; k += 64) {
+        double r[NX];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) r[i] = 0;
-            for (int seg = k - 1; seg <= k; ++seg) {
-                if (seg < 0 || seg >= N) continue;
-                const double dx = AT(X, (seg + 1) * NX) - AT(X, seg * NX);
-                const double dy = AT(X, (seg + 1) * NX + 1) - AT(X, seg * NX + 1);
-                const double rr = sqrt(dx * dx + dy * dy + p.path_eps);
-                const double sgn = seg == k ? -1.0 : 1.0;
-                r[0] += sgn * dx / rr;
-                r[1] += sgn * dy / rr;
+        for (int i = 0; i < NX; ++i) r[i] = 0;
+        for (int seg = k - 1; seg <= k; ++seg) {
+            if (seg < 0 || seg >= N) continue;
+            const double dx = AT(X, (seg + 1) * NX) - AT(X, seg * NX);
+            const double dy = AT(X, (seg + 1) * NX + 1) - AT(X, seg * NX + 1);
+            const double rr = sqrt(dx * dx + dy * dy + p.path_eps);
+            const double sgn = seg == k ? -1.0 : 1.0;
+            r[0] += sgn * dx / rr;
+            r[1] += sgn * dy / rr;
+        }
+        if (k > 0)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) r[i] += AT(yk, (k - 1) * NX + i);
+        double A[NX][NX], Bu[NX][NU];
+        if (k < N) {
+            double x[NX], u[NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+            for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+            Dyn<DYN>::jac(x, u, p.dt, p.wheelbase, A, Bu);
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                double t = 0;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) t += A[i][j] * AT(yk, k * NX + i);
+                r[j] -= t;
             }
-            if (k > 0)
+        }
+        if (k == 0)
 #pragma unroll
-                for (int i = 0; i < NX; ++i) r[i] += AT(yk, (k - 1) * NX + i);
-            double A[NX][NX], Bu[NX][NU];
-            if (k < N) {
-                double x[NX], u[NU];
+            for (int i = 0; i < NX; ++i) r[i] += AT(yi, i);
+        if (k == N)
 #pragma unroll
-                for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+            for (int i = 0; i < NX; ++i)
+                for (int cc = 0; cc < nc; ++cc)
+                    if (dm.tidx[cc] == i) r[i] += AT(yt, cc);
+        for (int j = 0; j < M; ++j)
+            for (int a = 0; a < 3 && a < NX; ++a) r[a] += AT(Jd, (k * M + j) * 3 + a) * AT(yd, k * M + j);
 #pragma unroll
-                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
-                Dyn<DYN>::jac(x, u, p.dt, p.wheelbase, A, Bu);
+        for (int i = 0; i < NX; ++i) dual = fmax(dual, fabs(r[i]));
+        if (k < N)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) {
-                    double t = 0;
+            for (int i = 0; i < NU; ++i) {
+                double t = -AT(zl, k * NU + i) + AT(zu, k * NU + i);
+                if (p.use_smooth && k < N - 1) t += 2.0 * p.smooth_weight * AT(U, k * NU + i);
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) t += A[i][j] * AT(yk, k * NX + i);
-                    r[j] -= t;
-                }
-            }
-            if (k == 0)
-#pragma unroll
-                for (int i = 0; i < NX; ++i) r[i] += AT(yi, i);
-            if (k == N)
-                for (int cc = 0; cc < nc; ++cc) r[dm.tidx[cc]] += AT(yt, cc);
-            for (int j = 0; j < M; ++j)
-                for (int a = 0; a < 3 && a < NX; ++a) r[a] += AT(Jd, (k * M + j) * 3 + a) * AT(yd, k * M + j);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) dual = fmax(dual, fabs(r[i]));
-            if (k < N)
-#pragma unroll
-                for (int i = 0; i < NU; ++i) {
-                    double t = -AT(zl, k * NU + i) + AT(zu, k * NU + i);
-                    if (p.use_smooth && k < N - 1) t += 2.0 * p.smooth_weight * AT(U, k * NU + i);
-#pragma unroll
-                    for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
-                    dual = fmax(dual, fabs(t));
-                }
-            if (dm.ns) {
-                double t = 2.0 * p.slack_penalty * AT(S, k) - AT(zs, k);
-                if (dm.sd)
-                    for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
+                for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
                 dual = fmax(dual, fabs(t));
             }
-            for (int j = 0; j < M; ++j) dual = fmax(dual, fabs(-AT(yd, k * M + j) - AT(vt, k * M + j)));
+        if (dm.ns) {
+            double t = 2.0 * p.slack_penalty * AT(S, k) - AT(zs, k);
+            if (dm.sd)
+                for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
+            dual = fmax(dual, fabs(t));
         }
-        for (int i = 0; i < NX; ++i) primal = fmax(primal, fabs(AT(rci, i)));
-        for (int cc = 0; cc < nc; ++cc) primal = fmax(primal, fabs(AT(rct, cc)));
-        for (int i = 0; i < N * NX; ++i) primal = fmax(primal, fabs(AT(rcd, i)));
-        cviol = primal;
-        for (int q = 0; q < (N + 1) * M; ++q) {
-            primal = fmax(primal, fabs(AT(rcq, q)));
-            cviol = fmax(cviol, fmax(0.0, -AT(dv, q)));
-        }
-        auto compl_ = [&](double z, double s) {
-            c0 = fmax(c0, fabs(z * s));
-            cmu = fmax(cmu, fabs(z * s - mu0));
-            zsum += fabs(z);
-            nzc++;
-        };
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < NU; ++i) {
-                const double u = AT(U, k * NU + i);
-                compl_(AT(zl, k * NU + i), u - p.umin[i]);
-                compl_(AT(zu, k * NU + i), p.umax[i] - u);
-            }
-        if (dm.ns)
-            for (int k = 0; k <= N; ++k) compl_(AT(zs, k), AT(S, k));
-        for (int q = 0; q < (N + 1) * M; ++q) compl_(AT(vt, q), AT(T, q));
-        for (int i = 0; i < NX; ++i) ysum += fabs(AT(yi, i));
-        for (int i = 0; i < N * NX; ++i) ysum += fabs(AT(yk, i));
-        for (int cc = 0; cc < nc; ++cc) ysum += fabs(AT(yt, cc));
-        for (int q = 0; q < (N + 1) * M; ++q) ysum += fabs(AT(yd, q));
+        for (int j = 0; j < M; ++j) dual = fmax(dual, fabs(-AT(yd, k * M + j) - AT(vt, k * M + j)));
     }
-    const int ny = NX + N * NX + nc + (N + 1) * M;
-    const double sd = fmax(100.0, (ysum + zsum) / (double)(ny + nzc)) / 100.0;
-    const double scc = fmax(100.0, zsum / (double)nzc) / 100.0;
+    for (int i = lane; i < NX; i += 64) primal = fmax(primal, fabs(AT(rci, i)));
+    for (int i = lane; i < nc; i += 64) primal = fmax(primal, fabs(AT(rct, i)));
+    for (int i = lane; i < N * NX; i += 64) primal = fmax(primal, fabs(AT(rcd, i)));
+    cviol = wmax(primal);
+    for (int q = lane; q < (N + 1) * M; q += 64) {
+        primal = fmax(primal, fabs(AT(rcq, q)));
+        cviol = fmax(cviol, fmax(0.0, -AT(dv, q)));
+    }
+    auto compl_ = [&](double z, double s) {
+        c0 = fmax(c0, fabs(z * s));
+        cmu = fmax(cmu, fabs(z * s - mu0));
+        zsum += fabs(z);
+        nzc += 1;
+    };
+    for (int e = lane; e < N * NU; e += 64) {
+        const double u = AT(U, e);
+        compl_(AT(zl, e), u - p.umin[e % NU]);
+        compl_(AT(zu, e), p.umax[e % NU] - u);
+    }
+    if (dm.ns)
+        for (int k = lane; k <= N; k += 64) compl_(AT(zs, k), AT(S, k));
+    for (int q = lane; q < (N + 1) * M; q += 64) compl_(AT(vt, q), AT(T, q));
+    for (int i = lane; i < NX; i += 64) ysum += fabs(AT(yi, i));
+    for (int i = lane; i < N * NX; i += 64) ysum += fabs(AT(yk, i));
+    for (int i = lane; i < nc; i += 64) ysum += fabs(AT(yt, i));
+    for (int q = lane; q < (N + 1) * M; q += 64) ysum += fabs(AT(yd, q));
+    dual = wmax(dual);
+    primal = wmax(primal);
+    cviol = wmax(cviol);
+    c0 = wmax(c0);
+    cmu = wmax(cmu);
+    zsum = wsum(zsum);
+    ysum = wsum(ysum);
+    nzc = wsum(nzc);
+    const double ny = NX + N * NX + nc + (N + 1) * M;
+    const double sd = fmax(100.0, (ysum + zsum) / (ny + nzc)) / 100.0;
+    const double scc = fmax(100.0, zsum / nzc) / 100.0;
     const double E0 = fmax(fmax(dual / sd, primal), c0 / scc);
-    SC(SC_E0) = E0;
     const int iters = (int)SC(SC_ITERS);
-    if (!isfinite(E0)) {
-        SC(SC_STATUS) = NLOT_NUMERIC;
-        SC(SC_PHASE) = PH_DONE;
-        return;
-    }
-    if (E0 <= o.tol && dual <= o.dual_inf_tol && cviol <= o.constr_viol_tol && c0 <= o.compl_inf_tol) {
-        SC(SC_STATUS) = NLOT_SOLVED;
-        SC(SC_PHASE) = PH_DONE;
-        return;
-    }
-    if (iters >= o.max_iter) {
-        SC(SC_STATUS) = NLOT_MAXITER;
-        SC(SC_PHASE) = PH_DONE;
-        return;
-    }
+    wsync();
+    auto finish = [&](int status) {
+        if (lane == 0) {
+            SC(SC_E0) = E0;
+            SC(SC_STATUS) = status;
+            SC(SC_PHASE) = PH_DONE;
+        }
+    };
+    if (!isfinite(E0)) return finish(NLOT_NUMERIC);
+    if (E0 <= o.tol && dual <= o.dual_inf_tol && cviol <= o.constr_viol_tol && c0 <= o.compl_inf_tol)
+        return finish(NLOT_SOLVED);
+    if (iters >= o.max_iter) return finish(NLOT_MAXITER);
     // ---- monotone barrier update ----
-    double mu = mu0;
+    double mu = mu0, tau = SC(SC_TAU);
+    bool reset_filter = false;
     if (iters > 0) {
         const double kap = o.barrier_tol_factor;
         double cm = cmu;
@@ -1078,42 +1252,48 @@ __global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolv
             nm = fmax(nm, fmin(o.tol, o.compl_inf_tol) / (kap + 1.0));
             if (nm >= mu) break;
             mu = nm;
-            SC(SC_MU) = mu;
-            SC(SC_TAU) = fmax(0.99, 1.0 - mu);
-            SC(SC_NFILT) = 0;
-            cm = 0;  // recompute the complementarity error for the new mu
-            for (int k = 0; k < N; ++k)
-                for (int i = 0; i < NU; ++i) {
-                    const double u = AT(U, k * NU + i);
-                    cm = fmax(cm, fabs(AT(zl, k * NU + i) * (u - p.umin[i]) - mu));
-                    cm = fmax(cm, fabs(AT(zu, k * NU + i) * (p.umax[i] - u) - mu));
-                }
+            tau = fmax(0.99, 1.0 - mu);
+            reset_filter = true;
+            cm = 0;
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e);
+                cm = fmax(cm, fabs(AT(zl, e) * (u - p.umin[e % NU]) - mu));
+                cm = fmax(cm, fabs(AT(zu, e) * (p.umax[e % NU] - u) - mu));
+            }
             if (dm.ns)
-                for (int k = 0; k <= N; ++k) cm = fmax(cm, fabs(AT(zs, k) * AT(S, k) - mu));
-            for (int q = 0; q < (N + 1) * M; ++q) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - mu));
+                for (int k = lane; k <= N; k += 64) cm = fmax(cm, fabs(AT(zs, k) * AT(S, k) - mu));
+            for (int q = lane; q < (N + 1) * M; q += 64) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - mu));
+            cm = wmax(cm);
         }
     }
+    wsync();
+    if (lane == 0) {
+        SC(SC_MU) = mu;
+        SC(SC_TAU) = tau;
+        if (reset_filter) SC(SC_NFILT) = 0;
+    }
+    wsync();
     // ---- search direction with inertia correction ----
+    PROF_T(t2);
+    int n_ric = 1;
     double dw = 0.0;
-    if (SV::riccati(p, dm, ws, b, MODE_NEWTON, 0.0)) {
+    if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, 0.0, sh, SL)) {
         const double last = SC(SC_DWLAST);
         dw = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
         for (;;) {
-            if (!SV::riccati(p, dm, ws, b, MODE_NEWTON, dw)) break;
+            ++n_ric;
+            if (!SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw, sh, SL)) break;
             dw *= (last == 0.0) ? 100.0 : 8.0;
             if (dw > 1e40) break;
         }
-        if (dw > 1e40) {
-            SC(SC_STATUS) = NLOT_NUMERIC;
-            SC(SC_PHASE) = PH_DONE;
-            return;
-        }
-        SC(SC_DWLAST) = dw;
+        if (dw > 1e40) return finish(NLOT_NUMERIC);
+        if (lane == 0) SC(SC_DWLAST) = dw;
     }
-    SC(SC_DW) = dw;
-    // ---- recover dt, yd+, dz ----
-    const double kappa_d = 1e-5, tau = SC(SC_TAU);
-    for (int k = 0; k <= N; ++k)
+    // ---- recover dt, yd+, dz; fraction to the boundary; line-search reference values ----
+    PROF_T(t3);
+    const double kappa_d = 1e-5;
+    double amax = 1.0, az = 1.0, gd = 0;
+    for (int k = lane; k <= N; k += 64) {
         for (int j = 0; j < M; ++j) {
             const int q = k * M + j;
             double Jdz = 0;
@@ -1121,48 +1301,23 @@ __global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolv
             if (dm.sd) Jdz += AT(dS, k);
             const double t = AT(T, q), v = AT(vt, q);
             const double dt_ = Jdz + AT(rcq, q);
+            const double dvt_ = mu / t - v - (v / t) * dt_;
             AT(dT, q) = dt_;
             AT(yd_n, q) = (v / t + dw) * dt_ + (-mu / t + kappa_d * mu);
-            AT(dvt, q) = mu / t - v - (v / t) * dt_;
+            AT(dvt, q) = dvt_;
+            amax = frac_to_bound(t, dt_, tau, amax);
+            az = frac_to_bound(v, dvt_, tau, az);
+            gd += (-mu / t + kappa_d * mu) * dt_;
         }
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < NU; ++i) {
-            const int q = k * NU + i;
-            const double u = AT(U, q), sl = u - p.umin[i], su = p.umax[i] - u, du = AT(dU, q);
-            AT(dzl, q) = mu / sl - AT(zl, q) - (AT(zl, q) / sl) * du;
-            AT(dzu, q) = mu / su - AT(zu, q) + (AT(zu, q) / su) * du;
+        if (dm.ns) {
+            const double s = AT(S, k), ds = AT(dS, k);
+            const double dzs_ = mu / s - AT(zs, k) - (AT(zs, k) / s) * ds;
+            AT(dzs, k) = dzs_;
+            amax = frac_to_bound(s, ds, tau, amax);
+            az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+            gd += (2.0 * p.slack_penalty * s - mu / s + kappa_d * mu) * ds;
         }
-    if (dm.ns)
-        for (int k = 0; k <= N; ++k) {
-            const double s = AT(S, k);
-            AT(dzs, k) = mu / s - AT(zs, k) - (AT(zs, k) / s) * AT(dS, k);
-        }
-    // ---- fraction to the boundary ----
-    double amax = 1.0, az = 1.0;
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < NU; ++i) {
-            const int q = k * NU + i;
-            const double u = AT(U, q);
-            amax = frac_to_bound(u - p.umin[i], AT(dU, q), tau, amax);
-            amax = frac_to_bound(p.umax[i] - u, -AT(dU, q), tau, amax);
-            az = frac_to_bound(AT(zl, q), AT(dzl, q), tau, az);
-            az = frac_to_bound(AT(zu, q), AT(dzu, q), tau, az);
-        }
-    if (dm.ns)
-        for (int k = 0; k <= N; ++k) {
-            amax = frac_to_bound(AT(S, k), AT(dS, k), tau, amax);
-            az = frac_to_bound(AT(zs, k), AT(dzs, k), tau, az);
-        }
-    for (int q = 0; q < (N + 1) * M; ++q) {
-        amax = frac_to_bound(AT(T, q), AT(dT, q), tau, amax);
-        az = frac_to_bound(AT(vt, q), AT(dvt, q), tau, az);
-    }
-    // ---- line-search reference values ----
-    double theta, phi;
-    theta_phi(mu, &theta, &phi);
-    double gd = 0;
-    for (int k = 0; k <= N; ++k) {  // objective gradient . d
-        for (int seg = k - 1; seg <= k; ++seg) {
+        for (int seg = k - 1; seg <= k; ++seg) {  // path-length gradient . dx_k
             if (seg < 0 || seg >= N) continue;
             const double dx = AT(X, (seg + 1) * NX) - AT(X, seg * NX);
             const double dy = AT(X, (seg + 1) * NX + 1) - AT(X, seg * NX + 1);
@@ -1171,20 +1326,27 @@ __global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolv
             gd += sgn * (dx / rr) * AT(dX, k * NX) + sgn * (dy / rr) * AT(dX, k * NX + 1);
         }
     }
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < NU; ++i) {
-            const int q = k * NU + i;
-            const double u = AT(U, q);
-            double gu = -mu / (u - p.umin[i]) + mu / (p.umax[i] - u);
-            if (p.use_smooth && k < N - 1) gu += 2.0 * p.smooth_weight * u;
-            gd += gu * AT(dU, q);
-        }
-    if (dm.ns)
-        for (int k = 0; k <= N; ++k) {
-            const double s = AT(S, k);
-            gd += (2.0 * p.slack_penalty * s - mu / s + kappa_d * mu) * AT(dS, k);
-        }
-    for (int q = 0; q < (N + 1) * M; ++q) gd += (-mu / AT(T, q) + kappa_d * mu) * AT(dT, q);
+    for (int e = lane; e < N * NU; e += 64) {
+        const int i = e % NU, k = e / NU;
+        const double u = AT(U, e), sl = u - p.umin[i], su = p.umax[i] - u, du = AT(dU, e);
+        const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * du;
+        const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * du;
+        AT(dzl, e) = dzl_;
+        AT(dzu, e) = dzu_;
+        amax = frac_to_bound(sl, du, tau, amax);
+        amax = frac_to_bound(su, -du, tau, amax);
+        az = frac_to_bound(AT(zl, e), dzl_, tau, az);
+        az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+        double gu = -mu / sl + mu / su;
+        if (p.use_smooth && k < N - 1) gu += 2.0 * p.smooth_weight * u;
+        gd += gu * du;
+    }
+    amax = wmin(amax);
+    az = wmin(az);
+    gd = wsum(gd);
+    wsync();
+    double theta, phi;
+    theta_phi(mu, &theta, &phi);
     const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3;
     double amin = gt;
     if (gd < 0) {
@@ -1192,54 +1354,78 @@ __global__ void __launch_bounds__(64) k_iterate(NlotProblem p, Dims dm, NlotSolv
         if (theta <= SC(SC_THMIN)) amin = fmin(amin, delta * pow(theta, sth) / pow(-gd, sph));
     }
     amin *= 0.05;
-    SC(SC_THETA) = theta;
-    SC(SC_PHI) = phi;
-    SC(SC_GD) = gd;
-    SC(SC_AMAX) = amax;
-    SC(SC_AMIN) = amin;
-    SC(SC_AZ) = az;
-    SC(SC_ALPHA) = amax;
-    SC(SC_TRIALS) = 0;
-    SC(SC_PHASE) = PH_LS;
+    wsync();
+#ifdef NLOT_PHASE_PROF
+    {
+        PROF_T(t4);
+        if (b == 0 && lane == 0)
+            printf("PROF it %d eval %lld opt %lld ric %lld n_ric %d rec %lld (x10ns)\n", iters, t1 - t0, t2 - t1,
+                   t3 - t2, n_ric, t4 - t3);
+    }
+#endif
+    if (lane == 0) {
+        SC(SC_E0) = E0;
+        SC(SC_DW) = dw;
+        SC(SC_THETA) = theta;
+        SC(SC_PHI) = phi;
+        SC(SC_GD) = gd;
+        SC(SC_AMAX) = amax;
+        SC(SC_AMIN) = amin;
+        SC(SC_AZ) = az;
+        SC(SC_ALPHA) = amax;
+        SC(SC_TRIALS) = 0;
+        SC(SC_PHASE) = PH_LS;
+    }
 }
 
-__device__ inline int cmp_le(double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(bas); }
-
 template <int DYN>
-__global__ void __launch_bounds__(64) k_accept(NlotProblem p, Dims dm, NlotSolverOptions o, Ws ws, int B,
+__global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+                                               const int* __restrict__ active, int* __restrict__ next,
                                                const double* __restrict__ x0, const double* __restrict__ xg) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
     constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    const int b = active[blockIdx.x], lane = threadIdx.x;
     int ph = (int)SC(SC_PHASE);
     if (ph == PH_LS) {
         const int N = dm.N, M = dm.M, nc = dm.nc;
-        const double al = SC(SC_ALPHA), mu = SC(SC_MU);
-        const int rank = (int)SC(SC_RANK);
+        const double a0 = SC(SC_ALPHA), mu = SC(SC_MU);
+        const int rank0 = (int)SC(SC_RANK), ncand = n_candidates(ws, b);
+        int ok = 0, ftype = 0, armijo = 0, cnd = 0;
+        double al = a0, th = 0, pht = 0;
+        const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
+        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
+        const int nf = (int)SC(SC_NFILT);
+        for (cnd = 0; cnd < ncand && !ok; ++cnd) {
+        al = ldexp(a0, -cnd);
+        const int rank = rank0 + cnd;
         const double* x0b = x0 + (size_t)b * NX;
         const double* xgb = xg + (size_t)b * NX;
         // theta and phi at the trial point x + al d
-        double th = 0, bar = 0, lin = 0;
-        for (int i = 0; i < NX; ++i) th += fabs(AT(X, i) + al * AT(dX, i) - x0b[i]);
-        for (int cc = 0; cc < nc; ++cc) {
+        double bar = 0, lin = 0;
+        th = 0;
+        for (int i = lane; i < NX; i += 64) th += fabs(AT(X, i) + al * AT(dX, i) - x0b[i]);
+        for (int cc = lane; cc < nc; cc += 64) {
             const int ix = N * NX + dm.tidx[cc];
             th += fabs(AT(X, ix) + al * AT(dX, ix) - xgb[dm.tidx[cc]]);
         }
-        for (int k = 0; k < N; ++k) {
-            double x[NX], u[NU], f[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i) + al * AT(dX, k * NX + i);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
-            Dyn<DYN>::f(x, u, p.wheelbase, f);
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-                th += fabs(AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (x[i] + p.dt * f[i]));
-        }
-        for (int k = 0; k <= N; ++k) {
-            double xk[NX], d[MMAX];
+        for (int k = lane; k <= N; k += 64) {
+            double xk[NX];
 #pragma unroll
             for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i) + al * AT(dX, k * NX + i);
+            if (k < N) {
+                double u[NU], f[NX];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
+                Dyn<DYN>::f(xk, u, p.wheelbase, f);
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+                    th += fabs(AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]));
+#pragma unroll
+                for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+            }
+            double d[MMAX];
             knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr);
             const double sk = AT(S, k) + al * AT(dS, k);
             for (int j = 0; j < M; ++j) {
@@ -1248,25 +1434,18 @@ __global__ void __launch_bounds__(64) k_accept(NlotProblem p, Dims dm, NlotSolve
                 bar += log(t);
                 lin += t;
             }
+            if (dm.ns) {
+                bar += log(sk);
+                lin += sk;
+            }
         }
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < NU; ++i) {
-                const double u = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
-                bar += log(u - p.umin[i]) + log(p.umax[i] - u);
-            }
-        if (dm.ns)
-            for (int k = 0; k <= N; ++k) {
-                const double s = AT(S, k) + al * AT(dS, k);
-                bar += log(s);
-                lin += s;
-            }
-        const double pht = objective(p, dm, ws, b, nullptr, nullptr, nullptr, al) - mu * bar + 1e-5 * mu * lin;
-        const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
-        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
+        th = wsum(th);
+        const double fo = objective_w(p, dm, ws, b, lane, al);
+        pht = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
         // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint
-        int ok = isfinite(th) && isfinite(pht) && th <= SC(SC_THMAX);
-        const int ftype = gd < 0 && al * pow(-gd, sph) > delta * pow(theta, sth);
-        const int armijo = cmp_le(pht - phi, eta * al * gd, phi);
+        ok = isfinite(th) && isfinite(pht) && th <= SC(SC_THMAX);
+        ftype = gd < 0 && al * pow(-gd, sph) > delta * pow(theta, sth);
+        armijo = cmp_le(pht - phi, eta * al * gd, phi);
         if (ok) {
             if (ftype && theta <= SC(SC_THMIN)) {
                 ok = armijo;
@@ -1278,17 +1457,18 @@ __global__ void __launch_bounds__(64) k_accept(NlotProblem p, Dims dm, NlotSolve
                 }
             }
         }
-        int nf = (int)SC(SC_NFILT);
-        if (ok)
-            for (int i = 0; i < nf; ++i) {
-                const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
-                if (!(th <= ft || pht <= fp)) {
-                    ok = 0;
-                    break;
-                }
-            }
         if (ok) {
-            if (!(ftype && armijo)) {  // augment the filter with (1-gt) theta, phi - gp theta
+            int bad = 0;
+            for (int i = lane; i < nf; i += 64) {
+                const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
+                if (!(th <= ft || pht <= fp)) bad = 1;
+            }
+            ok = wmax((double)bad) == 0.0;
+        }
+        }  // candidates
+        wsync();
+        if (ok) {
+            if (!(ftype && armijo) && lane == 0) {  // augment the filter: ((1-gt) theta, phi - gp theta)
                 const double ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
                 int w = 0;
                 for (int i = 0; i < nf; ++i) {
@@ -1299,77 +1479,93 @@ __global__ void __launch_bounds__(64) k_accept(NlotProblem p, Dims dm, NlotSolve
                         ++w;
                     }
                 }
-                nf = w;
-                if (nf == FILT_MAX) {
+                if (w == FILT_MAX) {
                     for (int i = 0; i + 1 < FILT_MAX; ++i) {
                         AT(filt, 2 * i) = AT(filt, 2 * (i + 1));
                         AT(filt, 2 * i + 1) = AT(filt, 2 * (i + 1) + 1);
                     }
-                    nf--;
+                    w--;
                 }
-                AT(filt, 2 * nf) = ntv;
-                AT(filt, 2 * nf + 1) = npv;
-                SC(SC_NFILT) = nf + 1;
+                AT(filt, 2 * w) = ntv;
+                AT(filt, 2 * w + 1) = npv;
+                SC(SC_NFILT) = w + 1;
             }
             // accept: primal and multipliers with alpha, bound multipliers with alpha_z + safeguard
-            for (int i = 0; i < (N + 1) * NX; ++i) AT(X, i) += al * AT(dX, i);
-            for (int i = 0; i < N * NU; ++i) AT(U, i) += al * AT(dU, i);
-            if (dm.ns)
-                for (int k = 0; k <= N; ++k) AT(S, k) += al * AT(dS, k);
-            for (int q = 0; q < (N + 1) * M; ++q) AT(T, q) += al * AT(dT, q);
-            for (int i = 0; i < NX; ++i) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
-            for (int i = 0; i < N * NX; ++i) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
-            for (int cc = 0; cc < nc; ++cc) AT(yt, cc) += al * (AT(yt_n, cc) - AT(yt, cc));
-            for (int q = 0; q < (N + 1) * M; ++q) AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
             const double az = SC(SC_AZ), ks = 1e10;
             auto zupd = [&](double z, double dz, double sl) {
-                double zn = z + az * dz;
+                const double zn = z + az * dz;
                 return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
             };
-            for (int k = 0; k < N; ++k)
-                for (int i = 0; i < NU; ++i) {
-                    const int q = k * NU + i;
-                    const double u = AT(U, q);
-                    AT(zl, q) = zupd(AT(zl, q), AT(dzl, q), u - p.umin[i]);
-                    AT(zu, q) = zupd(AT(zu, q), AT(dzu, q), p.umax[i] - u);
+            for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e) + al * AT(dU, e);
+                AT(U, e) = u;
+                AT(zl, e) = zupd(AT(zl, e), AT(dzl, e), u - p.umin[e % NU]);
+                AT(zu, e) = zupd(AT(zu, e), AT(dzu, e), p.umax[e % NU] - u);
+            }
+            for (int k = lane; k <= N; k += 64)
+                if (dm.ns) {
+                    const double s = AT(S, k) + al * AT(dS, k);
+                    AT(S, k) = s;
+                    AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s);
                 }
-            if (dm.ns)
-                for (int k = 0; k <= N; ++k) AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), AT(S, k));
-            for (int q = 0; q < (N + 1) * M; ++q) AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), AT(T, q));
-            SC(SC_ITERS) = SC(SC_ITERS) + 1;
-            SC(SC_PHASE) = PH_EVAL;
+            for (int q = lane; q < (N + 1) * M; q += 64) {
+                const double t = AT(T, q) + al * AT(dT, q);
+                AT(T, q) = t;
+                AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), t);
+                AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
+            }
+            for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
+            for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
+            for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
             ph = PH_EVAL;
+            if (lane == 0) {
+                SC(SC_ITERS) = SC(SC_ITERS) + 1;
+                SC(SC_PHASE) = PH_EVAL;
+            }
         } else {
-            const double na = 0.5 * al;
-            SC(SC_TRIALS) = SC(SC_TRIALS) + 1;
+            const double na = ldexp(a0, -ncand);
             if (na < SC(SC_AMIN)) {
-                SC(SC_STATUS) = NLOT_LS_FAILED;
-                SC(SC_PHASE) = PH_DONE;
                 ph = PH_DONE;
-            } else {
+                if (lane == 0) {
+                    SC(SC_STATUS) = NLOT_LS_FAILED;
+                    SC(SC_PHASE) = PH_DONE;
+                }
+            } else if (lane == 0) {
                 SC(SC_ALPHA) = na;
+                SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
             }
         }
     }
-    if (ph != PH_DONE) atomicAdd(&ws.cnt[2], 1);
+    if (ph != PH_DONE && lane == 0) next[atomicAdd(&ws.cnt[2], 1)] = b;
 }
 
-__global__ void k_finalize(NlotProblem p, Dims dm, Ws ws, int B, double* Xo, double* Uo, double* So, double* cost,
-                           int32_t* status, int32_t* iters) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+__global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
+                                                 double* cost, int32_t* status, int32_t* iters) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const int b = blockIdx.x, lane = threadIdx.x;
     const int N = dm.N, nx = dm.nx, nu = dm.nu;
-    for (int i = 0; i < (N + 1) * nx; ++i) Xo[(size_t)b * (N + 1) * nx + i] = AT(X, i);
-    for (int i = 0; i < N * nu; ++i) Uo[(size_t)b * N * nu + i] = AT(U, i);
-    if (So)
-        for (int k = 0; k <= N; ++k) So[(size_t)b * (N + 1) + k] = dm.ns ? AT(S, k) : 0.0;
-    for (int i = 0; i < (N + 1) * nx; ++i) AT(dX, i) = 0;
-    for (int i = 0; i < N * nu; ++i) AT(dU, i) = 0;
-    for (int k = 0; k <= N; ++k) AT(dS, k) = 0;
-    cost[b] = objective(p, dm, ws, b, nullptr, nullptr, nullptr, 0.0);
-    int st = (int)SC(SC_STATUS);
-    status[b] = st < 0 ? NLOT_MAXITER : st;
-    iters[b] = (int)SC(SC_ITERS);
+    for (int i = lane; i < (N + 1) * nx; i += 64) {
+        Xo[(size_t)b * (N + 1) * nx + i] = AT(X, i);
+        AT(dX, i) = 0;
+    }
+    for (int i = lane; i < N * nu; i += 64) {
+        Uo[(size_t)b * N * nu + i] = AT(U, i);
+        AT(dU, i) = 0;
+    }
+    for (int k = lane; k <= N; k += 64) {
+        if (So) So[(size_t)b * (N + 1) + k] = dm.ns ? AT(S, k) : 0.0;
+        AT(dS, k) = 0;
+    }
+    wsync();
+    const double c = objective_w(p, dm, ws, b, lane, 0.0);
+    if (lane == 0) {
+        cost[b] = c;
+        const int st = (int)SC(SC_STATUS);
+        status[b] = st < 0 ? NLOT_MAXITER : st;
+        iters[b] = (int)SC(SC_ITERS);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1409,65 +1605,95 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     const Dims dm = make_dims(p);
     const bool use_mlp = p.sdf_kind == NLOT_SDF_MLP;
     Ws ws = carve(dm, B, use_mlp, workspace);
+    NlotProblem* dP = (NlotProblem*)((char*)workspace + kHdrProblem);
+    Dims* dD = (Dims*)((char*)workspace + kHdrDims);
+    Ws* dW = (Ws*)((char*)workspace + kHdrWs);
+    static_assert(sizeof(NlotProblem) <= kHdrDims - kHdrProblem && sizeof(Dims) <= kHdrWs - kHdrDims &&
+                  sizeof(Ws) <= kHdr - kHdrWs, "workspace header");
+    NLOT_HIP_CHECK(hipMemcpyAsync(dP, &p, sizeof(NlotProblem), hipMemcpyHostToDevice, st));
+    NLOT_HIP_CHECK(hipMemcpyAsync(dD, &dm, sizeof(Dims), hipMemcpyHostToDevice, st));
+    NLOT_HIP_CHECK(hipMemcpyAsync(dW, &ws, sizeof(Ws), hipMemcpyHostToDevice, st));
     const int Bi = (int)B;
-    const int tpb = 64, grid = (Bi + tpb - 1) / tpb;
     const int64_t P = (int64_t)dm.ppk * (dm.N + 1);
     g_stats = NlotSolveStats{};
-    hipLaunchKernelGGL(k_init_state, dim3(grid), dim3(tpb), 0, st, p, dm, o, ws, x0, xg, Xinit, Bi);
+    hipLaunchKernelGGL(k_init_state, dim3(Bi), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit);
     NLOT_HIP_CHECK(hipGetLastError());
     int* hcnt = nullptr;
     NLOT_HIP_CHECK(hipHostMalloc((void**)&hcnt, 4 * sizeof(int), hipHostMallocDefault));
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    if (g_timing && use_mlp)
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (g_timing)
         for (auto& e : ev) hipEventCreate(&e);
-    // upper bound on global steps: every accepted iteration takes at most (1 + backtracks) steps
+    MlpOut mo{};
+    if (use_mlp) {
+        const int64_t plane = P * B * NSPEC;
+        mo.val = ws.mo; mo.gx = ws.mo + plane; mo.gy = ws.mo + 2 * plane; mo.hxx = ws.mo + 3 * plane;
+        mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
+        mo.sv = mo.sg = mo.sh = 1;
+    }
+    // Riccati stage slots in LDS when (N+1) slots fit beside the static LDS (NLOT_SLOTS=global forces HBM)
+    const size_t slot_bytes = (size_t)(dm.N + 1) * slot_len(dm.nx, dm.nu) * sizeof(double);
+    bool slots_lds = slot_bytes + sizeof(typename Solver<DYN>::Sh) <= kLdsBudget;
+    if (const char* e = getenv("NLOT_SLOTS")) slots_lds = slots_lds && strcmp(e, "global") != 0;
+    if (slots_lds)
+        NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)k_iterate<DYN, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)slot_bytes));
+    g_stats.slots_in_lds = slots_lds ? 1 : 0;
     const int max_steps = (o.max_iter + 2) * 64;
-    int rc = NLOT_OK;
-    for (int step = 0; step < max_steps; ++step) {
+    int rc = NLOT_OK, n_active = Bi, cur = 0;
+    for (int step = 0; step < max_steps && n_active > 0; ++step) {
+        const int* act = ws.act[cur];
+        int* nxt = ws.act[cur ^ 1];
         NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 4 * sizeof(int), st));
         if (use_mlp) {
-            hipLaunchKernelGGL(k_points, dim3(grid), dim3(tpb), 0, st, p, dm, ws, Bi, 0);
-            MlpOut mo{};
-            const int64_t plane = P * B;
-            mo.val = ws.mo; mo.gx = ws.mo + plane; mo.gy = ws.mo + 2 * plane; mo.hxx = ws.mo + 3 * plane;
-            mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
-            mo.sv = mo.sg = mo.sh = 1;
+            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0);
             if (ev[0]) hipEventRecord(ev[0], st);
-            rc = launch_mlp_strided(mlp->dev, ws.pts, B, ws.cnt + 0, (int)P, B, nullptr, mo, true, st);
+            // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
+            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[1], st);
-            hipLaunchKernelGGL(k_iterate<DYN>, dim3(grid), dim3(tpb), 0, st, p, dm, o, ws, Bi, x0, xg);
-            hipLaunchKernelGGL(k_points, dim3(grid), dim3(tpb), 0, st, p, dm, ws, Bi, 1);
+        }
+        if (ev[4]) hipEventRecord(ev[4], st);
+        if (slots_lds)
+            hipLaunchKernelGGL((k_iterate<DYN, true>), dim3(n_active), dim3(64), slot_bytes, st, dP, dD, o, dW, act, x0, xg);
+        else
+            hipLaunchKernelGGL((k_iterate<DYN, false>), dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg);
+        if (ev[4]) hipEventRecord(ev[5], st);
+        if (use_mlp) {
+            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1);
             if (ev[0]) hipEventRecord(ev[2], st);
-            rc = launch_mlp_strided(mlp->dev, ws.pts, B, ws.cnt + 1, (int)P, B, nullptr, mo, false, st);
+            rc = launch_mlp_strided(mlp->dev, ws.pts, (int64_t)n_active * NSPEC, ws.cnt + 1, (int)P, 0, nullptr, mo, false, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[3], st);
             g_stats.mlp_full_launches++;
             g_stats.mlp_value_launches++;
-        } else {
-            hipLaunchKernelGGL(k_iterate<DYN>, dim3(grid), dim3(tpb), 0, st, p, dm, o, ws, Bi, x0, xg);
         }
-        hipLaunchKernelGGL(k_accept<DYN>, dim3(grid), dim3(tpb), 0, st, p, dm, o, ws, Bi, x0, xg);
+        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg);
         NLOT_HIP_CHECK(hipGetLastError());
         NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, ws.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         g_stats.iterations = step + 1;
         g_stats.mlp_points_full += (int64_t)hcnt[0] * P;
         g_stats.mlp_points_value += (int64_t)hcnt[1] * P;
-        if (ev[0]) {
+        if (ev[0] && use_mlp) {
             float a = 0, c = 0;
             hipEventElapsedTime(&a, ev[0], ev[1]);
             hipEventElapsedTime(&c, ev[2], ev[3]);
             g_stats.mlp_full_ms += a;
             g_stats.mlp_value_ms += c;
         }
-        if (hcnt[2] == 0) break;
+        if (ev[4]) {
+            float a = 0;
+            hipEventElapsedTime(&a, ev[4], ev[5]);
+            g_stats.iterate_ms += a;
+        }
+        n_active = hcnt[2];
+        cur ^= 1;
     }
     for (auto& e : ev)
         if (e) hipEventDestroy(e);
     hipHostFree(hcnt);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(tpb), 0, st, p, dm, ws, Bi, X, U, S, cost, status, iters);
+    hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);
     NLOT_HIP_CHECK(hipGetLastError());
     NLOT_HIP_CHECK(hipStreamSynchronize(st));
     return NLOT_OK;

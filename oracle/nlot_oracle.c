@@ -1730,3 +1730,4 @@ void oracle_default_options(NlotSolverOptions* o) {
 int oracle_sizeof_problem(void) { return (int)sizeof(NlotProblem); }
 int oracle_sizeof_options(void) { return (int)sizeof(NlotSolverOptions); }
 int oracle_sizeof_mlpdesc(void) { return (int)sizeof(NlotMlpDesc); }
+int oracle_sizeof_stats(void) { return (int)sizeof(NlotSolveStats); }

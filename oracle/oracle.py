@@ -44,7 +44,7 @@ def lib():
         L.oracle_solve_batch.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
                                          C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, ip,
                                          C.c_long, C.c_int]
-        for n in ("oracle_sizeof_problem", "oracle_sizeof_options", "oracle_sizeof_mlpdesc"):
+        for n in ("oracle_sizeof_problem", "oracle_sizeof_options", "oracle_sizeof_mlpdesc", "oracle_sizeof_stats"):
             getattr(L, n).restype = C.c_int
         assert L.oracle_sizeof_problem() == C.sizeof(_abi.NlotProblem)
         assert L.oracle_sizeof_options() == C.sizeof(_abi.NlotSolverOptions)

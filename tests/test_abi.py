@@ -29,7 +29,8 @@ def test_library_exports_every_symbol():
     L = C.CDLL(_lib.LIB_PATH)
     for name in header_functions():
         assert hasattr(L, name), name
-    assert _lib.lib().nlot_abi_version() == 1
+    ver = int(re.search(r"#define NLOT_ABI_VERSION (\d+)", open(os.path.join(ROOT, "include", "nlot.h")).read())[1])
+    assert _lib.lib().nlot_abi_version() == ver
 
 
 def test_struct_layouts_match_header():
@@ -42,6 +43,7 @@ def test_struct_layouts_match_header():
     assert L.oracle_sizeof_problem() == C.sizeof(_abi.NlotProblem)
     assert L.oracle_sizeof_options() == C.sizeof(_abi.NlotSolverOptions)
     assert L.oracle_sizeof_mlpdesc() == C.sizeof(_abi.NlotMlpDesc)
+    assert L.oracle_sizeof_stats() == C.sizeof(_abi.NlotSolveStats)
 
 
 def test_default_options_agree():
