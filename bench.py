@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=48, help="instances for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
+                    help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
     return ap.parse_args()
 
 
@@ -69,7 +71,8 @@ def main():
     x0, xg = sample_start_goal(prob, a.batch, seed=a.seed, sdf=sdf_gpu, rank=rank)
     x0 = torch.tensor(x0, dtype=torch.float64, device=dev)
     xg = torch.tensor(xg, dtype=torch.float64, device=dev)
-    opt = _abi.default_options()
+    opt = _abi.default_options() if a.mu_strategy == "adaptive" else \
+        _abi.default_options(mu_strategy=0, barrier_tol_factor=10.0)
     ws = None
 
     def step():
@@ -135,7 +138,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu = cpu_baseline(prob, w, x0.cpu().numpy()[: a.cpu_sample], xg.cpu().numpy()[: a.cpu_sample],
-                           a.cpu_threads)
+                           a.cpu_threads, opt)
 
     if rank == 0:
         line = {
@@ -154,6 +157,7 @@ def main():
             "config": {
                 "workload": "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
+                "mu_strategy": a.mu_strategy,
                 "instances_per_gpu": a.batch,
                 "global_batch": a.batch * world,
                 "knots": prob.N + 1,
@@ -186,7 +190,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(prob, w, x0, xg, threads):
+def cpu_baseline(prob, w, x0, xg, threads, opt):
     """The oracle (C restatement, OpenMP over instances) on a bounded sample of the same workload."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -196,7 +200,7 @@ def cpu_baseline(prob, w, x0, xg, threads):
     threads = max(1, min(threads, os.cpu_count() or 1))
     hm = O.HostMlp(w)
     t = time.perf_counter()
-    r = O.solve_batch(prob, x0, xg, hm, threads=threads)
+    r = O.solve_batch(prob, x0, xg, hm, opt=opt, threads=threads)
     dt = time.perf_counter() - t
     ns = int((r["status"] == 0).sum())
     return {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",

@@ -111,9 +111,10 @@ typedef struct NlotProblem {
 typedef struct NlotSolverOptions {
     double tol;                  /* 1e-4 (runner.py:118) */
     int32_t max_iter;            /* 1000 (runner.py:117) */
-    int32_t mu_strategy;         /* 0 = monotone (Fiacco-McCormick); see DESIGN.md */
+    int32_t mu_strategy;         /* 0 = monotone (Fiacco-McCormick), 1 = adaptive with the quality-function
+                                    oracle (the reference's setting, runner.py:118-119; default) */
     double mu_init;              /* 0.1 */
-    double barrier_tol_factor;   /* kappa_eps (IPOPT default 10) */
+    double barrier_tol_factor;   /* kappa_eps (IPOPT default 10; the reference sets 0.05, runner.py:120) */
     double dual_inf_tol;         /* 1 */
     double constr_viol_tol;      /* 1e-4 */
     double compl_inf_tol;        /* 1e-4 */

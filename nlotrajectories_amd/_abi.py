@@ -65,8 +65,8 @@ class NlotSolveStats(C.Structure):
 
 def default_options(**kw) -> NlotSolverOptions:
     """IPOPT settings of runner.py:113-125 plus IPOPT defaults."""
-    o = NlotSolverOptions(tol=1e-4, max_iter=1000, mu_strategy=0, mu_init=0.1,
-                          barrier_tol_factor=10.0, dual_inf_tol=1.0, constr_viol_tol=1e-4,
+    o = NlotSolverOptions(tol=1e-4, max_iter=1000, mu_strategy=1, mu_init=0.1,
+                          barrier_tol_factor=0.05, dual_inf_tol=1.0, constr_viol_tol=1e-4,
                           compl_inf_tol=1e-4, constr_mult_init_max=1e3, bound_push=1e-2,
                           bound_frac=1e-2, max_soc=0)
     for k, v in kw.items():

@@ -21,9 +21,9 @@ extern "C" void nlot_default_options(NlotSolverOptions* o) {
     std::memset(o, 0, sizeof(*o));
     o->tol = 1e-4;               // runner.py:118
     o->max_iter = 1000;          // runner.py:117
-    o->mu_strategy = 0;          // monotone
+    o->mu_strategy = 1;          // adaptive + quality-function oracle (runner.py:118-119)
     o->mu_init = 0.1;
-    o->barrier_tol_factor = 10.0;
+    o->barrier_tol_factor = 0.05;  // runner.py:120
     o->dual_inf_tol = 1.0;
     o->constr_viol_tol = 1e-4;
     o->compl_inf_tol = 1e-4;

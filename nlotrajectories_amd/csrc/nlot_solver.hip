@@ -39,7 +39,9 @@ namespace nlot {
 enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3 };
 enum Scal {
     SC_MU, SC_TAU, SC_DWLAST, SC_THMAX, SC_THMIN, SC_ALPHA, SC_AMAX, SC_AMIN, SC_AZ, SC_THETA, SC_PHI, SC_GD,
-    SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_NCAND, SC_COUNT
+    SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_NCAND,
+    SC_FREE, SC_MUMAX, SC_NAF,  // adaptive mu: free-mode flag, mu_max, progress-filter entries
+    SC_COUNT
 };
 constexpr int FILT_MAX = 64;
 constexpr int NSPEC = 8;  // step lengths evaluated per line-search round after a first rejection
@@ -77,6 +79,10 @@ __host__ __device__ constexpr int rstg_len(int nx, int nu) {
 __host__ __device__ constexpr int slot_len(int nx, int nu) {
     return nx * (nx + nu + 1) + nx + 4 + cmax((nx + nu + 1) * (nx + nu + 1) + (nx + nu + 1), rstg_len(nx, nu));
 }
+// quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
+__host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
+    return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
+}
 constexpr size_t kLdsBudget = 150 * 1024;  // slots go to LDS when they fit, else to the global scratch
 
 // instance-major arrays: (name, per-instance length)
@@ -87,7 +93,8 @@ constexpr size_t kLdsBudget = 150 * 1024;  // slots go to LDS when they fit, els
     X_(rct, 8) X_(rcq, (N + 1) * M) X_(dX, (N + 1) * nx) X_(dU, N * nu) X_(dS, N + 1)                  \
     X_(dT, (N + 1) * M) X_(yi_n, nx) X_(yk_n, N * nx) X_(yt_n, 8) X_(yd_n, (N + 1) * M)                \
     X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1) X_(dvt, (N + 1) * M) X_(sc, SC_COUNT)               \
-    X_(filt, 2 * FILT_MAX) X_(stg, (N + 1) * slot_len(nx, nu))
+    X_(filt, 2 * FILT_MAX) X_(afilt, 2 * FILT_MAX) X_(qa, qf_len(N, nx, nu, M)) X_(qc, qf_len(N, nx, nu, M))  \
+    X_(stg, (N + 1) * slot_len(nx, nu))
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -322,9 +329,9 @@ struct Solver {
     // control diagonal, dynamics curvature) and emitted dense once, so it never occupies 64 doubles
     // of registers.
     __device__ __forceinline__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
-                                                 double dw, double* o) {
+                                                 double dw, double mu, double* o) {
         const int N = dm.N, M = dm.M;
-        const double mu = SC(SC_MU), kappa_d = 1e-5;
+        const double kappa_d = 1e-5;
         const bool newton = mode == MODE_NEWTON;
         double Pp[3][3], ps[3], gp[NX], gu[NU], uu[NU], ss = 0, gs = 0;
 #pragma unroll
@@ -497,11 +504,11 @@ struct Solver {
     // Build every stage's condensed matrices in parallel (lane = knot) into the slots.
     template <bool LDS>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                        double dw, double* SL) {
+                                        double dw, double mu_rhs, double* SL) {
         const int N = dm.N;
         for (int k = lane; k <= N; k += 64) {
             double* o = SL + (size_t)k * SLOT;
-            stage(p, dm, ws, b, k, mode, dw, o + oH);
+            stage(p, dm, ws, b, k, mode, dw, mu_rhs, o + oH);
             double A[NX][NX], Bu[NX][NU];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -538,14 +545,16 @@ struct Solver {
     // Per stage: 4 LDS barriers; the Q_vv factorisation is computed redundantly in every lane's
     // registers (no serial LDS round trips); the forward sweep is barrier-free (every lane carries dx).
     template <bool LDS>
+    // mu_rhs: the barrier parameter in the right-hand side (0 for the quality-function oracle's affine
+    // step); delta_c always uses the iterate's mu, SC(SC_MU).
     __device__ static int riccati_wave(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                       double dw, Sh& sh, double* SL) {
+                                       double dw, double mu_rhs, Sh& sh, double* SL) {
         const int N = dm.N, nc = dm.nc, ns = dm.ns;
 #ifdef NLOT_PHASE_PROF
         long long pa = 0, pb = 0, pc = 0, pd = 0;
 #endif
         PROF_T(r0);
-        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, SL);
+        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, mu_rhs, SL);
         PROF_T(r1);
         int cur = 0, negsum = 0;
         for (int e = lane; e < NX * NX + NX + NX * NC + NC * NC + NC; e += 64) {
@@ -1042,6 +1051,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         for (int q = lane; q < (N + 1) * M; q += 64) AT(yd, q) = 0;
     };
 
+    const double mu0 = SC(SC_MU);
     if (ph == PH_INIT) {
         eval_knots(false);
         for (int q = lane; q < (N + 1) * M; q += 64) {
@@ -1050,7 +1060,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         }
         wsync();
         // least-squares equality multipliers (IPOPT LeastSquareMultipliers)
-        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, sh, SL) == 0) {
+        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, mu0, sh, SL) == 0) {
             double ymax = 0;
             for (int k = lane; k <= N; k += 64)
                 for (int j = 0; j < M; ++j) {
@@ -1090,7 +1100,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) = AT(dv, q) - AT(T, q);
     wsync();
 
-    auto theta_phi = [&](double mu, double* th, double* phv) {
+    auto theta_phi = [&](double mu, double* th, double* phv, double* fout = nullptr) {
         double t = 0, bar = 0, lin = 0;
         for (int i = lane; i < NX; i += 64) t += fabs(AT(rci, i));
         for (int i = lane; i < nc; i += 64) t += fabs(AT(rct, i));
@@ -1112,9 +1122,9 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         *th = wsum(t);
         const double fo = objective_w(p, dm, ws, b, lane, 0.0);
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
+        if (fout) *fout = fo;
     };
     PROF_T(t1);
-    const double mu0 = SC(SC_MU);
     if (ph == PH_INIT) {
         double th0, p0;
         theta_phi(mu0, &th0, &p0);
@@ -1127,6 +1137,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
 
     // ---- optimality measures (IPOPT scaled E_0 / E_mu) ----
     double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0, nzc = 0;
+    double dsq = 0, psq = 0, csum = 0;  // quality-function oracle: ||grad L||^2, ||c, d - t||^2, sum z s
     for (int k = lane; k <= N; k += 64) {
         double r[NX];
 #pragma unroll
@@ -1170,7 +1181,10 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         for (int j = 0; j < M; ++j)
             for (int a = 0; a < 3 && a < NX; ++a) r[a] += AT(Jd, (k * M + j) * 3 + a) * AT(yd, k * M + j);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dual = fmax(dual, fabs(r[i]));
+        for (int i = 0; i < NX; ++i) {
+            dual = fmax(dual, fabs(r[i]));
+            dsq += r[i] * r[i];
+        }
         if (k < N)
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
@@ -1179,26 +1193,37 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
 #pragma unroll
                 for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
                 dual = fmax(dual, fabs(t));
+                dsq += t * t;
             }
         if (dm.ns) {
             double t = 2.0 * p.slack_penalty * AT(S, k) - AT(zs, k);
             if (dm.sd)
                 for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
             dual = fmax(dual, fabs(t));
+            dsq += t * t;
         }
-        for (int j = 0; j < M; ++j) dual = fmax(dual, fabs(-AT(yd, k * M + j) - AT(vt, k * M + j)));
+        for (int j = 0; j < M; ++j) {
+            const double t = -AT(yd, k * M + j) - AT(vt, k * M + j);
+            dual = fmax(dual, fabs(t));
+            dsq += t * t;
+        }
     }
-    for (int i = lane; i < NX; i += 64) primal = fmax(primal, fabs(AT(rci, i)));
-    for (int i = lane; i < nc; i += 64) primal = fmax(primal, fabs(AT(rct, i)));
-    for (int i = lane; i < N * NX; i += 64) primal = fmax(primal, fabs(AT(rcd, i)));
+    auto pri_ = [&](double v) {
+        primal = fmax(primal, fabs(v));
+        psq += v * v;
+    };
+    for (int i = lane; i < NX; i += 64) pri_(AT(rci, i));
+    for (int i = lane; i < nc; i += 64) pri_(AT(rct, i));
+    for (int i = lane; i < N * NX; i += 64) pri_(AT(rcd, i));
     cviol = wmax(primal);
     for (int q = lane; q < (N + 1) * M; q += 64) {
-        primal = fmax(primal, fabs(AT(rcq, q)));
+        pri_(AT(rcq, q));
         cviol = fmax(cviol, fmax(0.0, -AT(dv, q)));
     }
     auto compl_ = [&](double z, double s) {
         c0 = fmax(c0, fabs(z * s));
         cmu = fmax(cmu, fabs(z * s - mu0));
+        csum += z * s;
         zsum += fabs(z);
         nzc += 1;
     };
@@ -1222,6 +1247,9 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     zsum = wsum(zsum);
     ysum = wsum(ysum);
     nzc = wsum(nzc);
+    const double csum_w = wsum(csum), dsq_w = wsum(dsq), psq_w = wsum(psq);
+    const int n_dual_ = (N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M;
+    const int n_pri_ = NX + nc + N * NX + (N + 1) * M;
     const double ny = NX + N * NX + nc + (N + 1) * M;
     const double sd = fmax(100.0, (ysum + zsum) / (ny + nzc)) / 100.0;
     const double scc = fmax(100.0, zsum / nzc) / 100.0;
@@ -1239,32 +1267,107 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     if (E0 <= o.tol && dual <= o.dual_inf_tol && cviol <= o.constr_viol_tol && c0 <= o.compl_inf_tol)
         return finish(NLOT_SOLVED);
     if (iters >= o.max_iter) return finish(NLOT_MAXITER);
-    // ---- monotone barrier update ----
+    // ---- barrier parameter: monotone (IPOPT MonotoneMuUpdate) or adaptive (AdaptiveMuUpdate with the
+    //      quality-function oracle, runner.py:118-120; restated in oracle/nlot_oracle.c) ----
+    const double kap = o.barrier_tol_factor;
+    const double mu_floor = fmin(o.tol, o.compl_inf_tol) / (kap + 1.0);
+    constexpr double kMuMin = 1e-11;
     double mu = mu0, tau = SC(SC_TAU);
     bool reset_filter = false;
-    if (iters > 0) {
-        const double kap = o.barrier_tol_factor;
-        double cm = cmu;
+    auto compl_mu = [&](double m) {
+        double cm = 0;
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            cm = fmax(cm, fabs(AT(zl, e) * (u - p.umin[e % NU]) - m));
+            cm = fmax(cm, fabs(AT(zu, e) * (p.umax[e % NU] - u) - m));
+        }
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) cm = fmax(cm, fabs(AT(zs, k) * AT(S, k) - m));
+        for (int q = lane; q < (N + 1) * M; q += 64) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - m));
+        return wmax(cm);
+    };
+    auto barrier_decrease = [&](double cm) {  // Fiacco-McCormick: decrease while the barrier problem is solved
         for (;;) {
             const double Emu = fmax(fmax(dual / sd, primal), cm / scc);
             if (Emu > kap * mu) break;
-            double nm = fmin(0.2 * mu, pow(mu, 1.5));
-            nm = fmax(nm, fmin(o.tol, o.compl_inf_tol) / (kap + 1.0));
+            const double nm = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_floor);
             if (nm >= mu) break;
             mu = nm;
             tau = fmax(0.99, 1.0 - mu);
             reset_filter = true;
-            cm = 0;
-            for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e);
-                cm = fmax(cm, fabs(AT(zl, e) * (u - p.umin[e % NU]) - mu));
-                cm = fmax(cm, fabs(AT(zu, e) * (p.umax[e % NU] - u) - mu));
-            }
-            if (dm.ns)
-                for (int k = lane; k <= N; k += 64) cm = fmax(cm, fabs(AT(zs, k) * AT(S, k) - mu));
-            for (int q = lane; q < (N + 1) * M; q += 64) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - mu));
-            cm = wmax(cm);
+            cm = compl_mu(mu);
         }
+    };
+    bool use_qf = false;
+    const double avg = csum_w / nzc;
+    if (o.mu_strategy == 0) {
+        if (iters > 0) barrier_decrease(cmu);
+    } else {
+        double mu_max = SC(SC_MUMAX);
+        bool free_ = SC(SC_FREE) != 0.0;
+        int naf = (int)SC(SC_NAF);
+        if (iters == 0) {
+            mu_max = 1e3 * avg;
+            free_ = true;
+            naf = 0;
+        }
+        double th_c, ph_c, f_c;
+        theta_phi(mu0, &th_c, &ph_c, &f_c);
+        auto af_ok = [&]() {  // obj-constr progress filter (margin 1e-5 min(1, theta))
+            const double m = 1e-5 * fmin(1.0, th_c);
+            for (int i = 0; i < naf; ++i)
+                if (f_c + m >= AT(afilt, 2 * i) && th_c + m >= AT(afilt, 2 * i + 1)) return false;
+            return true;
+        };
+        if (!free_) {
+            const double Emu = fmax(fmax(dual / sd, primal), cmu / scc);
+            if (Emu <= kap * mu) {
+                if (af_ok()) free_ = true;
+                else barrier_decrease(cmu);
+            }
+        }
+        int naf_new = naf;
+        if (free_) {
+            if (af_ok()) {  // remember the point: drop dominated entries, append (oldest forgotten at capacity)
+                const double m = 1e-5 * fmin(1.0, th_c), nf = f_c - m, nt = th_c - m;
+                int w = 0;
+                for (int i = 0; i < naf; ++i)
+                    if (!(AT(afilt, 2 * i) >= nf && AT(afilt, 2 * i + 1) >= nt)) ++w;
+                naf_new = (w == FILT_MAX ? w - 1 : w) + 1;
+                wsync();
+                if (lane == 0) {
+                    w = 0;
+                    for (int i = 0; i < naf; ++i) {
+                        const double fi = AT(afilt, 2 * i), ti = AT(afilt, 2 * i + 1);
+                        if (!(fi >= nf && ti >= nt)) {
+                            AT(afilt, 2 * w) = fi;
+                            AT(afilt, 2 * w + 1) = ti;
+                            ++w;
+                        }
+                    }
+                    if (w == FILT_MAX) {
+                        for (int i = 0; i + 1 < FILT_MAX; ++i) {
+                            AT(afilt, 2 * i) = AT(afilt, 2 * i + 2);
+                            AT(afilt, 2 * i + 1) = AT(afilt, 2 * i + 3);
+                        }
+                        --w;
+                    }
+                    AT(afilt, 2 * w) = nf;
+                    AT(afilt, 2 * w + 1) = nt;
+                }
+            } else {  // insufficient progress: fixed mode at 0.8 x average complementarity
+                free_ = false;
+                mu = fmin(fmax(0.8 * avg, kMuMin), mu_max);
+                tau = fmax(0.99, 1.0 - mu);
+                reset_filter = true;
+            }
+        }
+        if (lane == 0) {
+            SC(SC_NAF) = naf_new;
+            SC(SC_FREE) = free_ ? 1.0 : 0.0;
+            SC(SC_MUMAX) = mu_max;
+        }
+        use_qf = free_;
     }
     wsync();
     if (lane == 0) {
@@ -1273,21 +1376,215 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         if (reset_filter) SC(SC_NFILT) = 0;
     }
     wsync();
-    // ---- search direction with inertia correction ----
+    // ---- search direction with inertia correction (free mode: the affine-scaling step, mu = 0) ----
     PROF_T(t2);
     int n_ric = 1;
     double dw = 0.0;
-    if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, 0.0, sh, SL)) {
-        const double last = SC(SC_DWLAST);
-        dw = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
+    // One call site for every Newton solve (inertia-correction retries, and in free mode the affine then
+    // the centering solve with the same delta_w): riccati_wave is inlined once.
+    const double last_dw = SC(SC_DWLAST);
+    bool qf_second = false;
+    // QualityFunctionMuOracle buffers: Riccati outputs + recovered slack/dual steps, affine (qa) and
+    // centering minus affine (qc)
+    {
+        const int oU = (N + 1) * NX, oS = oU + N * NU, oyi = oS + N + 1, oyk = oyi + NX, oyt = oyk + N * NX,
+                  oT = oyt + 8, ozl = oT + (N + 1) * M, ozu = ozl + N * NU, ozs = ozu + N * NU, ovt = ozs + N + 1;
+        // store the Riccati outputs and the recovered slack/dual steps at barrier parameter m (cen: minus aff)
+        auto qf_store = [&](double m, bool cen) {
+            double* dst = cen ? &AT(qc, 0) : &AT(qa, 0);
+            const double* aff = &AT(qa, 0);
+            auto put = [&](int i, double v) { dst[i] = cen ? v - aff[i] : v; };
+            for (int i = lane; i < (N + 1) * NX; i += 64) put(i, AT(dX, i));
+            for (int i = lane; i < N * NU; i += 64) put(oU + i, AT(dU, i));
+            for (int i = lane; i <= N; i += 64) put(oS + i, AT(dS, i));
+            for (int i = lane; i < NX; i += 64) put(oyi + i, AT(yi_n, i));
+            for (int i = lane; i < N * NX; i += 64) put(oyk + i, AT(yk_n, i));
+            for (int i = lane; i < 8; i += 64) put(oyt + i, AT(yt_n, i));
+            for (int k = lane; k <= N; k += 64) {
+                for (int j = 0; j < M; ++j) {
+                    const int q = k * M + j;
+                    double Jdz = 0;
+                    for (int a = 0; a < 3 && a < NX; ++a) Jdz += AT(Jd, q * 3 + a) * AT(dX, k * NX + a);
+                    if (dm.sd) Jdz += AT(dS, k);
+                    const double t = AT(T, q), v = AT(vt, q), dt_ = Jdz + AT(rcq, q);
+                    put(oT + q, dt_);
+                    put(ovt + q, m / t - v - (v / t) * dt_);
+                }
+                if (dm.ns) {
+                    const double sk = AT(S, k);
+                    put(ozs + k, m / sk - AT(zs, k) - (AT(zs, k) / sk) * AT(dS, k));
+                }
+            }
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = AT(dU, e);
+                put(ozl + e, m / sl - AT(zl, e) - (AT(zl, e) / sl) * du);
+                put(ozu + e, m / su - AT(zu, e) + (AT(zu, e) / su) * du);
+            }
+            wsync();
+        };
         for (;;) {
+            const int fail = SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw,
+                                                            qf_second ? avg : (use_qf ? 0.0 : mu), sh, SL);
+            if (qf_second) {
+                if (fail) return finish(NLOT_NUMERIC);  // same matrix as the affine solve
+                break;
+            }
+            if (!fail) {
+                if (dw > 0.0 && lane == 0) SC(SC_DWLAST) = dw;
+                if (!use_qf) break;
+                qf_store(0.0, false);
+                qf_second = true;
+                ++n_ric;
+                continue;
+            }
             ++n_ric;
-            if (!SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw, sh, SL)) break;
-            dw *= (last == 0.0) ? 100.0 : 8.0;
-            if (dw > 1e40) break;
+            dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
+            if (dw > 1e40) return finish(NLOT_NUMERIC);
         }
-        if (dw > 1e40) return finish(NLOT_NUMERIC);
-        if (lane == 0) SC(SC_DWLAST) = dw;
+        if (use_qf) {
+        qf_store(avg, true);
+        const double* qa_ = &AT(qa, 0);
+        const double* qc_ = &AT(qc, 0);
+        const double dual_t = dsq_w / (double)n_dual_, pri_t = psq_w / (double)n_pri_;
+        auto qf = [&](double sig) {  // q(sigma): 2-norm-squared, per-element averaged (oracle qf_eval)
+            const double tq = fmax(0.99, 1.0 - sig * avg);
+            double ap = 1.0, ad = 1.0;
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e), du = qa_[oU + e] + sig * qc_[oU + e];
+                ap = frac_to_bound(u - p.umin[e % NU], du, tq, ap);
+                ap = frac_to_bound(p.umax[e % NU] - u, -du, tq, ap);
+                ad = frac_to_bound(AT(zl, e), qa_[ozl + e] + sig * qc_[ozl + e], tq, ad);
+                ad = frac_to_bound(AT(zu, e), qa_[ozu + e] + sig * qc_[ozu + e], tq, ad);
+            }
+            if (dm.ns)
+                for (int k = lane; k <= N; k += 64) {
+                    ap = frac_to_bound(AT(S, k), qa_[oS + k] + sig * qc_[oS + k], tq, ap);
+                    ad = frac_to_bound(AT(zs, k), qa_[ozs + k] + sig * qc_[ozs + k], tq, ad);
+                }
+            for (int q = lane; q < (N + 1) * M; q += 64) {
+                ap = frac_to_bound(AT(T, q), qa_[oT + q] + sig * qc_[oT + q], tq, ap);
+                ad = frac_to_bound(AT(vt, q), qa_[ovt + q] + sig * qc_[ovt + q], tq, ad);
+            }
+            ap = wmin(ap);
+            ad = wmin(ad);
+            double csq = 0;
+            auto cq = [&](double sl, double dsl, double z, double dz) {
+                const double c = (sl + ap * dsl) * (z + ad * dz);
+                csq += c * c;
+            };
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e), du = qa_[oU + e] + sig * qc_[oU + e];
+                cq(u - p.umin[e % NU], du, AT(zl, e), qa_[ozl + e] + sig * qc_[ozl + e]);
+                cq(p.umax[e % NU] - u, -du, AT(zu, e), qa_[ozu + e] + sig * qc_[ozu + e]);
+            }
+            if (dm.ns)
+                for (int k = lane; k <= N; k += 64)
+                    cq(AT(S, k), qa_[oS + k] + sig * qc_[oS + k], AT(zs, k), qa_[ozs + k] + sig * qc_[ozs + k]);
+            for (int q = lane; q < (N + 1) * M; q += 64)
+                cq(AT(T, q), qa_[oT + q] + sig * qc_[oT + q], AT(vt, q), qa_[ovt + q] + sig * qc_[ovt + q]);
+            csq = wsum(csq);
+            return (1.0 - ad) * (1.0 - ad) * dual_t + (1.0 - ap) * (1.0 - ap) * pri_t + csq / nzc;
+        };
+        // sigma search (oracle qf_sigma / qf_golden) as a state machine with one q() call site
+        const double mu_max = SC(SC_MUMAX);
+        const double sig_up = fmin(100.0, mu_max / avg), sig_lo = fmax(1e-6, kMuMin / avg);
+        const double gfac = (3.0 - sqrt(5.0)) / 2.0;
+        enum { EV_1M, EV_1, EV_M1, EV_M2, EV_N1, EV_N2, EV_UP, EV_LO, LOOP, FINAL, DONE };
+        bool lg = false;
+        double tu0 = 0, tl0 = 0, up = 0, lo = 0, m1 = 0, m2 = 0, q1 = 0, q2 = 0, q_up = -1, q_lo = -1, q1m = 0,
+               qq = 0, sig = sig_up;
+        int nsec = 0, st;
+        auto toS = [&](double t_) { return lg ? pow(10.0, t_) : t_; };
+        auto start = [&](double su, double qu, double sl, double ql, bool l) {
+            lg = l;
+            tu0 = up = lg ? log10(su) : su;
+            tl0 = lo = lg ? log10(sl) : sl;
+            q_up = qu;
+            q_lo = ql;
+            m1 = lo + gfac * (up - lo);
+            m2 = lo + (1.0 - gfac) * (up - lo);
+            nsec = 0;
+        };
+        if (sig_lo >= sig_up) {
+            st = DONE;
+        } else if (sig_up <= 1.0) {
+            start(sig_up, -1.0, sig_lo, -1.0, true);
+            st = EV_M1;
+        } else if (sig_lo >= 1.0) {
+            start(sig_up, -1.0, sig_lo, -1.0, false);
+            st = EV_M1;
+        } else {
+            st = EV_1M;
+        }
+        while (st != DONE) {
+            const double x = st == EV_1M ? 0.99
+                           : st == EV_1  ? 1.0
+                           : (st == EV_M1 || st == EV_N1) ? toS(m1)
+                           : (st == EV_M2 || st == EV_N2) ? toS(m2)
+                           : st == EV_UP ? toS(up)
+                                         : toS(lo);
+            const double qv = qf(x);
+            switch (st) {
+                case EV_1M: q1m = qv; st = EV_1; break;
+                case EV_1:
+                    if (q1m > qv) start(sig_up, -1.0, 1.0, qv, false);
+                    else start(0.99, q1m, sig_lo, -1.0, true);
+                    st = EV_M1;
+                    break;
+                case EV_M1: q1 = qv; st = EV_M2; break;
+                case EV_M2: q2 = qv; st = LOOP; break;
+                case EV_N1: q1 = qv; st = LOOP; break;
+                case EV_N2: q2 = qv; st = LOOP; break;
+                case EV_UP: q_up = qv; st = FINAL; break;
+                default: q_lo = qv; st = FINAL; break;
+            }
+            while (st == LOOP || st == FINAL) {
+                if (st == LOOP) {
+                    if (nsec < 8 && (toS(up) - toS(lo)) >= 1e-2 * toS(up)) {
+                        ++nsec;
+                        if (q1 > q2) {
+                            lo = m1; q_lo = q1; m1 = m2; q1 = q2;
+                            m2 = lo + (1.0 - gfac) * (up - lo);
+                            st = EV_N2;
+                        } else {
+                            up = m2; q_up = q2; m2 = m1; q2 = q1;
+                            m1 = lo + gfac * (up - lo);
+                            st = EV_N1;
+                        }
+                    } else {
+                        sig = q1 < q2 ? toS(m1) : toS(m2);
+                        qq = q1 < q2 ? q1 : q2;
+                        if (up == tu0) st = q_up < 0 ? EV_UP : FINAL;
+                        else if (lo == tl0) st = q_lo < 0 ? EV_LO : FINAL;
+                        else st = DONE;
+                    }
+                } else {
+                    if (up == tu0) {
+                        if (q_up < qq) sig = toS(up);
+                    } else if (lo == tl0) {
+                        if (q_lo < qq) sig = toS(lo);
+                    }
+                    st = DONE;
+                }
+            }
+        }
+        mu = fmin(fmax(sig * avg, kMuMin), mu_max);
+        sig = mu / avg;
+        tau = fmax(0.99, 1.0 - mu);
+        for (int i = lane; i < (N + 1) * NX; i += 64) AT(dX, i) = qa_[i] + sig * qc_[i];
+        for (int i = lane; i < N * NU; i += 64) AT(dU, i) = qa_[oU + i] + sig * qc_[oU + i];
+        for (int i = lane; i <= N; i += 64) AT(dS, i) = qa_[oS + i] + sig * qc_[oS + i];
+        for (int i = lane; i < NX; i += 64) AT(yi_n, i) = qa_[oyi + i] + sig * qc_[oyi + i];
+        for (int i = lane; i < N * NX; i += 64) AT(yk_n, i) = qa_[oyk + i] + sig * qc_[oyk + i];
+        for (int i = lane; i < 8; i += 64) AT(yt_n, i) = qa_[oyt + i] + sig * qc_[oyt + i];
+        wsync();
+        if (lane == 0) {
+            SC(SC_MU) = mu;
+            SC(SC_TAU) = tau;
+            SC(SC_NFILT) = 0;  // the line-search filter belongs to one barrier problem
+        }
+        wsync();
+        }
     }
     // ---- recover dt, yd+, dz; fraction to the boundary; line-search reference values ----
     PROF_T(t3);
@@ -1593,7 +1890,7 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
     for (int i = 0; i < p->nu; ++i)
         if (!(p->umin[i] < p->umax[i])) { set_error("control bounds must satisfy min < max"); return NLOT_ERR_INVALID; }
     if (o->max_soc != 0) { set_error("max_soc > 0 is not implemented on the GPU path (DESIGN.md §4)"); return NLOT_ERR_INVALID; }
-    if (o->mu_strategy != 0) { set_error("only the monotone mu strategy is implemented"); return NLOT_ERR_INVALID; }
+    if (o->mu_strategy != 0 && o->mu_strategy != 1) { set_error("mu_strategy: 0 monotone, 1 adaptive"); return NLOT_ERR_INVALID; }
     if (B <= 0 || B > (int64_t)1 << 26) { set_error("B out of range"); return NLOT_ERR_INVALID; }
     return NLOT_OK;
 }

@@ -450,42 +450,6 @@ int oracle_knot_constraints(const NlotProblem* p, const NlotMlpDesc* m, const do
 /* ============================================================================================ */
 /* In-place Cholesky of the n x n row-major SPD matrix a (lower factor).  Returns 0 on success,
  * 1 when a pivot is not safely positive (the inertia test of the Newton system). */
-static int chol(double* a, int n) {
-    double scale = 1.0;
-    for (int i = 0; i < n; ++i) scale = fmax(scale, fabs(a[i * n + i]));
-    for (int j = 0; j < n; ++j) {
-        double d = a[j * n + j];
-        for (int k = 0; k < j; ++k) d -= a[j * n + k] * a[j * n + k];
-        if (!(d > 1e-13 * scale) || !isfinite(d)) return 1;
-        d = sqrt(d);
-        a[j * n + j] = d;
-        for (int i = j + 1; i < n; ++i) {
-            double s = a[i * n + j];
-            for (int k = 0; k < j; ++k) s -= a[i * n + k] * a[j * n + k];
-            a[i * n + j] = s / d;
-        }
-    }
-    return 0;
-}
-/* solve (L L^T) X = Bm for X (n x m, row-major), in place */
-static void chol_solve(const double* L, int n, double* Bm, int m) {
-    for (int c = 0; c < m; ++c) {
-        for (int i = 0; i < n; ++i) {
-            double s = Bm[i * m + c];
-            for (int k = 0; k < i; ++k) s -= L[i * n + k] * Bm[k * m + c];
-            Bm[i * m + c] = s / L[i * n + i];
-        }
-        for (int i = n - 1; i >= 0; --i) {
-            double s = Bm[i * m + c];
-            for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * Bm[k * m + c];
-            Bm[i * m + c] = s / L[i * n + i];
-        }
-    }
-}
-
-/* Symmetric indefinite LDL^T with diagonal (1x1) pivoting on the largest remaining |a_ii|.
- * a: n x n row-major, overwritten by unit-lower L (strict lower) and D (diagonal); perm: pivot order.
- * Returns 0 and sets *nneg, or 2 when a pivot is numerically zero (singular). */
 static int ldl(double* a, int n, int* perm, int* nneg) {
     double scale = 1e-300;
     for (int i = 0; i < n; ++i)
@@ -549,7 +513,7 @@ static void ldl_solve(const double* a, int n, const int* perm, double* Bm, int m
 /* ============================================================================================ */
 /* Solver state                                                                                 */
 /* ============================================================================================ */
-#define FILT_MAX 128
+#define FILT_MAX 64 /* same capacity as the GPU solver (csrc/nlot_solver.hip) */
 #define XMAX 8
 #define VMAX 5
 #define ZMAX (XMAX + VMAX)
@@ -588,6 +552,10 @@ typedef struct {
     double mu, tau, dw_last, theta_max, theta_min;
     int nfilt;
     double filt_theta[FILT_MAX], filt_phi[FILT_MAX];
+    /* adaptive mu (IpAdaptiveMuUpdate): free/fixed mode, mu_max and the obj-constr progress filter */
+    int free_mode, nafilt;
+    double mu_dc; /* mu for delta_c (the iterate's mu; the affine solve uses mu = 0 in the RHS) */
+    double mu_max, af_f[FILT_MAX], af_th[FILT_MAX];
     double lin_resid; /* debug: max residual of the linear KKT system */
     double dc_used;   /* delta_c applied to the terminal block in the last solve */
     double *arena;
@@ -764,13 +732,17 @@ static void eval_full(Sol* s) {
 /* Optimality measures (IPOPT's OptimalityErrorConvergenceCheck / curr_barrier_error). */
 typedef struct {
     double dual, primal, compl0, complmu, sd, sc, cviol;
+    /* for the quality-function mu oracle (IpQualityFunctionMuOracle, 2-norm-squared) */
+    double dual_sq, primal_sq, avg_compl;
+    int n_dual, n_pri, n_comp;
 } Errs;
 
 static void errors(const Sol* s, Errs* e) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0;
-    int ny = 0, nzc = 0;
+    double dsq = 0, psq = 0, csum = 0;
+    int ny = 0, nzc = 0, ndual = 0, npri = 0;
     /* dual infeasibility: grad L over x, u, s, t */
     for (int k = 0; k <= N; ++k) {
         double r[XMAX];
@@ -789,38 +761,60 @@ static void errors(const Sol* s, Errs* e) {
             for (int j = 0; j < s->nc; ++j) r[s->tidx[j]] += s->yt[j];
         for (int j = 0; j < M; ++j)
             for (int a = 0; a < 3; ++a) r[a] += s->Jd[(k * M + j) * 3 + a] * s->yd[k * M + j];
-        for (int i = 0; i < nx; ++i) dual = fmax(dual, fabs(r[i]));
+        for (int i = 0; i < nx; ++i) {
+            dual = fmax(dual, fabs(r[i]));
+            dsq += r[i] * r[i];
+            ndual++;
+        }
         if (k < N)
             for (int i = 0; i < nu; ++i) {
                 double t = s->gU[k * nu + i] - s->zl[k * nu + i] + s->zu[k * nu + i];
                 for (int a = 0; a < nx; ++a) t -= s->B[k * nx * nu + a * nu + i] * s->yk[k * nx + a];
                 dual = fmax(dual, fabs(t));
+                dsq += t * t;
+                ndual++;
             }
         if (s->ns) {
             double t = s->gS[k] - s->zs[k];
             if (s->sd)
                 for (int j = 0; j < M; ++j) t += s->yd[k * M + j];
             dual = fmax(dual, fabs(t));
+            dsq += t * t;
+            ndual++;
         }
-        for (int j = 0; j < M; ++j) dual = fmax(dual, fabs(-s->yd[k * M + j] - s->vt[k * M + j]));
+        for (int j = 0; j < M; ++j) {
+            double t = -s->yd[k * M + j] - s->vt[k * M + j];
+            dual = fmax(dual, fabs(t));
+            dsq += t * t;
+            ndual++;
+        }
     }
     /* primal infeasibility (c, d - t) and unscaled constraint violation */
-    for (int i = 0; i < nx; ++i) primal = fmax(primal, fabs(s->X[i] - s->x0[i]));
-    for (int j = 0; j < s->nc; ++j) primal = fmax(primal, fabs(s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]]));
+#define PRI(v)                                                                                   \
+    do {                                                                                         \
+        double vv = (v);                                                                         \
+        primal = fmax(primal, fabs(vv));                                                         \
+        psq += vv * vv;                                                                          \
+        npri++;                                                                                  \
+    } while (0)
+    for (int i = 0; i < nx; ++i) PRI(s->X[i] - s->x0[i]);
+    for (int j = 0; j < s->nc; ++j) PRI(s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]]);
     for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nx; ++i) primal = fmax(primal, fabs(s->X[(k + 1) * nx + i] - s->F[k * nx + i]));
+        for (int i = 0; i < nx; ++i) PRI(s->X[(k + 1) * nx + i] - s->F[k * nx + i]);
     cviol = primal;
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < M; ++j) {
-            primal = fmax(primal, fabs(s->dv[k * M + j] - s->T[k * M + j]));
+            PRI(s->dv[k * M + j] - s->T[k * M + j]);
             cviol = fmax(cviol, fmax(0.0, -s->dv[k * M + j]));
         }
+#undef PRI
     /* complementarity */
 #define COMPL(z, sl)                                                                             \
     do {                                                                                         \
         double zz = (z), ss = (sl);                                                              \
         c0 = fmax(c0, fabs(zz * ss));                                                            \
         cmu = fmax(cmu, fabs(zz * ss - s->mu));                                                  \
+        csum += zz * ss;                                                                         \
         zsum += fabs(zz);                                                                        \
         nzc++;                                                                                   \
     } while (0)
@@ -847,6 +841,12 @@ static void errors(const Sol* s, Errs* e) {
     e->compl0 = c0;
     e->complmu = cmu;
     e->cviol = cviol;
+    e->dual_sq = dsq;
+    e->primal_sq = psq;
+    e->n_dual = ndual;
+    e->n_pri = npri;
+    e->n_comp = nzc;
+    e->avg_compl = nzc ? csum / nzc : 0.0;
 }
 
 /* ============================================================================================ */
@@ -1118,7 +1118,7 @@ static int riccati(Sol* s, int mode) {
         if (st == 2 || nneg != negsum) {
             /* (near-)rank-deficient terminal block (e.g. no lateral motion of a unicycle at v = 0):
              * IPOPT's delta_c on those rows; a genuine inertia defect survives it. */
-            double dc = 1e-8 * pow(s->mu, 0.25);
+            double dc = 1e-8 * pow(s->mu_dc, 0.25); /* delta_c from the iterate's mu */
             for (int i = 0; i < nc * nc; ++i) L[i] = -Psi[i];
             for (int i = 0; i < nc; ++i) L[i * nc + i] += dc;
             if (ldl(L, nc, perm, &nneg)) return 1;
@@ -1385,6 +1385,152 @@ static void res_save(Sol* s, double* buf, int dir) {
     }
 }
 
+
+/* ============================================================================================ */
+/* Adaptive barrier update (runner.py:118-121: mu_strategy "adaptive", mu_oracle                */
+/* "quality-function", barrier_tol_factor 0.05) — restated from IPOPT 3.14's AdaptiveMuUpdate   */
+/* and QualityFunctionMuOracle (Nocedal, Waechter, Waltz, SIAM J. Optim. 19(4), 2009) with      */
+/* IPOPT's defaults: adaptive_mu_globalization obj-constr-filter (filter_margin_fact 1e-5,      */
+/* filter_max_margin 1), adaptive_mu_monotone_init_factor 0.8, mu_max_fact 1e3, mu_min 1e-11,   */
+/* sigma in [1e-6, 1e2], quality_function_norm_type 2-norm-squared, no centrality/balancing    */
+/* term, quality_function_max_section_steps 8, quality_function_section_sigma_tol 1e-2.         */
+/* ============================================================================================ */
+#define AMU_MU_MIN 1e-11
+static double afilt_margin(double th) { return 1e-5 * fmin(1.0, th); }
+static int afilt_acceptable(const Sol* s, double f, double th) {
+    const double m = afilt_margin(th);
+    for (int i = 0; i < s->nafilt; ++i)
+        if (f + m >= s->af_f[i] && th + m >= s->af_th[i]) return 0;
+    return 1;
+}
+static void afilt_add(Sol* s, double f, double th) {
+    const double m = afilt_margin(th), nf = f - m, nt = th - m;
+    int w = 0;
+    for (int i = 0; i < s->nafilt; ++i)
+        if (!(s->af_f[i] >= nf && s->af_th[i] >= nt)) {
+            s->af_f[w] = s->af_f[i];
+            s->af_th[w] = s->af_th[i];
+            ++w;
+        }
+    s->nafilt = w;
+    if (s->nafilt == FILT_MAX) { /* capacity: forget the oldest entry */
+        memmove(s->af_f, s->af_f + 1, sizeof(double) * (FILT_MAX - 1));
+        memmove(s->af_th, s->af_th + 1, sizeof(double) * (FILT_MAX - 1));
+        s->nafilt--;
+    }
+    s->af_f[s->nafilt] = nf;
+    s->af_th[s->nafilt] = nt;
+    s->nafilt++;
+}
+
+/* step = aff + sigma * cen over every step array (layout of step_save) */
+static void step_combine(Sol* s, const double* aff, const double* cen, double sigma) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double* arrs[] = {s->dX, s->dU, s->dS, s->dT, s->yi_n, s->yk_n, s->yt_n, s->yd_n, s->dzl, s->dzu, s->dzs, s->dvt};
+    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1, (N + 1) * M};
+    for (int a = 0; a < 12; ++a) {
+        for (int i = 0; i < lens[a]; ++i) arrs[a][i] = aff[i] + sigma * cen[i];
+        aff += lens[a];
+        cen += lens[a];
+    }
+}
+
+typedef struct {
+    const double *aff, *cen;
+    double avg;
+    const Errs* e;
+} QfCtx;
+
+/* quality function q(sigma) of the linearised KKT error after the fraction-to-boundary step */
+static double qf_eval(Sol* s, const QfCtx* q, double sigma) {
+    const NlotProblem* p = s->p;
+    int nu = s->nu, N = s->N, M = s->M;
+    step_combine(s, q->aff, q->cen, sigma);
+    const double tau = fmax(0.99, 1.0 - sigma * q->avg);
+    const double ap = primal_frac(s, tau), ad = dual_frac(s, tau);
+    double csq = 0;
+#define CQ(sl, dsl, z, dz)                                                                       \
+    do {                                                                                         \
+        double c_ = ((sl) + ap * (dsl)) * ((z) + ad * (dz));                                     \
+        csq += c_ * c_;                                                                          \
+    } while (0)
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int j = k * nu + i;
+            CQ(s->U[j] - p->umin[i], s->dU[j], s->zl[j], s->dzl[j]);
+            CQ(p->umax[i] - s->U[j], -s->dU[j], s->zu[j], s->dzu[j]);
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) CQ(s->S[k], s->dS[k], s->zs[k], s->dzs[k]);
+    for (int j = 0; j < (N + 1) * M; ++j) CQ(s->T[j], s->dT[j], s->vt[j], s->dvt[j]);
+#undef CQ
+    const Errs* e = q->e;
+    return (1.0 - ad) * (1.0 - ad) * e->dual_sq / e->n_dual + (1.0 - ap) * (1.0 - ap) * e->primal_sq / e->n_pri +
+           csq / e->n_comp;
+}
+
+/* golden-section search for the minimiser of q over [lo, up] (sigma space, or log10 sigma);
+ * q_lo / q_up < 0 mean "not evaluated yet" (QualityFunctionMuOracle::PerformGoldenSection[Log]) */
+static double qf_golden(Sol* s, const QfCtx* q, double sig_up, double q_up, double sig_lo, double q_lo, int lg) {
+    const double gfac = (3.0 - sqrt(5.0)) / 2.0;
+#define TO_T(x) (lg ? log10(x) : (x))
+#define TO_S(t) (lg ? pow(10.0, (t)) : (t))
+    const double t_up0 = TO_T(sig_up), t_lo0 = TO_T(sig_lo);
+    double up = t_up0, lo = t_lo0;
+    double m1 = lo + gfac * (up - lo), m2 = lo + (1.0 - gfac) * (up - lo);
+    double q1 = qf_eval(s, q, TO_S(m1)), q2 = qf_eval(s, q, TO_S(m2));
+    int n = 0;
+    while (n < 8 && (TO_S(up) - TO_S(lo)) >= 1e-2 * TO_S(up)) {
+        ++n;
+        if (q1 > q2) {
+            lo = m1;
+            q_lo = q1;
+            m1 = m2;
+            q1 = q2;
+            m2 = lo + (1.0 - gfac) * (up - lo);
+            q2 = qf_eval(s, q, TO_S(m2));
+        } else {
+            up = m2;
+            q_up = q2;
+            m2 = m1;
+            q2 = q1;
+            m1 = lo + gfac * (up - lo);
+            q1 = qf_eval(s, q, TO_S(m1));
+        }
+    }
+    double sig, qq;
+    if (q1 < q2) {
+        sig = TO_S(m1);
+        qq = q1;
+    } else {
+        sig = TO_S(m2);
+        qq = q2;
+    }
+    if (up == t_up0) {
+        if (q_up < 0) q_up = qf_eval(s, q, TO_S(up));
+        if (q_up < qq) sig = TO_S(up);
+    } else if (lo == t_lo0) {
+        if (q_lo < 0) q_lo = qf_eval(s, q, TO_S(lo));
+        if (q_lo < qq) sig = TO_S(lo);
+    }
+#undef TO_T
+#undef TO_S
+    return sig;
+}
+
+/* QualityFunctionMuOracle::CalculateMu: sigma minimising q, mu = sigma * avg_compl */
+static double qf_sigma(Sol* s, const QfCtx* q, double mu_min, double mu_max) {
+    const double avg = q->avg;
+    const double sig_up = fmin(100.0, mu_max / avg), sig_lo = fmax(1e-6, mu_min / avg);
+    if (sig_lo >= sig_up) return sig_up;
+    if (sig_up <= 1.0) return qf_golden(s, q, sig_up, -1.0, sig_lo, -1.0, 1);
+    if (sig_lo >= 1.0) return qf_golden(s, q, sig_up, -1.0, sig_lo, -1.0, 0);
+    const double sig_1m = 1.0 - fmax(1e-4, 1e-2);
+    const double q_1m = qf_eval(s, q, sig_1m), q_1 = qf_eval(s, q, 1.0);
+    if (q_1m > q_1) return qf_golden(s, q, sig_up, -1.0, 1.0, q_1, 0);
+    return qf_golden(s, q, sig_1m, q_1m, fmax(sig_lo, 1e-300), -1.0, 1);
+}
+
 /* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
  * seen, [4] = final mu, [5] = E_0 (scaled overall error) */
 int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
@@ -1413,6 +1559,8 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
     const int nres = XMAX + N * nx + CMAX + (N + 1) * M;
     int n_soc = 0;
     double lin_resid = 0;
+    double* qf_aff = (double*)malloc(sizeof(double) * 2 * nsave);
+    double* qf_cen = qf_aff + nsave;
     /* ---- initial point: LinearInitializer (trajectory_initialization.py:54-55), U = S = 0 ---- */
     for (int k = 0; k <= N; ++k)
         for (int i = 0; i < nx; ++i)
@@ -1434,6 +1582,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
     for (int k = 0; k <= N; ++k) s->zs[k] = 1.0;
     for (int i = 0; i < (N + 1) * M; ++i) s->vt[i] = 1.0;
     s->mu = o->mu_init;
+    s->mu_dc = s->mu;
     s->tau = fmax(0.99, 1.0 - s->mu);
     /* ---- least-squares equality multipliers (IPOPT LeastSquareMultipliers) ---- */
     eval_full(s);
@@ -1492,22 +1641,69 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             status = NLOT_MAXITER;
             break;
         }
-        /* ---- monotone barrier update (IPOPT MonotoneMuUpdate, fast decrease allowed) ---- */
-        if (iter > 0) {
-            double kap = o->barrier_tol_factor;
-            for (;;) {
-                double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
-                if (Emu > kap * s->mu) break;
-                double nm = fmin(0.2 * s->mu, pow(s->mu, 1.5));
-                nm = fmax(nm, fmin(o->tol, o->compl_inf_tol) / (kap + 1.0));
-                if (nm >= s->mu) break;
-                s->mu = nm;
-                s->tau = fmax(0.99, 1.0 - s->mu);
-                s->nfilt = 0;
-                errors(s, &e); /* complmu depends on mu */
+        /* ---- barrier parameter ---- */
+        const double kap = o->barrier_tol_factor;
+        const double mu_floor = fmin(o->tol, o->compl_inf_tol) / (kap + 1.0);
+        int use_qf = 0;
+        if (o->mu_strategy == 0) { /* IPOPT MonotoneMuUpdate, fast decrease allowed */
+            if (iter > 0) {
+                for (;;) {
+                    double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+                    if (Emu > kap * s->mu) break;
+                    double nm = fmin(0.2 * s->mu, pow(s->mu, 1.5));
+                    nm = fmax(nm, mu_floor);
+                    if (nm >= s->mu) break;
+                    s->mu = nm;
+                    s->tau = fmax(0.99, 1.0 - s->mu);
+                    s->nfilt = 0;
+                    errors(s, &e); /* complmu depends on mu */
+                }
             }
+        } else { /* IPOPT AdaptiveMuUpdate::UpdateBarrierParameter */
+            if (iter == 0) {
+                s->mu_max = 1e3 * e.avg_compl; /* mu_max_fact * initial average complementarity */
+                s->free_mode = 1;
+                s->nafilt = 0;
+            }
+            double th_c, ph_c;
+            merit(s, s->X, s->U, s->S, s->T, s->mu, &th_c, &ph_c, NULL);
+            const double f_c = s->f;
+            if (!s->free_mode) {
+                double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+                if (Emu <= kap * s->mu) { /* barrier problem solved: back to free mode, or decrease */
+                    if (afilt_acceptable(s, f_c, th_c)) {
+                        s->free_mode = 1;
+                    } else {
+                        for (;;) {
+                            double nm = fmax(fmin(0.2 * s->mu, pow(s->mu, 1.5)), mu_floor);
+                            if (nm >= s->mu) break;
+                            s->mu = nm;
+                            s->tau = fmax(0.99, 1.0 - s->mu);
+                            s->nfilt = 0;
+                            errors(s, &e);
+                            Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+                            if (Emu > kap * s->mu) break;
+                        }
+                    }
+                }
+            }
+            if (s->free_mode) {
+                if (afilt_acceptable(s, f_c, th_c)) {
+                    afilt_add(s, f_c, th_c); /* RememberCurrentPointAsAccepted */
+                } else { /* insufficient progress: fixed mode at 0.8 * average complementarity */
+                    s->free_mode = 0;
+                    s->mu = fmin(fmax(0.8 * e.avg_compl, AMU_MU_MIN), s->mu_max);
+                    s->tau = fmax(0.99, 1.0 - s->mu);
+                    s->nfilt = 0;
+                    errors(s, &e);
+                }
+            }
+            use_qf = s->free_mode;
         }
         /* ---- search direction with inertia correction ---- */
+        const double mu_it = s->mu;
+        s->mu_dc = mu_it;
+        if (use_qf) s->mu = 0.0; /* free mode: affine-scaling step first */
         double dw = 0.0;
         build(s, MODE_NEWTON, dw);
         if (riccati(s, MODE_NEWTON)) {
@@ -1526,6 +1722,27 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         }
         lin_resid = fmax(lin_resid, linear_residual(s, MODE_NEWTON));
         recover(s, dw);
+        if (use_qf) { /* QualityFunctionMuOracle: centering step, sigma search, mu = sigma avg */
+            step_save(s, qf_aff, 0);
+            s->mu = e.avg_compl;
+            build(s, MODE_NEWTON, dw);
+            if (riccati(s, MODE_NEWTON)) { /* same matrix as the affine solve: cannot fail */
+                status = NLOT_NUMERIC;
+                break;
+            }
+            recover(s, dw);
+            step_save(s, qf_cen, 0);
+            for (int i = 0; i < nsave; ++i) qf_cen[i] -= qf_aff[i];
+            QfCtx qc = {qf_aff, qf_cen, e.avg_compl, &e};
+            double sigma = qf_sigma(s, &qc, AMU_MU_MIN, s->mu_max);
+            double mu = fmin(fmax(sigma * e.avg_compl, AMU_MU_MIN), s->mu_max);
+            step_combine(s, qf_aff, qf_cen, mu / e.avg_compl);
+            s->mu = mu;
+            s->tau = fmax(0.99, 1.0 - mu);
+            s->nfilt = 0; /* the line-search filter belongs to one barrier problem */
+        } else {
+            s->mu = mu_it;
+        }
         /* ---- step sizes: fraction to the boundary ---- */
         double amax = 1.0, az = 1.0, tau = s->tau;
         for (int k = 0; k < N; ++k)
@@ -1677,6 +1894,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         ++iter;
     }
     free(Xt);
+    free(qf_aff);
     memcpy(Xout, s->X, sizeof(double) * (N + 1) * nx);
     memcpy(Uout, s->U, sizeof(double) * N * nu);
     if (Sout) memcpy(Sout, s->S, sizeof(double) * (N + 1));
@@ -1715,9 +1933,9 @@ void oracle_default_options(NlotSolverOptions* o) {
     memset(o, 0, sizeof *o);
     o->tol = 1e-4;
     o->max_iter = 1000;
-    o->mu_strategy = 0;
+    o->mu_strategy = 1;          /* adaptive + quality-function oracle (runner.py:118-119) */
     o->mu_init = 0.1;
-    o->barrier_tol_factor = 10.0;
+    o->barrier_tol_factor = 0.05; /* runner.py:120 */
     o->dual_inf_tol = 1.0;
     o->constr_viol_tol = 1e-4;
     o->compl_inf_tol = 1e-4;

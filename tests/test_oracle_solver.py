@@ -3,14 +3,18 @@ import numpy as np
 import pytest
 
 
+MONOTONE = dict(mu_strategy=0, barrier_tol_factor=10.0)
+
+
 def test_b2_converges_in_trust_constr_basin():
-    """benchmark_2 from the linear initial guess: the restated IPOPT converges (tol 1e-4) to the basin the
-    survey's independent scipy trust-constr solve found (cost 1.656058 at KKT 6.9e-9)."""
+    """benchmark_2 from the linear initial guess: the restated IPOPT (monotone mu) converges (tol 1e-4) to the
+    basin the survey's independent scipy trust-constr solve found (cost 1.656058 at KKT 6.9e-9)."""
     import oracle as O
+    from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
 
     b = BENCHMARKS["b2"]
-    r = O.solve_one(b["problem"], b["start"], b["goal"])
+    r = O.solve_one(b["problem"], b["start"], b["goal"], opt=_abi.default_options(**MONOTONE))
     assert r["status"] == 0
     assert abs(r["cost"] - 1.656058) < 2e-3
     assert r["constr_viol"] < 1e-4 and r["dual_inf"] < 1e-3
@@ -24,9 +28,26 @@ def test_b2_tight_tolerance_reaches_trust_constr_cost():
 
     b = BENCHMARKS["b2"]
     r = O.solve_one(b["problem"], b["start"], b["goal"], opt=_abi.default_options(tol=1e-8, constr_viol_tol=1e-8,
-                                                                                  compl_inf_tol=1e-8))
+                                                                                  compl_inf_tol=1e-8, **MONOTONE))
     assert r["status"] == 0
     assert abs(r["cost"] - 1.656058) < 5e-5
+
+
+def test_b2_adaptive_mu_reaches_a_kkt_point():
+    """The reference's IPOPT setting (mu_strategy adaptive, quality-function oracle, barrier_tol_factor 0.05,
+    runner.py:118-120) from the same start converges to another local minimum of b2 (the robot holds near
+    the start, then drives; cost 1.632809); tightening the tolerance confirms it is a KKT point."""
+    import oracle as O
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.problem import BENCHMARKS
+
+    b = BENCHMARKS["b2"]
+    r = O.solve_one(b["problem"], b["start"], b["goal"])
+    assert r["status"] == 0 and r["constr_viol"] < 1e-4
+    t = O.solve_one(b["problem"], b["start"], b["goal"], opt=_abi.default_options(tol=1e-8, constr_viol_tol=1e-8,
+                                                                                  compl_inf_tol=1e-8))
+    assert t["status"] == 0 and t["dual_inf"] < 1e-7 and t["constr_viol"] < 1e-10
+    assert abs(t["cost"] - 1.632809) < 1e-5 and abs(r["cost"] - t["cost"]) < 1e-4
 
 
 def test_b3_analytic_and_batch_equals_single():
@@ -46,7 +67,12 @@ def test_metric_learned_sdf_instance(artefact):
     import oracle as O
     from nlotrajectories_amd.problem import METRIC_PROBLEM
 
-    r = O.solve_one(METRIC_PROBLEM, [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0], O.HostMlp(artefact))
+    from nlotrajectories_amd import _abi
+
+    # monotone mu solves this diagonal instance; under the reference's adaptive setting it stalls in the
+    # fixed-mu mode on a ReLU kink of the learned SDF and ends in a line-search failure
+    r = O.solve_one(METRIC_PROBLEM, [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0], O.HostMlp(artefact),
+                    opt=_abi.default_options(**MONOTONE))
     assert r["status"] == 0
     assert r["constr_viol"] < 1e-4
     assert r["lin_resid"] < 1e-6

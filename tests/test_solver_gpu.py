@@ -21,24 +21,32 @@ def _oracle():
     return O
 
 
-def test_iterates_match_oracle_b2():
+STRATEGIES = {"adaptive": {}, "monotone": dict(mu_strategy=0, barrier_tol_factor=10.0)}
+
+
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+def test_iterates_match_oracle_b2(strategy):
     O = _oracle()
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.solver import solve_batch
 
     b = BENCHMARKS["b2"]
-    for k in (1, 2, 5, 10):
-        opt = _abi.default_options(max_iter=k)
+    for k in (1, 2, 5, 10, 20):
+        opt = _abi.default_options(max_iter=k, **STRATEGIES[strategy])
         rg = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=opt)
         rc = O.solve_one(b["problem"], b["start"], b["goal"], opt=opt)
         assert rg["iters"][0].item() == rc["iters"] == k
-        np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-7)
-        np.testing.assert_allclose(rg["U"][0].cpu().numpy(), rc["U"], atol=1e-7)
-        np.testing.assert_allclose(rg["S"][0].cpu().numpy(), rc["S"], atol=1e-7)
+        dx = {n: np.abs(rg[n][0].cpu().numpy() - rc[n]).max() for n in ("X", "U", "S")}
+        print(strategy, "k", k, "max |gpu - oracle|", dx)
+        # fp64 on both sides; summation orders differ, and the differences grow along the nonconvex path
+        tol = 1e-7 if k <= 10 else 1e-6
+        for n in dx:
+            assert dx[n] <= tol, (k, n, dx[n])
 
 
-def test_iterates_match_oracle_learned(artefact):
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+def test_iterates_match_oracle_learned(artefact, strategy):
     O = _oracle()
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.ops import DeviceMlp
@@ -48,7 +56,7 @@ def test_iterates_match_oracle_learned(artefact):
     mlp, hm = DeviceMlp(artefact), O.HostMlp(artefact)
     x0, xg = [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0]
     for k in (1, 3):
-        opt = _abi.default_options(max_iter=k)
+        opt = _abi.default_options(max_iter=k, **STRATEGIES[strategy])
         rg = solve_batch(METRIC_PROBLEM, np.array([x0]), np.array([xg]), mlp=mlp, options=opt)
         rc = O.solve_one(METRIC_PROBLEM, x0, xg, hm, opt=opt)
         np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-4)
@@ -62,8 +70,15 @@ def _stats(rg, rc):
     return (sg == sc).mean(), both, rel
 
 
-def test_batch_b2_analytic_matches_oracle():
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+def test_batch_b2_analytic_matches_oracle(strategy):
+    """Monotone mu at the reference's tol 1e-4 ends every instance at the same central-path point (mu at
+    its floor), so final costs agree to ~1e-7.  Under adaptive mu the termination point at tol 1e-4 depends
+    on the sigma choices along the path: a 1e-12 perturbation of x0 alone moves the oracle's own final
+    cost by a median 8e-4 (the duality gap ~ sum of complementarities), so that parity is checked at
+    tol 1e-8, where both sides converge to the KKT point itself."""
     O = _oracle()
+    from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.sampling import sample_start_goal
     from nlotrajectories_amd.solver import solve_batch
@@ -71,8 +86,10 @@ def test_batch_b2_analytic_matches_oracle():
     p = BENCHMARKS["b2"]["problem"]
     sdf = lambda P: np.sqrt(((np.asarray(P) - 0.5) ** 2).sum(1)) - 0.25
     x0, xg = sample_start_goal(p, 64, seed=1, sdf=sdf, lo=(0, 0), hi=(1, 1))
-    rg = solve_batch(p, x0, xg)
-    rc = O.solve_batch(p, x0, xg, threads=8)
+    tight = dict(tol=1e-8, constr_viol_tol=1e-8, compl_inf_tol=1e-8) if strategy == "adaptive" else {}
+    opt = _abi.default_options(**STRATEGIES[strategy], **tight)
+    rg = solve_batch(p, x0, xg, options=opt)
+    rc = O.solve_batch(p, x0, xg, opt=opt, threads=8)
     agree, both, rel = _stats(rg, rc)
     print("b2 agree", agree, "both", both.sum(), "rel<=1e-4", (rel[both] <= 1e-4).mean(), "median", np.median(rel[both]))
     assert agree >= 0.9
