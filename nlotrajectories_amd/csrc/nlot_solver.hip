@@ -70,15 +70,18 @@ static Dims make_dims(const NlotProblem& p) {
     return d;
 }
 
-// Per-stage slot of one Newton solve: [A | B | c | M | union{ H, g ; Riccati outputs K, k, Kn, P, p, G }]
-// (the condensed H, g of stage k are dead once the backward sweep has consumed them).
-__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
-__host__ __device__ constexpr int rstg_len(int nx, int nu) {
-    return (nu + 1) * nx + (nu + 1) + (nu + 1) * nx + nx * nx + nx + nx * nx;
-}
+// Riccati storage per knot (one Newton solve with up to two right-hand sides):
+//   slot (LDS when it fits, else HBM): [A B 0] (nx x nz) | c | M (2x2) | K (nv x nx) | k (2 x nv) | Kn (nv x nc)
+//     — everything the sequential forward sweep reads;
+//   hg (HBM): H (nz x nz) | g (2 x nz) — built in parallel over knots, read once by the backward sweep
+//     (prefetched one stage ahead);
+//   vf (HBM): P (nx x nx) | p (2 x nx) | Gamma (nx x nc) — written by the backward sweep, read by the
+//     parallel multiplier pass.  (nz = nx + nu + 1, nv = nu + 1, nc = nx.)
 __host__ __device__ constexpr int slot_len(int nx, int nu) {
-    return nx * (nx + nu + 1) + nx + 4 + cmax((nx + nu + 1) * (nx + nu + 1) + (nx + nu + 1), rstg_len(nx, nu));
+    return nx * (nx + nu + 1) + nx + 4 + (nu + 1) * nx + 2 * (nu + 1) + (nu + 1) * nx;
 }
+__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 1) + 2 * (nx + nu + 1); }
+__host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * nx + 2 * nx + nx * nx; }
 // quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
 __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
     return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
@@ -94,7 +97,8 @@ constexpr size_t kLdsBudget = 150 * 1024;  // slots go to LDS when they fit, els
     X_(dT, (N + 1) * M) X_(yi_n, nx) X_(yk_n, N * nx) X_(yt_n, 8) X_(yd_n, (N + 1) * M)                \
     X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1) X_(dvt, (N + 1) * M) X_(sc, SC_COUNT)               \
     X_(filt, 2 * FILT_MAX) X_(afilt, 2 * FILT_MAX) X_(qa, qf_len(N, nx, nu, M)) X_(qc, qf_len(N, nx, nu, M))  \
-    X_(stg, (N + 1) * slot_len(nx, nu))
+    X_(stg, (N + 1) * slot_len(nx, nu)) X_(hg, (N + 1) * hg_len(nx, nu)) X_(vf, (N + 1) * vf_len(nx, nu))   \
+    X_(dX2, (N + 1) * nx) X_(dU2, N * nu) X_(dS2, N + 1) X_(yi2, nx) X_(yk2, N * nx) X_(yt2, 8)
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -328,12 +332,15 @@ struct Solver {
     // o[NZ*NZ, NZ*NZ+NZ).  H is accumulated in its structured blocks (pose 3x3, pose-slack, slack,
     // control diagonal, dynamics curvature) and emitted dense once, so it never occupies 64 doubles
     // of registers.
+    // Two right-hand sides: g_r = g(mu_r) for r < nr (written at o[NZ*NZ + r*NZ]); g is affine in mu,
+    // accumulated as base + mu * coefficient.
     __device__ __forceinline__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
-                                                 double dw, double mu, double* o) {
+                                                 double dw, double mu0, double mu1, int nr, double* o) {
         const int N = dm.N, M = dm.M;
         const double kappa_d = 1e-5;
         const bool newton = mode == MODE_NEWTON;
         double Pp[3][3], ps[3], gp[NX], gu[NU], uu[NU], ss = 0, gs = 0;
+        double gpm[3] = {0, 0, 0}, gum[NU], gsm = 0;  // d g / d mu
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             ps[i] = 0;
@@ -343,7 +350,7 @@ struct Solver {
 #pragma unroll
         for (int i = 0; i < NX; ++i) gp[i] = 0;
 #pragma unroll
-        for (int i = 0; i < NU; ++i) gu[i] = uu[i] = 0;
+        for (int i = 0; i < NU; ++i) gu[i] = uu[i] = gum[i] = 0;
         // objective gradient and (Newton) Hessian of the path-length terms
         for (int seg = k - 1; seg <= k; ++seg) {
             if (seg < 0 || seg >= N) continue;
@@ -400,11 +407,11 @@ struct Solver {
                 for (int i = 0; i < NU; ++i) {
                     const double uv = AT(U, k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
                     uu[i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
-                    gu[i] += -mu / sl + mu / su;
+                    gum[i] += -1.0 / sl + 1.0 / su;
                 }
             if (dm.ns) {
                 ss += AT(zs, k) / Sk;
-                gs += -mu / Sk + kappa_d * mu;
+                gsm += -1.0 / Sk + kappa_d;
             }
         } else {
             if (k < N)
@@ -418,10 +425,11 @@ struct Solver {
 #pragma unroll
             for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + j) * 3 + a);
             const double t = AT(T, k * M + j), v = AT(vt, k * M + j);
-            double Dj, rhs;
+            double Dj, rhs, rhm = 0;
             if (newton) {
                 Dj = v / t + dw;
-                rhs = Dj * AT(rcq, k * M + j) + (-mu / t + kappa_d * mu);
+                rhs = Dj * AT(rcq, k * M + j);
+                rhm = -1.0 / t + kappa_d;
             } else {
                 Dj = 1.0;
                 rhs = -v;
@@ -429,6 +437,7 @@ struct Solver {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 gp[a] += J[a] * rhs;
+                gpm[a] += J[a] * rhm;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) Pp[a][c] += Dj * J[a] * J[c];
                 if (dm.sd) ps[a] += Dj * J[a];
@@ -436,6 +445,7 @@ struct Solver {
             if (dm.sd) {
                 ss += Dj;
                 gs += rhs;
+                gsm += rhm;
             }
         }
         // emit dense H, g; the slack column is NX + NU (k < N) or NX (k == N): compile-time per branch
@@ -461,11 +471,20 @@ struct Solver {
                     if (i == j && i < nz) h += dg;
                     o[i * NZ + j] = h;
                 }
-                double gi = 0;
-                if (i < NX) gi = gp[i];
-                else if (HU && i < NX + NU) gi = gu[i - NX];
-                if (hs && i == is) gi = gs;
-                o[NZ * NZ + i] = gi;
+                double gi = 0, gm = 0;
+                if (i < NX) {
+                    gi = gp[i];
+                    if (i < 3) gm = gpm[i];
+                } else if (HU && i < NX + NU) {
+                    gi = gu[i - NX];
+                    gm = gum[i - NX];
+                }
+                if (hs && i == is) {
+                    gi = gs;
+                    gm = gsm;
+                }
+                o[NZ * NZ + i] = gi + mu0 * gm;
+                if (nr > 1) o[NZ * NZ + NZ + i] = gi + mu1 * gm;
             }
         };
         if (k < N) emit(std::true_type{});
@@ -483,32 +502,33 @@ struct Solver {
         Mk[1][1] = -(r2 - dy * dy) / r3;
     }
 
-    // ---------------- wave-parallel Riccati (DESIGN.md §4.3) ----------------
-    // slot layout (see slot_len): [A B 0] (NX x NZ, dense) | c | M | union{ H, g ; K, k, Kn, P, p, G }
-    static constexpr int SLOT = slot_len(NX, NU), RSTG = rstg_len(NX, NU);
-    static constexpr int sAB = 0, sc = NX * NZ, sM = sc + NX, sU = sM + 4;
-    static constexpr int oH = sU, og = sU + NZ * NZ;                       // union: condensed stage
-    static constexpr int rK = sU, rk = rK + NV * NX, rKn = rk + NV, rP = rKn + NV * NC, rp = rP + NX * NX,
-                         rG = rp + NX;                                       // union: Riccati outputs
-    static_assert(rG + NX * NC == sU + RSTG, "slot layout");
-    static constexpr int NCOL = NX + 1 + NC;                               // gain columns: K | k | Kn
+    // ---------------- wave-parallel Riccati (DESIGN.md §7) ----------------
+    // slot (see slot_len): [A B 0] | c | M | K | k[2] | Kn;  hg: H | g[2];  vf: P | p[2] | G
+    static constexpr int SLOT = slot_len(NX, NU), HG = hg_len(NX, NU), VF = vf_len(NX, NU);
+    static constexpr int sAB = 0, sc = NX * NZ, sM = sc + NX, rK = sM + 4, rk = rK + NV * NX, rKn = rk + 2 * NV;
+    static_assert(rKn + NV * NC == SLOT, "slot layout");
+    static constexpr int vP = 0, vp = NX * NX, vG = vp + 2 * NX;
+    static_assert(vG + NX * NC == VF, "vf layout");
+    static constexpr int NCOL = NX + 2 + NC;                               // gain columns: K | k[2] | Kn
+    static constexpr int NPH2 = NZ * NZ + 2 * NZ + NZ * NC;                 // phase-2 entries (max)
+    static constexpr int NPRE = (NPH2 + 63) / 64;                           // prefetched H/g entries per lane
 
     struct Sh {
-        double P[2][NX][NX], pp[2][NX], G[2][NX][NC];  // value function (double-buffered)
-        double Psi[NC][NC], psi[NC];
-        double PAB[NX][NZ], Pcp[NX];
-        double Q[NZ][NZ], q[NZ], QN[NZ][NC];
-        double cols[NCOL][NV];                         // gains, column-major, zero beyond nv / nc
+        double P[2][NX][NX], pp[2][2][NX], G[2][NX][NC];  // value function (double-buffered), p per RHS
+        double Psi[NC][NC], psi[2][NC];
+        double PAB[NX][NZ], Pcp[2][NX];
+        double Q[NZ][NZ], q[2][NZ], QN[NZ][NC];
+        double cols[NCOL][NV];  // gains, column-major, zero beyond nv / nc
     };
 
-    // Build every stage's condensed matrices in parallel (lane = knot) into the slots.
+    // Build every stage's matrices in parallel (lane = knot): H, g -> hg (HBM); [A B], c, M -> slot.
     template <bool LDS>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                        double dw, double mu_rhs, double* SL) {
+                                        double dw, double mu0, double mu1, int nr, double* SL) {
         const int N = dm.N;
         for (int k = lane; k <= N; k += 64) {
             double* o = SL + (size_t)k * SLOT;
-            stage(p, dm, ws, b, k, mode, dw, mu_rhs, o + oH);
+            stage(p, dm, ws, b, k, mode, dw, mu0, mu1, nr, &AT(hg, k * HG));
             double A[NX][NX], Bu[NX][NU];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -538,41 +558,65 @@ struct Solver {
             o[sM + 2] = Mk[1][0];
             o[sM + 3] = Mk[1][1];
         }
-        xsync<LDS>();
+        __syncthreads();  // hg is in HBM: full fence
     }
 
-    // Returns 0, or 1 when the inertia test fails (uniform over the wave).  Writes dX, dU, dS, yi_n, yk_n, yt_n.
-    // Per stage: 4 LDS barriers; the Q_vv factorisation is computed redundantly in every lane's
-    // registers (no serial LDS round trips); the forward sweep is barrier-free (every lane carries dx).
+    // phase-2 entry e of stage k: the H or g value it starts from (0 for the QN entries)
+    __device__ __forceinline__ static double hg_of(const double* hgk, int e, int nr) {
+        return e < NZ * NZ + nr * NZ ? hgk[e] : 0.0;
+    }
+
+    // Returns 0, or 1 when the inertia test fails (uniform over the wave).  RHS 0 -> dX dU dS yi_n yk_n
+    // yt_n; RHS 1 (nr = 2, barrier parameter mu1) -> dX2 dU2 dS2 yi2 yk2 yt2.  delta_c uses SC(SC_MU).
+    // Per stage: 4 LDS barriers; Q_vv is factored redundantly in every lane's registers; the forward
+    // sweep carries dx in registers (no barriers); the multipliers are a parallel pass over knots.
     template <bool LDS>
-    // mu_rhs: the barrier parameter in the right-hand side (0 for the quality-function oracle's affine
-    // step); delta_c always uses the iterate's mu, SC(SC_MU).
     __device__ static int riccati_wave(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                       double dw, double mu_rhs, Sh& sh, double* SL) {
+                                       double dw, double mu0, double mu1, int nr, Sh& sh, double* SL) {
         const int N = dm.N, nc = dm.nc, ns = dm.ns;
 #ifdef NLOT_PHASE_PROF
         long long pa = 0, pb = 0, pc = 0, pd = 0;
 #endif
         PROF_T(r0);
-        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, mu_rhs, SL);
+        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, mu0, mu1, nr, SL);
         PROF_T(r1);
         int cur = 0, negsum = 0;
-        for (int e = lane; e < NX * NX + NX + NX * NC + NC * NC + NC; e += 64) {
+        for (int e = lane; e < NX * NX + 2 * NX + NX * NC + NC * NC + 2 * NC; e += 64) {
             if (e < NX * NX) sh.P[0][e / NX][e % NX] = 0;
-            else if (e < NX * NX + NX) sh.pp[0][e - NX * NX] = 0;
-            else if (e < NX * NX + NX + NX * NC) { int f = e - NX * NX - NX; sh.G[0][f / NC][f % NC] = 0; }
-            else if (e < NX * NX + NX + NX * NC + NC * NC) { int f = e - NX * NX - NX - NX * NC; sh.Psi[f / NC][f % NC] = 0; }
-            else sh.psi[e - NX * NX - NX - NX * NC - NC * NC] = 0;
+            else if (e < NX * NX + 2 * NX) { const int f = e - NX * NX; sh.pp[0][f / NX][f % NX] = 0; }
+            else if (e < NX * NX + 2 * NX + NX * NC) { const int f = e - NX * NX - 2 * NX; sh.G[0][f / NC][f % NC] = 0; }
+            else if (e < NX * NX + 2 * NX + NX * NC + NC * NC) { const int f = e - NX * NX - 2 * NX - NX * NC; sh.Psi[f / NC][f % NC] = 0; }
+            else { const int f = e - NX * NX - 2 * NX - NX * NC - NC * NC; sh.psi[f / NC][f % NC] = 0; }
         }
         if (mode == MODE_NEWTON && lane == 0) SC(SC_DC) = 0.0;
+        // H/g of the next stage to process, prefetched into registers one stage ahead
+        const int nph2 = NZ * NZ + nr * NZ + NZ * NC;
+        double pre[NPRE];
+#pragma unroll
+        for (int j = 0; j < NPRE; ++j) {
+            const int e = lane + 64 * j;
+            pre[j] = e < nph2 ? hg_of(&AT(hg, N * HG), e, nr) : 0.0;
+        }
         xsync<true>();
         for (int k = N; k >= 0; --k) {
             const int nv = (k < N ? NU : 0) + ns, nxt = cur ^ 1;
             double* slot = SL + (size_t)k * SLOT;
             const double* AB = slot + sAB;
+            double* vfk = &AT(vf, k * VF);
+            double hcur[NPRE];
+#pragma unroll
+            for (int j = 0; j < NPRE; ++j) hcur[j] = pre[j];
+            if (k > 0) {
+                const double* hgn = &AT(hg, (k - 1) * HG);
+#pragma unroll
+                for (int j = 0; j < NPRE; ++j) {
+                    const int e = lane + 64 * j;
+                    pre[j] = e < nph2 ? hg_of(hgn, e, nr) : 0.0;
+                }
+            }
             PROF_T(q0);
-            // (1) PAB = P [A B 0],  Pcp = P c + p
-            for (int e = lane; e < NX * NZ + NX; e += 64) {
+            // (1) PAB = P [A B 0],  Pcp_r = P c + p_r
+            for (int e = lane; e < NX * NZ + nr * NX; e += 64) {
                 if (e < NX * NZ) {
                     const int r = e / NZ, j = e % NZ;
                     double t = 0;
@@ -580,36 +624,39 @@ struct Solver {
                     for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * AB[q * NZ + j];
                     sh.PAB[r][j] = t;
                 } else {
-                    const int r = e - NX * NZ;
-                    double t = sh.pp[cur][r];
+                    const int f = e - NX * NZ, rr = f / NX, r = f % NX;
+                    double t = sh.pp[cur][rr][r];
 #pragma unroll
                     for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * slot[sc + q];
-                    sh.Pcp[r] = t;
+                    sh.Pcp[rr][r] = t;
                 }
             }
             xsync<true>();
             PROF_ACC(pa, q0);
             PROF_T(q1);
-            // (2) Q = H + cross + AB' PAB,  q = g + M c + AB' Pcp,  QN = AB' G   (cross: the path-length
+            // (2) Q = H + cross + AB' PAB,  q_r = g_r + M c + AB' Pcp_r,  QN = AB' G   (cross: the path-length
             //     coupling dx_k' M dx_{k+1} with dx_{k+1} = A dx + B dv + c substituted)
-            for (int e = lane; e < NZ * NZ + NZ + NZ * NC; e += 64) {
-                if (e < NZ * NZ) {
-                    const int i = e / NZ, j = e % NZ;
-                    double t = slot[oH + e];
-                    if (i < 2) t += slot[sM + i * 2] * AB[j] + slot[sM + i * 2 + 1] * AB[NZ + j];
-                    if (j < 2) t += slot[sM + j * 2] * AB[i] + slot[sM + j * 2 + 1] * AB[NZ + i];
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.PAB[r][j];
-                    sh.Q[i][j] = t;
-                } else if (e < NZ * NZ + NZ) {
-                    const int i = e - NZ * NZ;
-                    double t = slot[og + i];
+            for (int j = 0; j < NPRE; ++j) {
+                const int e = lane + 64 * j;
+                if (e >= nph2) continue;
+                if (e < NZ * NZ) {
+                    const int i = e / NZ, jj = e % NZ;
+                    double t = hcur[j];
+                    if (i < 2) t += slot[sM + i * 2] * AB[jj] + slot[sM + i * 2 + 1] * AB[NZ + jj];
+                    if (jj < 2) t += slot[sM + jj * 2] * AB[i] + slot[sM + jj * 2 + 1] * AB[NZ + i];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.PAB[r][jj];
+                    sh.Q[i][jj] = t;
+                } else if (e < NZ * NZ + nr * NZ) {
+                    const int f = e - NZ * NZ, rr = f / NZ, i = f % NZ;
+                    double t = hcur[j];
                     if (i < 2) t += slot[sM + i * 2] * slot[sc + 0] + slot[sM + i * 2 + 1] * slot[sc + 1];
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.Pcp[r];
-                    sh.q[i] = t;
+                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.Pcp[rr][r];
+                    sh.q[rr][i] = t;
                 } else {
-                    const int f = e - NZ * NZ - NZ, i = f / NC, cc = f % NC;
+                    const int f = e - NZ * NZ - nr * NZ, i = f / NC, cc = f % NC;
                     double t = 0;
 #pragma unroll
                     for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.G[cur][r][cc];
@@ -619,8 +666,8 @@ struct Solver {
             xsync<true>();
             PROF_ACC(pb, q1);
             PROF_T(q2);
-            // (3) every lane factors Q_vv in registers (identical, uniform inertia decision); lane c
-            //     solves gain column c and stores it (LDS for the value update, slot for the forward sweep)
+            // (3) every lane factors Q_vv in registers (identical, uniform inertia decision); lane c solves
+            //     gain column c (K | k_0 | k_1 | Kn) into LDS (value update) and the slot (forward sweep)
             if (nv > 0) {
                 double L[NV][NV];
                 int perm[NV], nneg;
@@ -639,8 +686,8 @@ struct Solver {
                         double r = 0;
                         if (v < nv) {
                             if (c < NX) r = -sh.Q[NX + v][c];
-                            else if (c == NX) r = -sh.q[NX + v];
-                            else if (c - NX - 1 < nc) r = -sh.QN[NX + v][c - NX - 1];
+                            else if (c < NX + 2) r = c - NX < nr ? -sh.q[c - NX][NX + v] : 0.0;
+                            else if (c - NX - 2 < nc) r = -sh.QN[NX + v][c - NX - 2];
                         }
                         col[v] = r;
                     }
@@ -650,26 +697,26 @@ struct Solver {
                         const double r = v < nv ? col[v] : 0.0;
                         sh.cols[c][v] = r;
                         if (c < NX) slot[rK + v * NX + c] = r;
-                        else if (c == NX) slot[rk + v] = r;
-                        else slot[rKn + v * NC + (c - NX - 1)] = r;
+                        else if (c < NX + 2) slot[rk + (c - NX) * NV + v] = r;
+                        else slot[rKn + v * NC + (c - NX - 2)] = r;
                     }
                 }
             } else if (lane < NCOL) {
+                const int c = lane;
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
-                    const int c = lane;
                     sh.cols[c][v] = 0.0;
                     if (c < NX) slot[rK + v * NX + c] = 0.0;
-                    else if (c == NX) slot[rk + v] = 0.0;
-                    else slot[rKn + v * NC + (c - NX - 1)] = 0.0;
+                    else if (c < NX + 2) slot[rk + (c - NX) * NV + v] = 0.0;
+                    else slot[rKn + v * NC + (c - NX - 2)] = 0.0;
                 }
             }
             xsync<true>();
             PROF_ACC(pc, q2);
             PROF_T(q3);
-            // (4) value function of stage k (symmetrised P) and the terminal-multiplier system; the
-            //     last knot carries the terminal equality C x_N = xg_sel
-            for (int e = lane; e < NX * NX + NX + NX * NC + NC * NC + NC; e += 64) {
+            // (4) value function of stage k (symmetrised P, p_r) and the terminal-multiplier system; the
+            //     last knot carries the terminal equality C x_N = xg_sel.  P, p, G also go to vf (HBM).
+            for (int e = lane; e < NX * NX + nr * NX + NX * NC + NC * NC + nr * NC; e += 64) {
                 if (e < NX * NX) {
                     const int i = e / NX, j = e % NX;
                     double t = sh.Q[i][j], t2 = sh.Q[j][i];
@@ -680,43 +727,43 @@ struct Solver {
                     }
                     const double r = i == j ? t : 0.5 * (t + t2);
                     sh.P[nxt][i][j] = r;
-                    slot[rP + e] = r;
-                } else if (e < NX * NX + NX) {
-                    const int i = e - NX * NX;
-                    double t = sh.q[i];
+                    vfk[vP + e] = r;
+                } else if (e < NX * NX + nr * NX) {
+                    const int f = e - NX * NX, rr = f / NX, i = f % NX;
+                    double t = sh.q[rr][i];
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX][v];
-                    sh.pp[nxt][i] = t;
-                    slot[rp + i] = t;
-                } else if (e < NX * NX + NX + NX * NC) {
-                    const int f = e - NX * NX - NX, i = f / NC, cc = f % NC;
+                    for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + rr][v];
+                    sh.pp[nxt][rr][i] = t;
+                    vfk[vp + f] = t;
+                } else if (e < NX * NX + nr * NX + NX * NC) {
+                    const int f = e - NX * NX - nr * NX, i = f / NC, cc = f % NC;
                     double t;
                     if (k == N) {
                         t = (cc < nc && dm.tidx[cc] == i) ? 1.0 : 0.0;
                     } else {
                         t = sh.QN[i][cc];
 #pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + 1 + cc][v];
+                        for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + 2 + cc][v];
                     }
                     sh.G[nxt][i][cc] = t;
-                    slot[rG + f] = t;
-                } else if (e < NX * NX + NX + NX * NC + NC * NC) {
-                    const int f = e - NX * NX - NX - NX * NC, a = f / NC, cc = f % NC;
+                    vfk[vG + f] = t;
+                } else if (e < NX * NX + nr * NX + NX * NC + NC * NC) {
+                    const int f = e - NX * NX - nr * NX - NX * NC, a = f / NC, cc = f % NC;
                     double t = 0;
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + 1 + cc][v];
+                    for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + 2 + cc][v];
                     sh.Psi[a][cc] += t;
                 } else {
-                    const int a = e - NX * NX - NX - NX * NC - NC * NC;
+                    const int f = e - NX * NX - nr * NX - NX * NC - NC * NC, rr = f / NC, a = f % NC;
                     if (k == N) {
-                        sh.psi[a] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
+                        sh.psi[rr][a] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
                     } else {
                         double t = 0;
 #pragma unroll
                         for (int r = 0; r < NX; ++r) t += sh.G[cur][r][a] * slot[sc + r];
 #pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX][v];
-                        sh.psi[a] += t;
+                        for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + rr][v];
+                        sh.psi[rr][a] += t;
                     }
                 }
             }
@@ -724,14 +771,16 @@ struct Solver {
             xsync<true>();
             PROF_ACC(pd, q3);
         }
-        xsync<LDS>();  // slot outputs (HBM in the fallback) are read across lanes below
+        __syncthreads();  // slot (HBM in the fallback) and vf are read across lanes below
         PROF_T(r2);
-        // terminal multiplier (every lane, identical): -Psi nu = G0' dx0 + psi, delta_c on the terminal block
-        double dx[NX], nu_[NC];
+        // terminal multipliers (every lane, identical): -Psi nu_r = G0' dx0 + psi_r, delta_c on the terminal block
+        double dx0[NX], nu_[2][NC];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dx[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
+        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) nu_[cc] = 0.0;
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) nu_[rr][cc] = 0.0;
         if (nc) {
             double L[NC][NC];
             int perm[NC], nneg;
@@ -751,106 +800,128 @@ struct Solver {
                 if (lane == 0) SC(SC_DC) = dc;
             }
 #pragma unroll
-            for (int cc = 0; cc < NC; ++cc) {
-                double t = 0;
-                if (cc < nc) {
-                    t = sh.psi[cc];
+            for (int rr = 0; rr < 2; ++rr) {
+                if (rr >= nr) break;
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) t += sh.G[cur][r][cc] * dx[r];
+                for (int cc = 0; cc < NC; ++cc) {
+                    double t = 0;
+                    if (cc < nc) {
+                        t = sh.psi[rr][cc];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) t += sh.G[cur][r][cc] * dx0[r];
+                    }
+                    nu_[rr][cc] = t;
                 }
-                nu_[cc] = t;
+                ldl_solve1<NC>(L, nc, perm, nu_[rr]);
             }
-            ldl_solve1<NC>(L, nc, perm, nu_);
         } else if (negsum) {
             return 1;
         }
         PROF_T(r3);
-        // forward sweep (every lane carries dx; no barriers): dv = k + K dx + Kn nu, dx+ = A dx + B dv + c
+        // forward sweep (every lane carries dx_r; no barriers; the two RHS chains interleave):
+        //   dv_r = k_r + K dx_r + Kn nu_r,  dx_r+ = A dx_r + B dv_r + c
+        double dx[2][NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx[0][i] = dx[1][i] = dx0[i];
+        double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
+        double* dUo[2] = {&AT(dU, 0), &AT(dU2, 0)};
+        double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
         for (int k = 0; k <= N; ++k) {
             const int nv = (k < N ? NU : 0) + ns;
             const double* slot = SL + (size_t)k * SLOT;
-            double dv[NV];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                double t = slot[rk + v];
+            for (int rr = 0; rr < 2; ++rr) {
+                if (rr >= nr) break;
+                double dv[NV];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) t += slot[rK + v * NX + j] * dx[j];
+                for (int v = 0; v < NV; ++v) {
+                    double t = slot[rk + rr * NV + v];
 #pragma unroll
-                for (int cc = 0; cc < NC; ++cc) t += slot[rKn + v * NC + cc] * nu_[cc];
-                dv[v] = t;
-            }
-            double mine = 0;
+                    for (int j = 0; j < NX; ++j) t += slot[rK + v * NX + j] * dx[rr][j];
 #pragma unroll
-            for (int i = 0; i < NX; ++i)
-                if (i == lane) mine = dx[i];
-            if (lane < NX) AT(dX, k * NX + lane) = mine;
-            if (k < N) {
-                double dvl = 0;
-#pragma unroll
-                for (int v = 0; v < NU; ++v)
-                    if (v == lane) dvl = dv[v];
-                if (lane < NU) AT(dU, k * NU + lane) = dvl;
-            }
-            if (ns && lane == 0) AT(dS, k) = k < N ? dv[NU] : dv[0];
-            if (k < N) {
-                double dn[NX];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double t = slot[sc + i];
-#pragma unroll
-                    for (int j = 0; j < NZ; ++j) {
-                        const double z = j < NX ? dx[j] : (j - NX < nv ? dv[j - NX] : 0.0);
-                        t += slot[sAB + i * NZ + j] * z;
-                    }
-                    dn[i] = t;
+                    for (int cc = 0; cc < NC; ++cc) t += slot[rKn + v * NC + cc] * nu_[rr][cc];
+                    dv[v] = t;
                 }
+                double mine = 0;
 #pragma unroll
-                for (int i = 0; i < NX; ++i) dx[i] = dn[i];
+                for (int i = 0; i < NX; ++i)
+                    if (i == lane) mine = dx[rr][i];
+                if (lane < NX) dXo[rr][k * NX + lane] = mine;
+                if (k < N) {
+                    double dvl = 0;
+#pragma unroll
+                    for (int v = 0; v < NU; ++v)
+                        if (v == lane) dvl = dv[v];
+                    if (lane < NU) dUo[rr][k * NU + lane] = dvl;
+                }
+                if (ns && lane == 0) dSo[rr][k] = k < N ? dv[NU] : dv[0];
+                if (k < N) {
+                    double dn[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        double t = slot[sc + i];
+#pragma unroll
+                        for (int j = 0; j < NZ; ++j) {
+                            const double z = j < NX ? dx[rr][j] : (j - NX < nv ? dv[j - NX] : 0.0);
+                            t += slot[sAB + i * NZ + j] * z;
+                        }
+                        dn[i] = t;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) dx[rr][i] = dn[i];
+                }
             }
         }
         wsync();  // dX visible to every lane
         // equality multipliers in parallel over knots: y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k,
         // y_init = -grad V_0(dx_0)
-        for (int k = lane - 1; k < N; k += 64) {
-            const double* s1 = SL + (size_t)(k + 1) * SLOT;
-            double xn[NX];
+        double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
+        double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
+        double* yto[2] = {&AT(yt_n, 0), &AT(yt2, 0)};
 #pragma unroll
-            for (int j = 0; j < NX; ++j) xn[j] = AT(dX, (k + 1) * NX + j);
-            double mx0 = 0, mx1 = 0;
-            if (k >= 0) {
-                const double* s0 = SL + (size_t)k * SLOT;
-                const double d0 = AT(dX, k * NX), d1 = AT(dX, k * NX + 1);
-                mx0 = s0[sM + 0] * d0 + s0[sM + 2] * d1;
-                mx1 = s0[sM + 1] * d0 + s0[sM + 3] * d1;
-            }
+        for (int rr = 0; rr < 2; ++rr) {
+            if (rr >= nr) break;
+            for (int k = lane - 1; k < N; k += 64) {
+                const double* v1 = &AT(vf, (k + 1) * VF);
+                double xn[NX];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double t = s1[rp + i];
+                for (int j = 0; j < NX; ++j) xn[j] = dXo[rr][(k + 1) * NX + j];
+                double mx0 = 0, mx1 = 0;
+                if (k >= 0) {
+                    const double* s0 = SL + (size_t)k * SLOT;
+                    const double d0 = dXo[rr][k * NX], d1 = dXo[rr][k * NX + 1];
+                    mx0 = s0[sM + 0] * d0 + s0[sM + 2] * d1;
+                    mx1 = s0[sM + 1] * d0 + s0[sM + 3] * d1;
+                }
 #pragma unroll
-                for (int j = 0; j < NX; ++j) t += s1[rP + i * NX + j] * xn[j];
+                for (int i = 0; i < NX; ++i) {
+                    double t = v1[vp + rr * NX + i];
 #pragma unroll
-                for (int cc = 0; cc < NC; ++cc) t += s1[rG + i * NC + cc] * nu_[cc];
-                if (k < 0) {
-                    AT(yi_n, i) = -t;
-                } else {
-                    const double mt = i == 0 ? mx0 : (i == 1 ? mx1 : 0.0);
-                    AT(yk_n, k * NX + i) = -t - mt;
+                    for (int j = 0; j < NX; ++j) t += v1[vP + i * NX + j] * xn[j];
+#pragma unroll
+                    for (int cc = 0; cc < NC; ++cc) t += v1[vG + i * NC + cc] * nu_[rr][cc];
+                    if (k < 0) {
+                        yio[rr][i] = -t;
+                    } else {
+                        const double mt = i == 0 ? mx0 : (i == 1 ? mx1 : 0.0);
+                        yko[rr][k * NX + i] = -t - mt;
+                    }
                 }
             }
-        }
-        if (lane < nc) {
-            double v = 0;
+            if (lane < nc) {
+                double v = 0;
 #pragma unroll
-            for (int cc = 0; cc < NC; ++cc)
-                if (cc == lane) v = nu_[cc];
-            AT(yt_n, lane) = v;
+                for (int cc = 0; cc < NC; ++cc)
+                    if (cc == lane) v = nu_[rr][cc];
+                yto[rr][lane] = v;
+            }
         }
         wsync();
 #ifdef NLOT_PHASE_PROF
         PROF_T(r4);
         if (b == 0 && lane == 0 && mode == MODE_NEWTON && SC(SC_ITERS) < 4)
-            printf("RIC build %lld back %lld [PAB %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", r1 - r0,
-                   r2 - r1, pa, pb, pc, pd, r3 - r2, r4 - r3);
+            printf("RIC nr %d build %lld back %lld [PAB %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", nr,
+                   r1 - r0, r2 - r1, pa, pb, pc, pd, r3 - r2, r4 - r3);
 #endif
         return 0;
     }
@@ -1060,7 +1131,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         }
         wsync();
         // least-squares equality multipliers (IPOPT LeastSquareMultipliers)
-        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, mu0, sh, SL) == 0) {
+        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, mu0, 0.0, 1, sh, SL) == 0) {
             double ymax = 0;
             for (int k = lane; k <= N; k += 64)
                 for (int j = 0; j < M; ++j) {
@@ -1383,65 +1454,64 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     // One call site for every Newton solve (inertia-correction retries, and in free mode the affine then
     // the centering solve with the same delta_w): riccati_wave is inlined once.
     const double last_dw = SC(SC_DWLAST);
-    bool qf_second = false;
     // QualityFunctionMuOracle buffers: Riccati outputs + recovered slack/dual steps, affine (qa) and
     // centering minus affine (qc)
     {
         const int oU = (N + 1) * NX, oS = oU + N * NU, oyi = oS + N + 1, oyk = oyi + NX, oyt = oyk + N * NX,
                   oT = oyt + 8, ozl = oT + (N + 1) * M, ozu = ozl + N * NU, ozs = ozu + N * NU, ovt = ozs + N + 1;
         // store the Riccati outputs and the recovered slack/dual steps at barrier parameter m (cen: minus aff)
+        // (cen: the second right-hand side's arrays dX2 ...)
         auto qf_store = [&](double m, bool cen) {
             double* dst = cen ? &AT(qc, 0) : &AT(qa, 0);
             const double* aff = &AT(qa, 0);
+            const double* sX = cen ? &AT(dX2, 0) : &AT(dX, 0);
+            const double* sU = cen ? &AT(dU2, 0) : &AT(dU, 0);
+            const double* sS = cen ? &AT(dS2, 0) : &AT(dS, 0);
+            const double* syi = cen ? &AT(yi2, 0) : &AT(yi_n, 0);
+            const double* syk = cen ? &AT(yk2, 0) : &AT(yk_n, 0);
+            const double* syt = cen ? &AT(yt2, 0) : &AT(yt_n, 0);
             auto put = [&](int i, double v) { dst[i] = cen ? v - aff[i] : v; };
-            for (int i = lane; i < (N + 1) * NX; i += 64) put(i, AT(dX, i));
-            for (int i = lane; i < N * NU; i += 64) put(oU + i, AT(dU, i));
-            for (int i = lane; i <= N; i += 64) put(oS + i, AT(dS, i));
-            for (int i = lane; i < NX; i += 64) put(oyi + i, AT(yi_n, i));
-            for (int i = lane; i < N * NX; i += 64) put(oyk + i, AT(yk_n, i));
-            for (int i = lane; i < 8; i += 64) put(oyt + i, AT(yt_n, i));
+            for (int i = lane; i < (N + 1) * NX; i += 64) put(i, sX[i]);
+            for (int i = lane; i < N * NU; i += 64) put(oU + i, sU[i]);
+            for (int i = lane; i <= N; i += 64) put(oS + i, sS[i]);
+            for (int i = lane; i < NX; i += 64) put(oyi + i, syi[i]);
+            for (int i = lane; i < N * NX; i += 64) put(oyk + i, syk[i]);
+            for (int i = lane; i < 8; i += 64) put(oyt + i, syt[i]);
             for (int k = lane; k <= N; k += 64) {
                 for (int j = 0; j < M; ++j) {
                     const int q = k * M + j;
                     double Jdz = 0;
-                    for (int a = 0; a < 3 && a < NX; ++a) Jdz += AT(Jd, q * 3 + a) * AT(dX, k * NX + a);
-                    if (dm.sd) Jdz += AT(dS, k);
+                    for (int a = 0; a < 3 && a < NX; ++a) Jdz += AT(Jd, q * 3 + a) * sX[k * NX + a];
+                    if (dm.sd) Jdz += sS[k];
                     const double t = AT(T, q), v = AT(vt, q), dt_ = Jdz + AT(rcq, q);
                     put(oT + q, dt_);
                     put(ovt + q, m / t - v - (v / t) * dt_);
                 }
                 if (dm.ns) {
                     const double sk = AT(S, k);
-                    put(ozs + k, m / sk - AT(zs, k) - (AT(zs, k) / sk) * AT(dS, k));
+                    put(ozs + k, m / sk - AT(zs, k) - (AT(zs, k) / sk) * sS[k]);
                 }
             }
             for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = AT(dU, e);
+                const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = sU[e];
                 put(ozl + e, m / sl - AT(zl, e) - (AT(zl, e) / sl) * du);
                 put(ozu + e, m / su - AT(zu, e) + (AT(zu, e) / su) * du);
             }
             wsync();
         };
-        for (;;) {
-            const int fail = SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw,
-                                                            qf_second ? avg : (use_qf ? 0.0 : mu), sh, SL);
-            if (qf_second) {
-                if (fail) return finish(NLOT_NUMERIC);  // same matrix as the affine solve
-                break;
-            }
+        for (;;) {  // free mode: affine (mu = 0) and centering (mu = avg) right-hand sides in one solve
+            const int fail = SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw, use_qf ? 0.0 : mu,
+                                                            avg, use_qf ? 2 : 1, sh, SL);
             if (!fail) {
                 if (dw > 0.0 && lane == 0) SC(SC_DWLAST) = dw;
-                if (!use_qf) break;
-                qf_store(0.0, false);
-                qf_second = true;
-                ++n_ric;
-                continue;
+                break;
             }
             ++n_ric;
             dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
             if (dw > 1e40) return finish(NLOT_NUMERIC);
         }
         if (use_qf) {
+        qf_store(0.0, false);
         qf_store(avg, true);
         const double* qa_ = &AT(qa, 0);
         const double* qc_ = &AT(qc, 0);
