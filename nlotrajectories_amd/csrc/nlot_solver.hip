@@ -77,11 +77,14 @@ static Dims make_dims(const NlotProblem& p) {
 //     (prefetched one stage ahead);
 //   vf (HBM): P (nx x nx) | p (2 x nx) | Gamma (nx x nc) — written by the backward sweep, read by the
 //     parallel multiplier pass.  (nz = nx + nu + 1, nv = nu + 1, nc = nx.)
+//   Layouts (row-major, ncol = nx + 2 + nc gain columns K | k_0 | k_1 | Kn):
+//     slot = [A B 0 | c] (nx x (nz+1)) | M | GN (ncol x nv);  hg = [H | g_0 g_1] (nz x (nz+2));
+//     vf = [P | p_0 p_1 | Gamma] (nx x ncol).
 __host__ __device__ constexpr int slot_len(int nx, int nu) {
-    return nx * (nx + nu + 1) + nx + 4 + (nu + 1) * nx + 2 * (nu + 1) + (nu + 1) * nx;
+    return nx * (nx + nu + 2) + 4 + (nx + 2 + nx) * (nu + 1);
 }
-__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 1) + 2 * (nx + nu + 1); }
-__host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * nx + 2 * nx + nx * nx; }
+__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 3); }
+__host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * (nx + 2 + nx); }
 // quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
 __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
     return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
@@ -190,6 +193,13 @@ __device__ inline double wmin(double v) {
     return __shfl(v, 0);
 }
 __device__ inline void wsync() { __syncthreads(); }  // one-wave workgroups: barrier + LDS/global fence
+// value of v in lane l (compile-time-uniform l) broadcast to the wave through two v_readlane_b32
+__device__ __forceinline__ double bcast_lane(double v, int l) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, l);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 // LDS-only workgroup sync (s_waitcnt lgkmcnt(0) + s_barrier): outstanding global stores are not waited
 // for.  Used inside the Riccati recursion when its slots live in LDS; the global fallback needs wsync.
 template <bool LDS>
@@ -332,8 +342,8 @@ struct Solver {
     // o[NZ*NZ, NZ*NZ+NZ).  H is accumulated in its structured blocks (pose 3x3, pose-slack, slack,
     // control diagonal, dynamics curvature) and emitted dense once, so it never occupies 64 doubles
     // of registers.
-    // Two right-hand sides: g_r = g(mu_r) for r < nr (written at o[NZ*NZ + r*NZ]); g is affine in mu,
-    // accumulated as base + mu * coefficient.
+    // Two right-hand sides: g_r = g(mu_r) for r < nr, written as o = [H | g_0 g_1] (NZ x (NZ+2)); g is
+    // affine in mu, accumulated as base + mu * coefficient.
     __device__ __forceinline__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
                                                  double dw, double mu0, double mu1, int nr, double* o) {
         const int N = dm.N, M = dm.M;
@@ -469,7 +479,7 @@ struct Solver {
                         if (j == is && i < 3) h += ps[i];
                     }
                     if (i == j && i < nz) h += dg;
-                    o[i * NZ + j] = h;
+                    o[i * (NZ + 2) + j] = h;
                 }
                 double gi = 0, gm = 0;
                 if (i < NX) {
@@ -483,8 +493,8 @@ struct Solver {
                     gi = gs;
                     gm = gsm;
                 }
-                o[NZ * NZ + i] = gi + mu0 * gm;
-                if (nr > 1) o[NZ * NZ + NZ + i] = gi + mu1 * gm;
+                o[i * (NZ + 2) + NZ] = gi + mu0 * gm;
+                o[i * (NZ + 2) + NZ + 1] = nr > 1 ? gi + mu1 * gm : 0.0;
             }
         };
         if (k < N) emit(std::true_type{});
@@ -503,25 +513,32 @@ struct Solver {
     }
 
     // ---------------- wave-parallel Riccati ----------------
-    // slot (see slot_len): [A B 0] | c | M | K | k[2] | Kn;  hg: H | g[2];  vf: P | p[2] | G
+    // Extended layouts make every phase one or two uniform index formulas:
+    //   slot: ABc = [A B 0 | c] (NX x (NZ+1)) | M (2x2) | GN[c][v] (NCOL x NV: K^T | k_0 | k_1 | Kn^T)
+    //   hg:   [H | g_0 g_1] (NZ x (NZ+2));  vf / VE: [P | p_0 p_1 | G] (NX x NCOL)
+    //   QE:   [Q | q_0 q_1 | QN] (NZ x NQE);  W: [P AB | P c + p_0 | P c + p_1 | G] (NX x NQE)
+    //   PE:   [Psi | psi_0 psi_1] (NC x (NC+2));  R: minus the gain right-hand sides (NCOL x NV)
+    static constexpr int NCOL = NX + 2 + NC, NQE = NZ + 2 + NC, NAB = NZ + 1;
     static constexpr int SLOT = slot_len(NX, NU), HG = hg_len(NX, NU), VF = vf_len(NX, NU);
-    static constexpr int sAB = 0, sc = NX * NZ, sM = sc + NX, rK = sM + 4, rk = rK + NV * NX, rKn = rk + 2 * NV;
-    static_assert(rKn + NV * NC == SLOT, "slot layout");
-    static constexpr int vP = 0, vp = NX * NX, vG = vp + 2 * NX;
-    static_assert(vG + NX * NC == VF, "vf layout");
-    static constexpr int NCOL = NX + 2 + NC;                               // gain columns: K | k[2] | Kn
-    static constexpr int NPH2 = NZ * NZ + 2 * NZ + NZ * NC;                 // phase-2 entries (max)
-    static constexpr int NPRE = (NPH2 + 63) / 64;                           // prefetched H/g entries per lane
+    static constexpr int sAB = 0, sM = NX * NAB, sGN = sM + 4;
+    static_assert(sGN + NCOL * NV == SLOT, "slot layout");
+    static_assert(NZ * (NZ + 2) == HG && NX * NCOL == VF, "hg / vf layout");
+    static constexpr int NPH2 = NZ * NQE;             // phase-2 entries
+    static constexpr int NPRE = (NPH2 + 63) / 64;    // prefetched H/g entries per lane
 
     struct Sh {
-        double P[2][NX][NX], pp[2][2][NX], G[2][NX][NC];  // value function (double-buffered), p per RHS
-        double Psi[NC][NC], psi[2][NC];
-        double PAB[NX][NZ], Pcp[2][NX];
-        double Q[NZ][NZ], q[2][NZ], QN[NZ][NC];
-        double cols[NCOL][NV];  // gains, column-major, zero beyond nv / nc
+        double VE[2][NX][NCOL];  // value function (double-buffered)
+        double PE[NC][NC + 2];   // terminal system
+        double W[NX][NQE];
+        double QE[NZ][NQE];
+        double R[NCOL][NV];      // -(right-hand sides) of the gain columns
+        double cols[NCOL][NV];   // gains, zero beyond nv / nc
     };
 
-    // Build every stage's matrices in parallel (lane = knot): H, g -> hg (HBM); [A B], c, M -> slot.
+    // gain column c <-> QE column
+    __host__ __device__ static constexpr int qe_col(int c) { return c < NX ? c : NZ + (c - NX); }
+
+    // Build every stage's matrices in parallel (lane = knot): [H | g] -> hg (HBM); [A B 0 | c], M -> slot.
     template <bool LDS>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
                                         double dw, double mu0, double mu1, int nr, double* SL) {
@@ -550,8 +567,8 @@ struct Solver {
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
 #pragma unroll
-                for (int j = 0; j < NZ; ++j) o[sAB + i * NZ + j] = j < NX ? A[i][j] : (j < NX + NU ? Bu[i][j - NX] : 0.0);
-                o[sc + i] = (k < N && mode == MODE_NEWTON) ? -AT(rcd, k * NX + i) : 0.0;
+                for (int j = 0; j < NZ; ++j) o[sAB + i * NAB + j] = j < NX ? A[i][j] : (j < NX + NU ? Bu[i][j - NX] : 0.0);
+                o[sAB + i * NAB + NZ] = (k < N && mode == MODE_NEWTON) ? -AT(rcd, k * NX + i) : 0.0;
             }
             o[sM + 0] = Mk[0][0];
             o[sM + 1] = Mk[0][1];
@@ -561,9 +578,59 @@ struct Solver {
         __syncthreads();  // hg is in HBM: full fence
     }
 
-    // phase-2 entry e of stage k: the H or g value it starts from (0 for the QN entries)
+    // phase-2 entry e = (i, col): its H / g starting value (QN columns start at 0)
     __device__ __forceinline__ static double hg_of(const double* hgk, int e, int nr) {
-        return e < NZ * NZ + nr * NZ ? hgk[e] : 0.0;
+        const int i = e / NQE, col = e % NQE;
+        return col < NZ + nr ? hgk[i * (NZ + 2) + col] : 0.0;
+    }
+
+    // Pivoted LDL^T of the symmetric 3x3 Q_vv held in QE (rows/cols NX..NX+2), identical in arithmetic
+    // and pivot order to the generic ldl_factor / the oracle's ldl(); the permutation is applied through
+    // the (uniform, broadcast) LDS addresses instead of register swaps.  Returns 0 or 2 (singular).
+    __device__ __forceinline__ static int ldl3(const Sh& sh, int o[3], double& d0, double& d1, double& d2,
+                                               double& l10, double& l20, double& l21, int& nneg) {
+        auto q = [&](int i, int j) { return sh.QE[NX + i][NX + j]; };
+        double scale = 1e-300;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) scale = fmax(scale, fabs(q(i, j)));
+        const double a00 = q(0, 0), a11 = q(1, 1), a22 = q(2, 2);
+        int pv = 0;
+        if (fabs(a11) > fabs(a00)) pv = 1;
+        if (fabs(a22) > fabs(pv == 1 ? a11 : a00)) pv = 2;
+        o[0] = pv;
+        o[1] = pv == 1 ? 0 : 1;
+        o[2] = pv == 2 ? 0 : 2;
+        nneg = 0;
+        d0 = q(o[0], o[0]);
+        if (!(fabs(d0) > 1e-13 * scale) || !isfinite(d0)) return 2;
+        if (d0 < 0) ++nneg;
+        const double c1 = q(o[1], o[0]), c2 = q(o[2], o[0]);
+        double b11 = q(o[1], o[1]) - c1 * c1 / d0;
+        double b21 = q(o[2], o[1]) - c2 * c1 / d0;
+        double b22 = q(o[2], o[2]) - c2 * c2 / d0;
+        l10 = c1 / d0;
+        l20 = c2 / d0;
+        if (fabs(b22) > fabs(b11)) {  // swap positions 1 and 2 (rows of L included)
+            const int t = o[1];
+            o[1] = o[2];
+            o[2] = t;
+            const double tb = b11;
+            b11 = b22;
+            b22 = tb;
+            const double tl = l10;
+            l10 = l20;
+            l20 = tl;
+        }
+        d1 = b11;
+        if (!(fabs(d1) > 1e-13 * scale) || !isfinite(d1)) return 2;
+        if (d1 < 0) ++nneg;
+        d2 = b22 - b21 * b21 / d1;
+        l21 = b21 / d1;
+        if (!(fabs(d2) > 1e-13 * scale) || !isfinite(d2)) return 2;
+        if (d2 < 0) ++nneg;
+        return 0;
     }
 
     // Returns 0, or 1 when the inertia test fails (uniform over the wave).  RHS 0 -> dX dU dS yi_n yk_n
@@ -581,27 +648,23 @@ struct Solver {
         build_stages<LDS>(p, dm, ws, b, lane, mode, dw, mu0, mu1, nr, SL);
         PROF_T(r1);
         int cur = 0, negsum = 0;
-        for (int e = lane; e < NX * NX + 2 * NX + NX * NC + NC * NC + 2 * NC; e += 64) {
-            if (e < NX * NX) sh.P[0][e / NX][e % NX] = 0;
-            else if (e < NX * NX + 2 * NX) { const int f = e - NX * NX; sh.pp[0][f / NX][f % NX] = 0; }
-            else if (e < NX * NX + 2 * NX + NX * NC) { const int f = e - NX * NX - 2 * NX; sh.G[0][f / NC][f % NC] = 0; }
-            else if (e < NX * NX + 2 * NX + NX * NC + NC * NC) { const int f = e - NX * NX - 2 * NX - NX * NC; sh.Psi[f / NC][f % NC] = 0; }
-            else { const int f = e - NX * NX - 2 * NX - NX * NC - NC * NC; sh.psi[f / NC][f % NC] = 0; }
+        for (int e = lane; e < NX * NCOL + NC * (NC + 2); e += 64) {
+            if (e < NX * NCOL) sh.VE[0][e / NCOL][e % NCOL] = 0;
+            else { const int f = e - NX * NCOL; sh.PE[f / (NC + 2)][f % (NC + 2)] = 0; }
         }
         if (mode == MODE_NEWTON && lane == 0) SC(SC_DC) = 0.0;
-        // H/g of the next stage to process, prefetched into registers one stage ahead
-        const int nph2 = NZ * NZ + nr * NZ + NZ * NC;
-        double pre[NPRE];
+        double pre[NPRE];  // H/g of the next stage, prefetched into registers one stage ahead
 #pragma unroll
         for (int j = 0; j < NPRE; ++j) {
             const int e = lane + 64 * j;
-            pre[j] = e < nph2 ? hg_of(&AT(hg, N * HG), e, nr) : 0.0;
+            pre[j] = e < NPH2 ? hg_of(&AT(hg, N * HG), e, nr) : 0.0;
         }
         xsync<true>();
         for (int k = N; k >= 0; --k) {
             const int nv = (k < N ? NU : 0) + ns, nxt = cur ^ 1;
             double* slot = SL + (size_t)k * SLOT;
-            const double* AB = slot + sAB;
+            const double* ABc = slot + sAB;
+            const double* Mk = slot + sM;
             double* vfk = &AT(vf, k * VF);
             double hcur[NPRE];
 #pragma unroll
@@ -611,159 +674,146 @@ struct Solver {
 #pragma unroll
                 for (int j = 0; j < NPRE; ++j) {
                     const int e = lane + 64 * j;
-                    pre[j] = e < nph2 ? hg_of(hgn, e, nr) : 0.0;
+                    pre[j] = e < NPH2 ? hg_of(hgn, e, nr) : 0.0;
                 }
             }
             PROF_T(q0);
-            // (1) PAB = P [A B 0],  Pcp_r = P c + p_r
-            for (int e = lane; e < NX * NZ + nr * NX; e += 64) {
-                if (e < NX * NZ) {
-                    const int r = e / NZ, j = e % NZ;
-                    double t = 0;
+            // (1) W = [P AB | P c + p_0 | P c + p_1 | G]
+            for (int e = lane; e < NX * NQE; e += 64) {
+                const int r = e / NQE, col = e % NQE;
+                double t;
+                if (col < NZ + 2) {
+                    const int cc = col < NZ ? col : NZ;
+                    t = col < NZ ? 0.0 : sh.VE[cur][r][NX + col - NZ];
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * AB[q * NZ + j];
-                    sh.PAB[r][j] = t;
+                    for (int q = 0; q < NX; ++q) t += sh.VE[cur][r][q] * ABc[q * NAB + cc];
                 } else {
-                    const int f = e - NX * NZ, rr = f / NX, r = f % NX;
-                    double t = sh.pp[cur][rr][r];
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t += sh.P[cur][r][q] * slot[sc + q];
-                    sh.Pcp[rr][r] = t;
+                    t = sh.VE[cur][r][NX + 2 + col - NZ - 2];
                 }
+                sh.W[r][col] = t;
             }
             xsync<true>();
             PROF_ACC(pa, q0);
             PROF_T(q1);
-            // (2) Q = H + cross + AB' PAB,  q_r = g_r + M c + AB' Pcp_r,  QN = AB' G   (cross: the path-length
-            //     coupling dx_k' M dx_{k+1} with dx_{k+1} = A dx + B dv + c substituted)
+            // (2) QE = [H | g] + cross + AB' W  (cross: the path-length coupling dx_k' M dx_{k+1} with
+            //     dx_{k+1} = A dx + B dv + c substituted); rows of the controls also fill R
 #pragma unroll
             for (int j = 0; j < NPRE; ++j) {
                 const int e = lane + 64 * j;
-                if (e >= nph2) continue;
-                if (e < NZ * NZ) {
-                    const int i = e / NZ, jj = e % NZ;
-                    double t = hcur[j];
-                    if (i < 2) t += slot[sM + i * 2] * AB[jj] + slot[sM + i * 2 + 1] * AB[NZ + jj];
-                    if (jj < 2) t += slot[sM + jj * 2] * AB[i] + slot[sM + jj * 2 + 1] * AB[NZ + i];
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.PAB[r][jj];
-                    sh.Q[i][jj] = t;
-                } else if (e < NZ * NZ + nr * NZ) {
-                    const int f = e - NZ * NZ, rr = f / NZ, i = f % NZ;
-                    double t = hcur[j];
-                    if (i < 2) t += slot[sM + i * 2] * slot[sc + 0] + slot[sM + i * 2 + 1] * slot[sc + 1];
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.Pcp[rr][r];
-                    sh.q[rr][i] = t;
-                } else {
-                    const int f = e - NZ * NZ - nr * NZ, i = f / NC, cc = f % NC;
-                    double t = 0;
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r * NZ + i] * sh.G[cur][r][cc];
-                    sh.QN[i][cc] = t;
+                if (e >= NPH2) continue;
+                const int i = e / NQE, col = e % NQE;
+                double t = hcur[j];
+                if (col < NZ + 2) {
+                    const int cc = col < NZ ? col : NZ;
+                    if (i < 2) t += Mk[i * 2] * ABc[cc] + Mk[i * 2 + 1] * ABc[NAB + cc];
+                    if (col < 2) t += Mk[col * 2] * ABc[i] + Mk[col * 2 + 1] * ABc[NAB + i];
                 }
+#pragma unroll
+                for (int r = 0; r < NX; ++r) t += ABc[r * NAB + i] * sh.W[r][col];
+                sh.QE[i][col] = t;
+                if (i >= NX && (col < NX || col >= NZ)) sh.R[col < NX ? col : NX + col - NZ][i - NX] = -t;
             }
             xsync<true>();
             PROF_ACC(pb, q1);
             PROF_T(q2);
             // (3) every lane factors Q_vv in registers (identical, uniform inertia decision); lane c solves
-            //     gain column c (K | k_0 | k_1 | Kn) into LDS (value update) and the slot (forward sweep)
-            if (nv > 0) {
+            //     gain column c into LDS (value update) and the slot (forward sweep)
+            if (nv == 3 && NV == 3) {
+                int o[3], nneg;
+                double d0, d1, d2, l10, l20, l21;
+                if (ldl3(sh, o, d0, d1, d2, l10, l20, l21, nneg)) return 1;
+                negsum += nneg;
+                if (negsum > nc) return 1;
+                if (lane < NCOL) {
+                    const double x0 = -sh.R[lane][0], x1 = -sh.R[lane][1], x2 = -sh.R[lane][2];
+                    auto pick = [&](int i) { return i == 0 ? x0 : (i == 1 ? x1 : x2); };
+                    double t0 = pick(o[0]), t1 = pick(o[1]), t2 = pick(o[2]);
+                    t1 -= l10 * t0;
+                    t2 -= l20 * t0;
+                    t2 -= l21 * t1;
+                    t0 /= d0;
+                    t1 /= d1;
+                    t2 /= d2;
+                    t1 -= l21 * t2;
+                    t0 -= l10 * t1;
+                    t0 -= l20 * t2;
+                    double y[3];
+#pragma unroll
+                    for (int v = 0; v < 3; ++v) y[v] = o[0] == v ? t0 : (o[1] == v ? t1 : t2);
+#pragma unroll
+                    for (int v = 0; v < 3; ++v) {
+                        sh.cols[lane][v] = -y[v];
+                        slot[sGN + lane * NV + v] = -y[v];
+                    }
+                }
+            } else if (nv > 0) {
                 double L[NV][NV];
                 int perm[NV], nneg;
 #pragma unroll
                 for (int i = 0; i < NV; ++i)
 #pragma unroll
-                    for (int j = 0; j < NV; ++j) L[i][j] = (i < nv && j < nv) ? sh.Q[NX + i][NX + j] : 0.0;
+                    for (int j = 0; j < NV; ++j) L[i][j] = (i < nv && j < nv) ? sh.QE[NX + i][NX + j] : 0.0;
                 if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
                 negsum += nneg;
                 if (negsum > nc) return 1;
                 if (lane < NCOL) {
-                    const int c = lane;
                     double col[NV];
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        double r = 0;
-                        if (v < nv) {
-                            if (c < NX) r = -sh.Q[NX + v][c];
-                            else if (c < NX + 2) r = c - NX < nr ? -sh.q[c - NX][NX + v] : 0.0;
-                            else if (c - NX - 2 < nc) r = -sh.QN[NX + v][c - NX - 2];
-                        }
-                        col[v] = r;
-                    }
+                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? sh.R[lane][v] : 0.0;
                     ldl_solve1<NV>(L, nv, perm, col);
 #pragma unroll
                     for (int v = 0; v < NV; ++v) {
                         const double r = v < nv ? col[v] : 0.0;
-                        sh.cols[c][v] = r;
-                        if (c < NX) slot[rK + v * NX + c] = r;
-                        else if (c < NX + 2) slot[rk + (c - NX) * NV + v] = r;
-                        else slot[rKn + v * NC + (c - NX - 2)] = r;
+                        sh.cols[lane][v] = r;
+                        slot[sGN + lane * NV + v] = r;
                     }
                 }
             } else if (lane < NCOL) {
-                const int c = lane;
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
-                    sh.cols[c][v] = 0.0;
-                    if (c < NX) slot[rK + v * NX + c] = 0.0;
-                    else if (c < NX + 2) slot[rk + (c - NX) * NV + v] = 0.0;
-                    else slot[rKn + v * NC + (c - NX - 2)] = 0.0;
+                    sh.cols[lane][v] = 0.0;
+                    slot[sGN + lane * NV + v] = 0.0;
                 }
             }
             xsync<true>();
             PROF_ACC(pc, q2);
             PROF_T(q3);
-            // (4) value function of stage k (symmetrised P, p_r) and the terminal-multiplier system; the
-            //     last knot carries the terminal equality C x_N = xg_sel.  P, p, G also go to vf (HBM).
-            for (int e = lane; e < NX * NX + nr * NX + NX * NC + NC * NC + nr * NC; e += 64) {
-                if (e < NX * NX) {
-                    const int i = e / NX, j = e % NX;
-                    double t = sh.Q[i][j], t2 = sh.Q[j][i];
+            // (4) value function VE = [P | p_0 p_1 | G] (P symmetrised; the last knot carries the terminal
+            //     equality C x_N = xg_sel) and the terminal system PE = [Psi | psi_0 psi_1]
+            for (int e = lane; e < NX * NCOL + NC * (NC + 2); e += 64) {
+                if (e < NX * NCOL) {
+                    const int i = e / NCOL, c = e % NCOL;
+                    double t = sh.QE[i][qe_col(c)];
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        t += sh.Q[i][NX + v] * sh.cols[j][v];
-                        t2 += sh.Q[j][NX + v] * sh.cols[i][v];
+                    for (int v = 0; v < NV; ++v) t += sh.QE[i][NX + v] * sh.cols[c][v];
+                    if (c < NX && c != i) {
+                        double t2 = sh.QE[c][i];
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) t2 += sh.QE[c][NX + v] * sh.cols[i][v];
+                        t = 0.5 * (t + t2);
                     }
-                    const double r = i == j ? t : 0.5 * (t + t2);
-                    sh.P[nxt][i][j] = r;
-                    vfk[vP + e] = r;
-                } else if (e < NX * NX + nr * NX) {
-                    const int f = e - NX * NX, rr = f / NX, i = f % NX;
-                    double t = sh.q[rr][i];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + rr][v];
-                    sh.pp[nxt][rr][i] = t;
-                    vfk[vp + f] = t;
-                } else if (e < NX * NX + nr * NX + NX * NC) {
-                    const int f = e - NX * NX - nr * NX, i = f / NC, cc = f % NC;
-                    double t;
-                    if (k == N) {
+                    if (k == N && c >= NX + 2) {
+                        const int cc = c - NX - 2;
                         t = (cc < nc && dm.tidx[cc] == i) ? 1.0 : 0.0;
-                    } else {
-                        t = sh.QN[i][cc];
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.Q[i][NX + v] * sh.cols[NX + 2 + cc][v];
                     }
-                    sh.G[nxt][i][cc] = t;
-                    vfk[vG + f] = t;
-                } else if (e < NX * NX + nr * NX + NX * NC + NC * NC) {
-                    const int f = e - NX * NX - nr * NX - NX * NC, a = f / NC, cc = f % NC;
-                    double t = 0;
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + 2 + cc][v];
-                    sh.Psi[a][cc] += t;
+                    sh.VE[nxt][i][c] = t;
+                    vfk[e] = t;
                 } else {
-                    const int f = e - NX * NX - nr * NX - NX * NC - NC * NC, rr = f / NC, a = f % NC;
-                    if (k == N) {
-                        sh.psi[rr][a] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
-                    } else {
+                    const int f = e - NX * NCOL, a = f / (NC + 2), c = f % (NC + 2);
+                    if (c < NC) {  // Psi
                         double t = 0;
 #pragma unroll
-                        for (int r = 0; r < NX; ++r) t += sh.G[cur][r][a] * slot[sc + r];
+                        for (int v = 0; v < NV; ++v) t += sh.QE[NX + v][NZ + 2 + a] * sh.cols[NX + 2 + c][v];
+                        sh.PE[a][c] += t;
+                    } else if (k == N) {
+                        sh.PE[a][c] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
+                    } else {  // psi_r
+                        double t = 0;
 #pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.QN[NX + v][a] * sh.cols[NX + rr][v];
-                        sh.psi[rr][a] += t;
+                        for (int q = 0; q < NX; ++q) t += sh.VE[cur][q][NX + 2 + a] * ABc[q * NAB + NZ];
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) t += sh.QE[NX + v][NZ + 2 + a] * sh.cols[NX + c - NC][v];
+                        sh.PE[a][c] += t;
                     }
                 }
             }
@@ -787,14 +837,14 @@ struct Solver {
 #pragma unroll
             for (int i = 0; i < NC; ++i)
 #pragma unroll
-                for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.Psi[i][j] : 0.0;
+                for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.PE[i][j] : 0.0;
             int f = ldl_factor<NC>(L, nc, perm, &nneg);
             if (f == 2 || nneg != negsum) {
                 const double dc = 1e-8 * pow(SC(SC_MU), 0.25);
 #pragma unroll
                 for (int i = 0; i < NC; ++i)
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.Psi[i][j] + (i == j ? dc : 0.0) : 0.0;
+                    for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.PE[i][j] + (i == j ? dc : 0.0) : 0.0;
                 if (ldl_factor<NC>(L, nc, perm, &nneg)) return 1;
                 if (nneg != negsum) return 1;
                 if (lane == 0) SC(SC_DC) = dc;
@@ -806,9 +856,9 @@ struct Solver {
                 for (int cc = 0; cc < NC; ++cc) {
                     double t = 0;
                     if (cc < nc) {
-                        t = sh.psi[rr][cc];
+                        t = sh.PE[cc][NC + rr];
 #pragma unroll
-                        for (int r = 0; r < NX; ++r) t += sh.G[cur][r][cc] * dx0[r];
+                        for (int r = 0; r < NX; ++r) t += sh.VE[cur][r][NX + 2 + cc] * dx0[r];
                     }
                     nu_[rr][cc] = t;
                 }
@@ -818,61 +868,118 @@ struct Solver {
             return 1;
         }
         PROF_T(r3);
-        // forward sweep (every lane carries dx_r; no barriers; the two RHS chains interleave):
-        //   dv_r = k_r + K dx_r + Kn nu_r,  dx_r+ = A dx_r + B dv_r + c
-        double dx[2][NX];
+        // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots, in place: row i of
+        // [A B 0 | c] becomes [Phi_i | B_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r)
+        // (the slack column of B is identically zero, so it can hold off_0)
+        static_assert(NU + 1 == NV, "slack is the last control column");
+        for (int k = lane; k < N; k += 64) {
+            double* slot = SL + (size_t)k * SLOT;
+            const double* GN = slot + sGN;
+            double dv[2][NU], Kt[NU][NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dx[0][i] = dx[1][i] = dx0[i];
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int v = 0; v < NU; ++v) {
+                    double t = GN[(NX + rr) * NV + v];
+#pragma unroll
+                    for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
+                    dv[rr][v] = t;
+                }
+#pragma unroll
+            for (int v = 0; v < NU; ++v)
+#pragma unroll
+                for (int j = 0; j < NX; ++j) Kt[v][j] = GN[j * NV + v];
+#pragma unroll 1
+            for (int i = 0; i < NX; ++i) {
+                double* r_ = slot + sAB + i * NAB;
+                double Bi[NU];
+#pragma unroll
+                for (int v = 0; v < NU; ++v) Bi[v] = r_[NX + v];
+                double o0 = r_[NZ], o1 = r_[NZ];
+#pragma unroll
+                for (int v = 0; v < NU; ++v) {
+                    o0 += Bi[v] * dv[0][v];
+                    o1 += Bi[v] * dv[1][v];
+                }
+#pragma unroll
+                for (int j = 0; j < NX; ++j) {
+                    double t = r_[j];
+#pragma unroll
+                    for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][j];
+                    r_[j] = t;
+                }
+                r_[NX + NU] = o0;
+                r_[NZ] = o1;
+            }
+        }
+        if (LDS) xsync<true>(); else __syncthreads();
+        // (F2) the chain dx_{k+1} = Phi_k dx_k + off_k: lane i < NX carries dx[i] of both RHS; the other
+        //      components arrive by readlane (no LDS, no barrier); Phi rows are prefetched a stage ahead
         double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
         double* dUo[2] = {&AT(dU, 0), &AT(dU2, 0)};
         double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
-        for (int k = 0; k <= N; ++k) {
-            const int nv = (k < N ? NU : 0) + ns;
-            const double* slot = SL + (size_t)k * SLOT;
+        {
+            const int li = lane < NX ? lane : 0;
+            double x0 = 0;
 #pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                if (rr >= nr) break;
-                double dv[NV];
+            for (int i = 0; i < NX; ++i)
+                if (i == lane) x0 = dx0[i];
+            double x[2] = {x0, x0};
+            double row[NX + 2], nrow[NX + 2];
+            auto load_row = [&](int k, double* rw) {
+                const double* sl = SL + (size_t)k * SLOT + sAB + li * NAB;
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double t = slot[rk + rr * NV + v];
+                for (int j = 0; j < NX; ++j) rw[j] = sl[j];
+                rw[NX] = sl[NX + NU];
+                rw[NX + 1] = sl[NZ];
+            };
+            if (N > 0) load_row(0, nrow);
+            for (int k = 0; k < N; ++k) {
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) t += slot[rK + v * NX + j] * dx[rr][j];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) t += slot[rKn + v * NC + cc] * nu_[rr][cc];
-                    dv[v] = t;
+                for (int j = 0; j < NX + 2; ++j) row[j] = nrow[j];
+                if (k + 1 < N) load_row(k + 1, nrow);
+                if (lane < NX) {
+                    dXo[0][k * NX + lane] = x[0];
+                    if (nr > 1) dXo[1][k * NX + lane] = x[1];
                 }
-                double mine = 0;
 #pragma unroll
-                for (int i = 0; i < NX; ++i)
-                    if (i == lane) mine = dx[rr][i];
-                if (lane < NX) dXo[rr][k * NX + lane] = mine;
-                if (k < N) {
-                    double dvl = 0;
+                for (int rr = 0; rr < 2; ++rr) {
+                    double t = row[NX + rr];
 #pragma unroll
-                    for (int v = 0; v < NU; ++v)
-                        if (v == lane) dvl = dv[v];
-                    if (lane < NU) dUo[rr][k * NU + lane] = dvl;
+                    for (int j = 0; j < NX; ++j) t += row[j] * bcast_lane(x[rr], j);
+                    x[rr] = t;
                 }
-                if (ns && lane == 0) dSo[rr][k] = k < N ? dv[NU] : dv[0];
-                if (k < N) {
-                    double dn[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        double t = slot[sc + i];
-#pragma unroll
-                        for (int j = 0; j < NZ; ++j) {
-                            const double z = j < NX ? dx[rr][j] : (j - NX < nv ? dv[j - NX] : 0.0);
-                            t += slot[sAB + i * NZ + j] * z;
-                        }
-                        dn[i] = t;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) dx[rr][i] = dn[i];
-                }
+            }
+            if (lane < NX) {
+                dXo[0][N * NX + lane] = x[0];
+                if (nr > 1) dXo[1][N * NX + lane] = x[1];
             }
         }
         wsync();  // dX visible to every lane
+        // (F3) controls and slacks in parallel over knots: dv_k = k_r + K dx_k + Kn nu_r
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            if (rr >= nr) break;
+            for (int k = lane; k <= N; k += 64) {
+                const int nv = (k < N ? NU : 0) + ns;
+                const double* GN = SL + (size_t)k * SLOT + sGN;
+                double dv[NV];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    double t = GN[(NX + rr) * NV + v];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) t += GN[j * NV + v] * dXo[rr][k * NX + j];
+#pragma unroll
+                    for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
+                    dv[v] = t;
+                }
+                if (k < N)
+#pragma unroll
+                    for (int v = 0; v < NU; ++v) dUo[rr][k * NU + v] = dv[v];
+                if (ns) dSo[rr][k] = k < N ? dv[NU] : dv[0];
+                (void)nv;
+            }
+        }
         // equality multipliers in parallel over knots: y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k,
         // y_init = -grad V_0(dx_0)
         double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
@@ -888,18 +995,18 @@ struct Solver {
                 for (int j = 0; j < NX; ++j) xn[j] = dXo[rr][(k + 1) * NX + j];
                 double mx0 = 0, mx1 = 0;
                 if (k >= 0) {
-                    const double* s0 = SL + (size_t)k * SLOT;
+                    const double* s0 = SL + (size_t)k * SLOT + sM;
                     const double d0 = dXo[rr][k * NX], d1 = dXo[rr][k * NX + 1];
-                    mx0 = s0[sM + 0] * d0 + s0[sM + 2] * d1;
-                    mx1 = s0[sM + 1] * d0 + s0[sM + 3] * d1;
+                    mx0 = s0[0] * d0 + s0[2] * d1;
+                    mx1 = s0[1] * d0 + s0[3] * d1;
                 }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    double t = v1[vp + rr * NX + i];
+                    double t = v1[i * NCOL + NX + rr];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) t += v1[vP + i * NX + j] * xn[j];
+                    for (int j = 0; j < NX; ++j) t += v1[i * NCOL + j] * xn[j];
 #pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) t += v1[vG + i * NC + cc] * nu_[rr][cc];
+                    for (int cc = 0; cc < NC; ++cc) t += v1[i * NCOL + NX + 2 + cc] * nu_[rr][cc];
                     if (k < 0) {
                         yio[rr][i] = -t;
                     } else {
@@ -920,7 +1027,7 @@ struct Solver {
 #ifdef NLOT_PHASE_PROF
         PROF_T(r4);
         if (b == 0 && lane == 0 && mode == MODE_NEWTON && SC(SC_ITERS) < 4)
-            printf("RIC nr %d build %lld back %lld [PAB %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", nr,
+            printf("RIC nr %d build %lld back %lld [W %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", nr,
                    r1 - r0, r2 - r1, pa, pb, pc, pd, r3 - r2, r4 - r3);
 #endif
         return 0;
