@@ -30,13 +30,41 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxResidentLayers = 2;
 
+// sin and cos of a Fourier-layer argument (|x| up to ~1e3 here: weights ~N(0, 9.4^2), inputs in the
+// workspace box): 3-part Cody-Waite reduction by pi/2 with FMA, Cephes sinf/cosf minimax polynomials on
+// [-pi/4, pi/4] (~1 ulp), quadrant by select.  No slow path: ~20 instructions for both.
+__device__ __forceinline__ void sincos_fourier(float x, float* sn, float* cs) {
+    const float j = rintf(x * 0.636619772367581343f);
+    float r = fmaf(j, -1.57079637050628662109375f, x);
+    r = fmaf(j, 4.37113900018624283e-8f, r);
+    r = fmaf(j, 1.71512451e-15f, r);
+    const float r2 = r * r;
+    const float ps = fmaf(fmaf(fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f), r2 * r, r);
+    const float pc = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2,
+                                    4.166664568298827e-2f), r2, -0.5f), r2, 1.0f);
+    const int q = (int)j & 3;
+    const float s0 = (q & 1) ? pc : ps, c0 = (q & 1) ? ps : pc;
+    *sn = (q & 2) ? -s0 : s0;
+    *cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // row index (hidden unit) held by register r of a 32x32 accumulator on lane-half hl
 __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
+
+// FULL kernels with one hidden layer run 512-thread blocks (8 waves = 2 per SIMD) sharing one LDS copy of
+// the weights, with a per-wave [64][33] staging tile for the reverse sweep (two k-halves at a time).
+__host__ __device__ constexpr size_t mlp_lds_floats(int H, int L, bool staged) {
+    return (size_t)L * H * (H + 1) + 4 * H + (size_t)L * H + (staged ? (size_t)8 * 64 * 33 : 0);
+}
+__host__ __device__ constexpr bool mlp_staged(int H, int L) {
+    return L == 1 && H % 64 == 0 && mlp_lds_floats(H, L, true) * 4 <= 160 * 1024;
+}
+__host__ __device__ constexpr int mlp_threads(int H, int L, bool full) { return full && mlp_staged(H, L) ? 512 : 256; }
 
 template <int H, int L, bool FULL>
 // Point g of the launch (g < cnt * P_per, cnt = *cnt_dev when given: the solver's compacted instances)
 // lives at address g (ld == 0, contiguous rank-major list) or (g % cnt) + (g / cnt) * ld of pts/lam/out.
-__global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+__global__ __launch_bounds__(mlp_threads(H, L, FULL), (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
                                                       const int* __restrict__ cnt_dev, int P_per, int64_t ld,
                                                       const float* __restrict__ lam, MlpOut out) {
     constexpr int HP = H + 1;   // padded LDS row
@@ -48,6 +76,11 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
     float* sb0 = sA1 + H;                               // [H]
     float* sb = sb0 + H;                                // [L][H]
     float* sw = sb + L * H;                             // [H]
+    // FULL kernels whose LDS budget allows: a per-wave [H][33] staging tile for the reverse sweep's
+    // operand and for df/dh0 (runtime k-loops instead of fully unrolled register chains: no spills)
+    constexpr bool STAGED = FULL && mlp_staged(H, L);
+    float* sStage = sw + H;                             // [8 waves][64][33] when STAGED
+    constexpr int TP = mlp_threads(H, L, FULL) / 2;     // points per block tile (32 per wave)
 
     for (int idx = threadIdx.x; idx < L * H * H; idx += blockDim.x) {
         int l = idx / (H * H), rem = idx - l * H * H, j = rem / H, k = rem - j * H;
@@ -69,8 +102,8 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
     const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
     const float scale = w.scale;
 
-    for (int64_t tile = blockIdx.x; tile * 128 < npts; tile += gridDim.x) {
-        const int64_t gi = tile * 128 + wave * 32 + il;
+    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += gridDim.x) {
+        const int64_t gi = tile * TP + wave * 32 + il;
         const bool valid = gi < npts;
         const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
         float px = 0.f, py = 0.f;
@@ -86,7 +119,14 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
         for (int s = 0; s < H / 2; ++s) {
             const int k = 2 * s + hl;
             const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
-            const float h0 = fourier ? cosf(z) * scale : (z > 0.f ? z : 0.f);
+            float h0;
+            if (fourier) {
+                float sn, cs;
+                sincos_fourier(z, &sn, &cs);
+                h0 = cs * scale;
+            } else {
+                h0 = z > 0.f ? z : 0.f;
+            }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const float a = sW[(t * 32 + il) * HP + k];
@@ -153,6 +193,69 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
         } else {
             // ---------------- reverse sweep ----------------
             const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
+            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+            if constexpr (STAGED) {
+                float* sE = sStage + wave * (64 * 33);  // [k within the half][point], padded
+                const uint64_t m = mask[0];
+                f32x16 g[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) g[t] = f32x16{};
+                // g = W^T e with e = lam * w_out .* mask, staged 64 rows of k at a time
+#pragma unroll
+                for (int hh = 0; hh < H / 64; ++hh) {
+                    __syncthreads();
+#pragma unroll
+                    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int t = 2 * hh + tt, kl = tt * 32 + acc_row(r, hl);
+                            sE[kl * 33 + il] = ((m >> (t * 16 + r)) & 1) ? lm * sw[t * 32 + acc_row(r, hl)] : 0.f;
+                        }
+                    __syncthreads();
+#pragma unroll 4
+                    for (int s = 0; s < 32; ++s) {
+                        const int kl = 2 * s + hl, k = hh * 64 + kl;
+                        const float bv = sE[kl * 33 + il];
+#pragma unroll
+                        for (int t = 0; t < NT; ++t) {
+                            const float a = sW[k * HP + t * 32 + il];
+                            g[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, g[t], 0, 0, 0);
+                        }
+                    }
+                }
+                // g = df/dh0 (x lam): contract with the input layer's derivatives, lane = (k, point)
+#pragma unroll
+                for (int hh = 0; hh < H / 64; ++hh) {
+                    __syncthreads();
+#pragma unroll
+                    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) sE[(tt * 32 + acc_row(r, hl)) * 33 + il] = g[2 * hh + tt][r];
+                    __syncthreads();
+#pragma unroll 2
+                    for (int s = 0; s < 32; ++s) {
+                        const int kl = 2 * s + hl, k = hh * 64 + kl;
+                        const float ax = sA0[k], ay = sA1[k];
+                        const float z = fmaf(py, ay, px * ax) + sb0[k];
+                        const float d = sE[kl * 33 + il];
+                        float dz, c2;
+                        if (fourier) {
+                            float sn, cs;
+                            sincos_fourier(z, &sn, &cs);
+                            dz = d * (-scale * sn);
+                            c2 = d * (-scale * cs);
+                        } else {
+                            dz = z > 0.f ? d : 0.f;
+                            c2 = 0.f;
+                        }
+                        gx = fmaf(ax, dz, gx);
+                        gy = fmaf(ay, dz, gy);
+                        hxx = fmaf(ax * ax, c2, hxx);
+                        hxy = fmaf(ax * ay, c2, hxy);
+                        hyy = fmaf(ay * ay, c2, hyy);
+                    }
+                }
+            } else {
             // e = lam * w_out .* mask_top  (in place, accumulator layout)
             {
                 const uint64_t m = mask[L - 1];
@@ -192,7 +295,6 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
                 }
             }
             // acc = df/dh0 (x lam); contract with the input layer's derivatives
-            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -204,7 +306,7 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
                     float dz, c2;
                     if (fourier) {
                         float sn, cs;
-                        sincosf(z, &sn, &cs);
+                        sincos_fourier(z, &sn, &cs);
                         dz = d * (-scale * sn);
                         c2 = d * (-scale * cs);
                     } else {
@@ -217,6 +319,7 @@ __global__ __launch_bounds__(256, (FULL || L > 1) ? 1 : 2) void mlp_kernel(MlpDe
                     hxy = fmaf(ax * ay, c2, hxy);
                     hyy = fmaf(ay * ay, c2, hyy);
                 }
+            }
             gx += __shfl_xor(gx, 32);
             gy += __shfl_xor(gy, 32);
             hxx += __shfl_xor(hxx, 32);
@@ -255,18 +358,19 @@ static int num_cus() {
 template <int H, int L, bool FULL>
 static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                     const float* lam, const MlpOut& out, hipStream_t stream) {
-    const size_t lds = sizeof(float) * ((size_t)w.n_hidden * H * (H + 1) + 4 * H + (size_t)w.n_hidden * H);
+    const size_t lds = sizeof(float) * mlp_lds_floats(H, L, FULL && mlp_staged(H, L));
     static bool attr_set = false;
     if (!attr_set) {
         NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_kernel<H, L, FULL>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    int64_t tiles = (n * P_per + 127) / 128;
+    constexpr int NTH = mlp_threads(H, L, FULL);
+    int64_t tiles = (n * P_per + NTH / 2 - 1) / (NTH / 2);
     // resident blocks per CU: VGPR-limited (FULL: 1 wave/SIMD) and LDS-limited
     int64_t cap = (int64_t)num_cus() * ((!FULL && L == 1 && lds <= 80 * 1024) ? 2 : 1);
     int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
-    hipLaunchKernelGGL((mlp_kernel<H, L, FULL>), dim3(grid), dim3(256), lds, stream, w, pts, n, n_dev, P_per, ld, lam, out);
+    hipLaunchKernelGGL((mlp_kernel<H, L, FULL>), dim3(grid), dim3(NTH), lds, stream, w, pts, n, n_dev, P_per, ld, lam, out);
     NLOT_HIP_CHECK(hipGetLastError());
     return NLOT_OK;
 }
