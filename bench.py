@@ -39,9 +39,9 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=16384, help="instances per GPU per step")
+    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step (SURVEY.md §8d config 3: 1024 / 16384 / 65536)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=48, help="instances for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
