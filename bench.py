@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from nlotrajectories_amd import _abi  # noqa: E402
+from nlotrajectories_amd.dist import gather_solutions, max_over_ranks, rank_world, sum_over_ranks  # noqa: E402
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
 from nlotrajectories_amd.problem import METRIC_PROBLEM  # noqa: E402
@@ -52,9 +53,7 @@ def parse():
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, local, world = rank_world()
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -78,11 +77,8 @@ def main():
     def step():
         r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws)
         solved = (r["status"] == 0)
-        if world > 1:  # gather solved trajectories to every rank (RCCL over xGMI)
-            Xg = [torch.empty_like(r["X"]) for _ in range(world)]
-            sg = [torch.empty_like(r["status"]) for _ in range(world)]
-            dist.all_gather(Xg, r["X"])
-            dist.all_gather(sg, r["status"])
+        if world > 1:  # gather the solutions to every rank (RCCL over xGMI): the only collective
+            gather_solutions(r, keys=("X", "U", "cost", "status"))
         return r, int(solved.sum().item())
 
     from nlotrajectories_amd.solver import workspace_bytes
@@ -113,13 +109,8 @@ def main():
     elapsed = time.perf_counter() - t0
     set_timing(False)
     status_counts = torch.bincount(r["status"].long(), minlength=4).cpu().numpy().tolist()
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        s = torch.tensor([solved_total], device=dev, dtype=torch.int64)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        solved_total = int(s.item())
+    elapsed = max_over_ranks(elapsed, dev)
+    solved_total = sum_over_ranks(solved_total, dev)
 
     # roofline of the dominant kernel: the full (value + gradient + Hessian) SDF-MLP launch
     flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1
