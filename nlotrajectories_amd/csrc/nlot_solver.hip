@@ -1088,12 +1088,12 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
 // afterwards the next NSPEC halvings that stay >= alpha_min (speculative backtracking: the same
 // accepted alpha as sequential halving, because the acceptance test of one candidate does not
 // depend on the others)
-__device__ __forceinline__ int n_candidates(const Ws& ws, int b) {
+__device__ __forceinline__ int n_candidates(const Ws& ws, int b, int nspec) {
     if (SC(SC_TRIALS) == 0) return 1;
     const double amin = SC(SC_AMIN);
     double a = SC(SC_ALPHA);
     int n = 1;
-    for (int j = 1; j < NSPEC; ++j) {
+    for (int j = 1; j < nspec; ++j) {
         a *= 0.5;
         if (a < amin) break;
         ++n;
@@ -1102,7 +1102,9 @@ __device__ __forceinline__ int n_candidates(const Ws& ws, int b) {
 }
 
 // corners of X (+ alpha dX) of instances in the wanted phase, appended to the compacted point list
-__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, const int* __restrict__ active, int trial) {
+// nspec: step lengths per line-search round (host-chosen per global step; the accepted alpha does not
+// depend on it, only the number of rounds)
+__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, const int* __restrict__ active, int trial, int nspec) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const int b = active[blockIdx.x], lane = threadIdx.x;
@@ -1111,7 +1113,7 @@ __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ p
     if (!want) return;
     // trial: the first round evaluates alpha_max; later rounds the next NSPEC halvings that stay
     // >= alpha_min (speculative backtracking, identical outcome to sequential halving)
-    const int ncand = trial ? n_candidates(ws, b) : 1;
+    const int ncand = trial ? n_candidates(ws, b, nspec) : 1;
     const double a0 = trial ? SC(SC_ALPHA) : 0.0;
     int rank = 0;
     if (lane == 0) {
@@ -1855,7 +1857,7 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
 template <int DYN>
 __global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* __restrict__ next,
-                                               const double* __restrict__ x0, const double* __restrict__ xg) {
+                                               const double* __restrict__ x0, const double* __restrict__ xg, int nspec) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -1865,7 +1867,7 @@ __global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ p
     if (ph == PH_LS) {
         const int N = dm.N, M = dm.M, nc = dm.nc;
         const double a0 = SC(SC_ALPHA), mu = SC(SC_MU);
-        const int rank0 = (int)SC(SC_RANK), ncand = n_candidates(ws, b);
+        const int rank0 = (int)SC(SC_RANK), ncand = n_candidates(ws, b, nspec);  // same count as k_points
         int ok = 0, ftype = 0, armijo = 0, cnd = 0;
         double al = a0, th = 0, pht = 0;
         const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
@@ -2112,6 +2114,9 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)k_iterate<DYN, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)slot_bytes));
     g_stats.slots_in_lds = slots_lds ? 1 : 0;
+    int spec_threshold = 8192, spec_bulk = 1;  // measured best of {512, 2048, 8192} x {1, 2} (B = 65536)
+    if (const char* e = getenv("NLOT_SPEC_THRESHOLD")) spec_threshold = atoi(e);
+    if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
     const int max_steps = (o.max_iter + 2) * 64;
     int rc = NLOT_OK, n_active = Bi, cur = 0;
     for (int step = 0; step < max_steps && n_active > 0; ++step) {
@@ -2119,13 +2124,16 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         int* nxt = ws.act[cur ^ 1];
         NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 4 * sizeof(int), st));
         if (use_mlp) {
-            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0);
+            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0, 1);
             if (ev[0]) hipEventRecord(ev[0], st);
             // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
             rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[1], st);
         }
+        // speculative backtracking only while the GPU is latency-bound (few active instances); in the
+        // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
+        const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
         if (ev[4]) hipEventRecord(ev[4], st);
         if (slots_lds)
             hipLaunchKernelGGL((k_iterate<DYN, true>), dim3(n_active), dim3(64), slot_bytes, st, dP, dD, o, dW, act, x0, xg);
@@ -2133,7 +2141,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             hipLaunchKernelGGL((k_iterate<DYN, false>), dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg);
         if (ev[4]) hipEventRecord(ev[5], st);
         if (use_mlp) {
-            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1);
+            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1, nspec);
             if (ev[0]) hipEventRecord(ev[2], st);
             rc = launch_mlp_strided(mlp->dev, ws.pts, (int64_t)n_active * NSPEC, ws.cnt + 1, (int)P, 0, nullptr, mo, false, st);
             if (rc) break;
@@ -2141,7 +2149,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             g_stats.mlp_full_launches++;
             g_stats.mlp_value_launches++;
         }
-        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg);
+        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
         NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, ws.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
