@@ -183,6 +183,18 @@ class MlpWeights:
             return MlpWeights(_abi.MLP_IN_LINEAR_RELU, H, len(Ws), 1.0, float(g(model.output_layer.bias)[0]), arrays)
         raise TypeError(f"unsupported model type {type(model).__name__} (DESIGN.md §7)")
 
+    def save(self, path) -> None:
+        """Plain npz (no pickle): the arrays plus the scalar fields."""
+        np.savez(path, in_kind=self.in_kind, hidden=self.hidden, n_hidden=self.n_hidden,
+                 fourier_scale=self.fourier_scale, b_out=self.b_out, **self.arrays)
+
+    @staticmethod
+    def load(path) -> "MlpWeights":
+        z = np.load(path, allow_pickle=False)
+        arrays = {k: z[k].astype(np.float32) for k in ("A", "b0", "W", "b", "w_out")}
+        return MlpWeights(int(z["in_kind"]), int(z["hidden"]), int(z["n_hidden"]), float(z["fourier_scale"]),
+                          float(z["b_out"]), arrays)
+
     @staticmethod
     def artefact() -> "MlpWeights":
         """The reference artefact _l4c_generated/nn_sdf.pt (FourierMLP 2-128-128-1, scale 10),
