@@ -9,13 +9,11 @@ pytestmark = pytest.mark.gpu
 CFG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs")
 
 
-@pytest.mark.parametrize("name,weights", [("benchmark_2_unicycle_circle", None),
-                                          ("benchmark_3_unicycle_convex", "artefact")])
-def test_run_benchmark_cli(tmp_path, name, weights):
+def test_run_benchmark_cli(tmp_path):
     from nlotrajectories_amd.cli import CSV_HEADER, main
 
-    main(["--config", os.path.join(CFG, name + ".yaml"), "--initializer", "linear", "--results", str(tmp_path)]
-         + (["--weights", weights] if weights else []))
+    name = "benchmark_2_unicycle_circle"
+    main(["--config", os.path.join(CFG, name + ".yaml"), "--initializer", "linear", "--results", str(tmp_path)])
     rows = open(tmp_path / f"{name}_results.csv").read().strip().split("\n")
     assert rows[0] == CSV_HEADER
     vals = rows[1].split(",")
@@ -30,3 +28,19 @@ def test_run_benchmark_returns_trajectory():
                                  verbose=False)
     assert status == "success" and X.shape == (5, 51) and U.shape == (2, 50)
     assert np.abs(X[:, 0] - [0, 0, 0.785, 0, 0]).max() < 1e-4
+
+
+def test_learned_config_matches_oracle():
+    """benchmark_3 with the learned SDF (artefact weights): the CLI's outcome equals the oracle's on the
+    same NLP (both end in a line-search failure from the linear guess under the adaptive setting)."""
+    import oracle as O
+    from nlotrajectories_amd.cli import run_benchmark
+    from nlotrajectories_amd.config import Config
+    from nlotrajectories_amd.nn import MlpWeights
+
+    f = os.path.join(CFG, "benchmark_3_unicycle_convex.yaml")
+    X, U, status = run_benchmark(f, initializer="linear", weights="artefact", verbose=False)
+    cfg = Config.load(f)
+    rc = O.solve_one(cfg.to_problem(), cfg.body.start_state, cfg.body.goal_state, O.HostMlp(MlpWeights.artefact()))
+    assert status == ("success" if rc["status"] == 0 else "failed")
+    assert X.shape == (5, 41) and U.shape == (2, 40)
