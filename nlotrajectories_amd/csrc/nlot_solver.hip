@@ -1619,14 +1619,75 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
             dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
             if (dw > 1e40) return finish(NLOT_NUMERIC);
         }
+        PROF_T(tq0);
         if (use_qf) {
         qf_store(0.0, false);
         qf_store(avg, true);
         const double* qa_ = &AT(qa, 0);
         const double* qc_ = &AT(qc, 0);
         const double dual_t = dsq_w / (double)n_dual_, pri_t = psq_w / (double)n_pri_;
+        // Fast path (N + 1 <= 64 knots, N NU <= 128): every complementarity pair a lane owns (<= 6) is
+        // cached in registers once; q(sigma) is then FMA work plus three wave reductions, and the
+        // fraction to the boundary is tau / max(-dslack / slack) (reciprocals precomputed, no division
+        // per pair).  Other sizes take the generic loop below.
+        const bool qf_fast = N * NU <= 128 && N + 1 <= 64 && (N + 1) * M <= 64;
+        constexpr int QP = 6;
+        double c_sl[QP], c_isl[QP], c_da[QP], c_dc[QP], c_z[QP], c_iz[QP], c_za[QP], c_zc[QP];
+        if (qf_fast) {
+            auto put = [&](int j, double sl, double da, double dc, double z, double za, double zc) {
+                c_sl[j] = sl;
+                c_isl[j] = 1.0 / sl;
+                c_da[j] = da;
+                c_dc[j] = dc;
+                c_z[j] = z;
+                c_iz[j] = 1.0 / z;
+                c_za[j] = za;
+                c_zc[j] = zc;
+            };
+            auto none = [&](int j) {
+                c_sl[j] = 1.0; c_isl[j] = 0.0; c_da[j] = c_dc[j] = 0.0;
+                c_z[j] = 0.0; c_iz[j] = 0.0; c_za[j] = c_zc[j] = 0.0;
+            };
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = lane + 64 * h;
+                if (e < N * NU) {
+                    const double u = AT(U, e), da = qa_[oU + e], dc = qc_[oU + e];
+                    put(2 * h, u - p.umin[e % NU], da, dc, AT(zl, e), qa_[ozl + e], qc_[ozl + e]);
+                    put(2 * h + 1, p.umax[e % NU] - u, -da, -dc, AT(zu, e), qa_[ozu + e], qc_[ozu + e]);
+                } else {
+                    none(2 * h);
+                    none(2 * h + 1);
+                }
+            }
+            if (dm.ns && lane <= N) put(4, AT(S, lane), qa_[oS + lane], qc_[oS + lane], AT(zs, lane), qa_[ozs + lane],
+                                        qc_[ozs + lane]);
+            else none(4);
+            if (lane < (N + 1) * M) put(5, AT(T, lane), qa_[oT + lane], qc_[oT + lane], AT(vt, lane), qa_[ovt + lane],
+                                        qc_[ovt + lane]);
+            else none(5);
+        }
         auto qf = [&](double sig) {  // q(sigma): 2-norm-squared, per-element averaged (oracle qf_eval)
             const double tq = fmax(0.99, 1.0 - sig * avg);
+            if (qf_fast) {
+                double rp = 0.0, rd = 0.0;
+#pragma unroll
+                for (int j = 0; j < QP; ++j) {
+                    rp = fmax(rp, -(c_da[j] + sig * c_dc[j]) * c_isl[j]);
+                    rd = fmax(rd, -(c_za[j] + sig * c_zc[j]) * c_iz[j]);
+                }
+                rp = wmax(rp);
+                rd = wmax(rd);
+                const double ap = rp > 0.0 ? fmin(1.0, tq / rp) : 1.0, ad = rd > 0.0 ? fmin(1.0, tq / rd) : 1.0;
+                double csq = 0.0;
+#pragma unroll
+                for (int j = 0; j < QP; ++j) {
+                    const double c = (c_sl[j] + ap * (c_da[j] + sig * c_dc[j])) * (c_z[j] + ad * (c_za[j] + sig * c_zc[j]));
+                    csq += c * c;
+                }
+                csq = wsum(csq);
+                return (1.0 - ad) * (1.0 - ad) * dual_t + (1.0 - ap) * (1.0 - ap) * pri_t + csq / nzc;
+            }
             double ap = 1.0, ad = 1.0;
             for (int e = lane; e < N * NU; e += 64) {
                 const double u = AT(U, e), du = qa_[oU + e] + sig * qc_[oU + e];
@@ -1764,6 +1825,10 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         }
         wsync();
         }
+#ifdef NLOT_PHASE_PROF
+        PROF_T(tq1);
+        if (b == 0 && lane == 0 && iters < 4) printf("QF store+sigma+combine %lld (x10ns)\n", tq1 - tq0);
+#endif
     }
     // ---- recover dt, yd+, dz; fraction to the boundary; line-search reference values ----
     PROF_T(t3);
