@@ -41,6 +41,10 @@ enum Scal {
     SC_MU, SC_TAU, SC_DWLAST, SC_THMAX, SC_THMIN, SC_ALPHA, SC_AMAX, SC_AMIN, SC_AZ, SC_THETA, SC_PHI, SC_GD,
     SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_NCAND,
     SC_FREE, SC_MUMAX, SC_NAF,  // adaptive mu: free-mode flag, mu_max, progress-filter entries
+    // hand-off k_iter_a -> k_ric -> k_iter_b: Newton-solve state (0 idle, 1 pending, 2 solved, 3 LSQ
+    // failed), its barrier parameters and right-hand-side count, and the optimality scalars the
+    // quality-function oracle needs
+    SC_RIC, SC_RMU0, SC_RMU1, SC_RNR, SC_USEQF, SC_AVG, SC_DSQ, SC_PSQ, SC_NZC,
     SC_COUNT
 };
 constexpr int FILT_MAX = 64;
@@ -89,7 +93,6 @@ __host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * (nx + 2 +
 __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
     return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
 }
-constexpr size_t kLdsBudget = 150 * 1024;  // slots go to LDS when they fit, else to the global scratch
 
 // instance-major arrays: (name, per-instance length)
 #define NLOT_WS_ARRAYS(X_)                                                                             \
@@ -541,9 +544,9 @@ struct Solver {
     // Build every stage's matrices in parallel (lane = knot): [H | g] -> hg (HBM); [A B 0 | c], M -> slot.
     template <bool LDS>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                        double dw, double mu0, double mu1, int nr, double* SL) {
+                                        double dw, double mu0, double mu1, int nr, double* SL, int stride = 64) {
         const int N = dm.N;
-        for (int k = lane; k <= N; k += 64) {
+        for (int k = lane; k <= N; k += stride) {
             double* o = SL + (size_t)k * SLOT;
             stage(p, dm, ws, b, k, mode, dw, mu0, mu1, nr, &AT(hg, k * HG));
             double A[NX][NX], Bu[NX][NU];
@@ -587,7 +590,8 @@ struct Solver {
     // Pivoted LDL^T of the symmetric 3x3 Q_vv held in QE (rows/cols NX..NX+2), identical in arithmetic
     // and pivot order to the generic ldl_factor / the oracle's ldl(); the permutation is applied through
     // the (uniform, broadcast) LDS addresses instead of register swaps.  Returns 0 or 2 (singular).
-    __device__ __forceinline__ static int ldl3(const Sh& sh, int o[3], double& d0, double& d1, double& d2,
+    template <class ShT>
+    __device__ __forceinline__ static int ldl3(const ShT& sh, int o[3], double& d0, double& d1, double& d2,
                                                double& l10, double& l20, double& l21, int& nneg) {
         auto q = [&](int i, int j) { return sh.QE[NX + i][NX + j]; };
         double scale = 1e-300;
@@ -1035,6 +1039,645 @@ struct Solver {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Lane-group Riccati (kernel k_ric): G lanes per instance, 64 / G instances per wavefront.
+// Lane j of a group owns column j of the stage's extended matrices.  It keeps W[:, j] and QE[:, j]
+// in registers, plus its gain column and (terminal columns) its row of [Psi | psi].  LDS holds only
+// what other lanes read: the staged [A B 0 | c] | M of the stage (double-buffered; HBM loads run a
+// few stages ahead in registers), the value function, the three control columns of QE (Q_vv, Q_xv)
+// and the gains.  Per stage: 3 wave-local LDS syncs, each followed by one batch of 16-byte reads;
+// the 3x3 pivots are inverted once (reciprocals).
+// ---------------------------------------------------------------------------------------------
+template <int DYN>
+struct RicG {
+    using SV = Solver<DYN>;
+    static constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NC = SV::NC;
+    static constexpr int NCOL = SV::NCOL, NQE = SV::NQE, NAB = SV::NAB;
+    static constexpr int G = NQE <= 16 ? 16 : 32;  // lanes per instance (>= one per QE column)
+    static constexpr int IPW = 64 / G;             // instances per wavefront
+    static constexpr int NABM = NX * NAB + 4;      // [A B 0 | c] | M, contiguous at the start of a slot
+    static constexpr int NST = (NABM + G - 1) / G; // staged doubles per lane
+    static constexpr int ev(int n) { return n + (n & 1); }  // rows padded to 16 bytes
+    static constexpr int NABP = ev(NAB), NXP = ev(NX), NZP = ev(NZ), NCOLP = ev(NCOL);
+    static_assert(SV::sAB == 0 && SV::sM == NX * NAB && NCOL <= NQE && NQE <= G && NV <= 4, "RicG layout");
+    struct alignas(16) Sh {  // per instance; every row starts on a 16-byte boundary
+        double ab[2][NX * NABP + 4];  // [A B 0 | c] rows (padded) | M
+        double VE[NX][NCOLP];         // value function [P | p_0 p_1 | Gamma] of the stage after
+        double QT[NV][NZP];           // columns NX .. NX+NV-1 of QE, transposed
+        double VU[NCOL][NXP];         // value update before symmetrisation, column-major
+        double cols[NCOL][4];         // gains
+        double PE[NC][NC + 2];
+    };
+};
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+// Newton (or least-squares) solve of the instances whose stage matrices k_iter_a built (SC_RIC = 1),
+// with IPOPT's inertia correction: on a wrong inertia the group rebuilds its stages with the next
+// delta_w and factorises again.  Outputs: dX dU dS yi_n yk_n yt_n (and the second right-hand side).
+template <int DYN>
+__global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+                                            const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
+                                            int mode) {
+    using R = RicG<DYN>;
+    using SV = Solver<DYN>;
+    constexpr int NX = R::NX, NU = R::NU, NV = R::NV, NZ = R::NZ, NC = R::NC, NCOL = R::NCOL, NQE = R::NQE;
+    constexpr int NAB = R::NAB, G = R::G, NABM = R::NABM, NST = R::NST, NABP = R::NABP, NCOLP = R::NCOLP;
+    constexpr int SLOT = SV::SLOT, HG = SV::HG, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    __shared__ typename R::Sh shg[R::IPW];
+    const int grp = threadIdx.x / G, l = threadIdx.x % G, gb = grp * G;
+    const int si = blockIdx.x * R::IPW + grp;
+    if (si >= n_active) return;
+    const int b = active[si];
+    if ((int)SC(SC_RIC) != 1) return;
+    typename R::Sh& sh = shg[grp];
+    const int N = dm.N, nc = dm.nc, ns = dm.ns;
+    const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
+    const int nr = (int)SC(SC_RNR);
+    double* SL = &AT(stg, 0);
+    const int j = l;  // QE column of this lane
+    const int gc = j < NX ? j : ((j >= NZ && j < NQE) ? NX + (j - NZ) : -1);  // gain column (qe_col^-1)
+    const int a_pe = j - (NZ + 2);                                              // [Psi | psi] row
+    const bool own_pe = a_pe >= 0 && a_pe < NC;
+    double nu_[2][NC], dx0[NX];
+    auto abc_nz = [&](const double* AB, int qq) { return AB[qq * R::NABP + NZ]; };
+
+    // backward sweep + terminal multipliers; 0, or 1 on a wrong inertia (uniform within the group)
+    auto backward = [&]() -> int {
+        for (int e = l; e < NX * NCOLP; e += G) (&sh.VE[0][0])[e] = 0.0;
+        double pe[NC + 2];
+#pragma unroll
+        for (int c = 0; c < NC + 2; ++c) pe[c] = 0.0;
+        if (mode == MODE_NEWTON && l == 0) SC(SC_DC) = 0.0;
+        // Stage inputs from HBM (written by k_iter_a, read once): a register ring RING stages deep hides
+        // the load latency behind the recursion (slot 0 = stage k, slot s = stage k - s).
+        constexpr int RING = 2;
+        double pf[RING][NZ], sf[RING][NST], w[NX], q[NZ], gcol[NV], vr[NX];
+        auto load_stage = [&](int k, double* h, double* s) {
+            if (k < 0) return;
+            const double* hgk = &AT(hg, k * HG);  // hg column j ([H | g_0 g_1], zero beyond nr)
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) h[i] = j < NZ + nr ? hgk[i * (NZ + 2) + j] : 0.0;
+            const double* s0 = SL + (size_t)k * SLOT;
+#pragma unroll
+            for (int t = 0; t < NST; ++t) {
+                const int e = l + G * t;
+                s[t] = e < NABM ? s0[e] : 0.0;
+            }
+        };
+        auto put_st = [&](int buf, const double* s) {  // slot order -> padded LDS rows
+#pragma unroll
+            for (int t = 0; t < NST; ++t) {
+                const int e = l + G * t;
+                if (e < NABM) sh.ab[buf][e < NX * NAB ? (e / NAB) * NABP + e % NAB : NX * NABP + (e - NX * NAB)] = s[t];
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < RING; ++r) load_stage(N - r, pf[r], sf[r]);
+        put_st(N & 1, sf[0]);
+        int negsum = 0;
+        const bool wcol = j < NZ + 2;              // W column j is P AB (+ p_r), not a Gamma pass-through
+        const int cc = j < NZ ? j : NZ;            // AB column (the c column for the p_r columns)
+        const int jc = j >= NZ && j < NQE ? NX + j - NZ : 0;  // VE column carried into W
+        const bool vlane = j >= NX && j < NX + NV;  // control columns: Q_vv, Q_xv
+        xsync<true>();
+        for (int k = N; k >= 0; --k) {
+            const int nv = (k < N ? NU : 0) + ns;
+            const double* AB = sh.ab[k & 1];
+            const double* Mk = AB + NX * NABP;
+            // ---- batch 1: P (rows of VE), this lane's VE column and AB column, M ----
+            double P[NX][NX], vc[NX], abc[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const d2v* row = reinterpret_cast<const d2v*>(&sh.VE[r][0]);
+#pragma unroll
+                for (int c2 = 0; c2 < NX / 2; ++c2) {
+                    const d2v v = row[c2];
+                    P[r][2 * c2] = v.x;
+                    P[r][2 * c2 + 1] = v.y;
+                }
+                if (NX & 1) P[r][NX - 1] = sh.VE[r][NX - 1];
+                vc[r] = sh.VE[r][jc];
+                abc[r] = AB[r * NABP + cc];
+            }
+            const d2v m01 = reinterpret_cast<const d2v*>(Mk)[0], m23 = reinterpret_cast<const d2v*>(Mk)[1];
+            // (1) W[:, j] = [P AB | P c + p_0 | P c + p_1 | G][:, j]
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                double t = j < NZ ? 0.0 : vc[r];
+#pragma unroll
+                for (int qq = 0; qq < NX; ++qq) t += P[r][qq] * abc[qq];
+                w[r] = wcol ? t : vc[r];
+            }
+            // (2) QE[:, j] = [H | g] + cross + AB' W  (cross: path-length coupling through the dynamics)
+            const double mj0 = j == 0 ? m01.x : m23.x, mj1 = j == 0 ? m01.y : m23.y;
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+                double ab_i[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) ab_i[r] = AB[r * NABP + i];
+                double t = pf[0][i];
+                if (i < 2) {
+                    const double x = (i == 0 ? m01.x : m23.x) * abc[0] + (i == 0 ? m01.y : m23.y) * abc[1];
+                    t = wcol ? t + x : t;
+                }
+                {
+                    const double x = mj0 * ab_i[0] + mj1 * ab_i[1];
+                    t = (wcol && j < 2) ? t + x : t;
+                }
+#pragma unroll
+                for (int r = 0; r < NX; ++r) t += ab_i[r] * w[r];
+                q[i] = t;
+            }
+            if (vlane) {
+                d2v* dst = reinterpret_cast<d2v*>(&sh.QT[j - NX][0]);
+#pragma unroll
+                for (int i2 = 0; i2 < NZ / 2; ++i2) dst[i2] = d2v{q[2 * i2], q[2 * i2 + 1]};
+                if (NZ & 1) sh.QT[j - NX][NZ - 1] = q[NZ - 1];
+            }
+            xsync<true>();
+            // ---- batch 2: the control columns of QE (Q_vv, Q_xv) ----
+            double Qv[NV][NZ];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const d2v* src = reinterpret_cast<const d2v*>(&sh.QT[v][0]);
+#pragma unroll
+                for (int i2 = 0; i2 < NZ / 2; ++i2) {
+                    const d2v x = src[i2];
+                    Qv[v][2 * i2] = x.x;
+                    Qv[v][2 * i2 + 1] = x.y;
+                }
+                if (NZ & 1) Qv[v][NZ - 1] = sh.QT[v][NZ - 1];
+            }
+            // (3) Q_vv factorised by every lane (identical, uniform inertia decision); lane j solves its
+            //     gain column in registers
+#pragma unroll
+            for (int v = 0; v < NV; ++v) gcol[v] = 0.0;
+            if (nv == 3 && NV == 3) {
+                // pivoted LDL^T of the symmetric 3x3 (pivot order of ldl_factor: largest diagonal first,
+                // then the larger remaining diagonal), reciprocal pivots
+                auto qv = [&](int a, int c) {  // Q_vv[a][c] = QE[NX + a][NX + c] = Qv[c][NX + a] (static a, c)
+                    return Qv[c][NX + a];
+                };
+                double scale = 1e-300;
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) scale = fmax(scale, fabs(qv(a, c)));
+                const double a00 = qv(0, 0), a11 = qv(1, 1), a22 = qv(2, 2);
+                int pv = 0;
+                if (fabs(a11) > fabs(a00)) pv = 1;
+                if (fabs(a22) > fabs(pv == 1 ? a11 : a00)) pv = 2;
+                int o0 = pv, o1 = pv == 1 ? 0 : 1, o2 = pv == 2 ? 0 : 2;
+                // pivoted entries by LDS address (a register array indexed at run time would go to scratch)
+                const double d0 = sh.QT[o0][NX + o0], c1 = sh.QT[o0][NX + o1], c2 = sh.QT[o0][NX + o2];
+                const double e11 = sh.QT[o1][NX + o1], e21 = sh.QT[o1][NX + o2], e22 = sh.QT[o2][NX + o2];
+                if (!(fabs(d0) > 1e-13 * scale) || !isfinite(d0)) return 1;
+                const double i0 = 1.0 / d0;
+                double l10 = c1 * i0, l20 = c2 * i0;
+                double b11 = e11 - c1 * l10;
+                const double b21 = e21 - c2 * l10;
+                double b22 = e22 - c2 * l20;
+                if (fabs(b22) > fabs(b11)) {  // swap positions 1 and 2 (rows of L included)
+                    const int t = o1;
+                    o1 = o2;
+                    o2 = t;
+                    const double tb = b11;
+                    b11 = b22;
+                    b22 = tb;
+                    const double tl = l10;
+                    l10 = l20;
+                    l20 = tl;
+                }
+                const double d1 = b11;
+                if (!(fabs(d1) > 1e-13 * scale) || !isfinite(d1)) return 1;
+                const double i1 = 1.0 / d1, l21 = b21 * i1, d2 = b22 - b21 * l21;
+                if (!(fabs(d2) > 1e-13 * scale) || !isfinite(d2)) return 1;
+                const double i2 = 1.0 / d2;
+                negsum += (d0 < 0) + (d1 < 0) + (d2 < 0);
+                if (negsum > nc) return 1;
+                if (gc >= 0) {
+                    const double x0 = q[NX], x1 = q[NX + 1], x2 = q[NX + 2];
+                    // permutations as exact 0/1 blends (selects by a run-time index become scratch arrays)
+                    auto pick = [&](int o) { return (o == 0 ? 1.0 : 0.0) * x0 + (o == 1 ? 1.0 : 0.0) * x1 + (o == 2 ? 1.0 : 0.0) * x2; };
+                    double t0 = pick(o0), t1 = pick(o1), t2 = pick(o2);
+                    t1 -= l10 * t0;
+                    t2 -= l20 * t0;
+                    t2 -= l21 * t1;
+                    t0 *= i0;
+                    t1 *= i1;
+                    t2 *= i2;
+                    t1 -= l21 * t2;
+                    t0 -= l10 * t1;
+                    t0 -= l20 * t2;
+#pragma unroll
+                    for (int v = 0; v < 3; ++v)
+                        gcol[v] = -((o0 == v ? 1.0 : 0.0) * t0 + (o1 == v ? 1.0 : 0.0) * t1 + (o2 == v ? 1.0 : 0.0) * t2);
+                }
+            } else if (nv > 0) {
+                double L[NV][NV];
+                int perm[NV], nneg;
+#pragma unroll
+                for (int a = 0; a < NV; ++a)
+#pragma unroll
+                    for (int c = 0; c < NV; ++c) L[a][c] = (a < nv && c < nv) ? Qv[c][NX + a] : 0.0;
+                if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
+                negsum += nneg;
+                if (negsum > nc) return 1;
+                if (gc >= 0) {
+                    double col[NV];
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? -q[NX + v] : 0.0;
+                    ldl_solve1<NV>(L, nv, perm, col);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) gcol[v] = v < nv ? col[v] : 0.0;
+                }
+            }
+            // (4a) gains to LDS and to the slot (forward sweep); raw value update of column gc
+            if (gc >= 0) {
+                double* GN = SL + (size_t)k * SLOT + sGN;
+                d2v* cd = reinterpret_cast<d2v*>(&sh.cols[gc][0]);
+                cd[0] = d2v{gcol[0], NV > 1 ? gcol[NV > 1 ? 1 : 0] : 0.0};
+                if (NV > 2) cd[1] = d2v{gcol[NV > 2 ? 2 : 0], 0.0};
+#pragma unroll
+                for (int v = 0; v < NV; ++v) GN[gc * NV + v] = gcol[v];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    double t = q[i];
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) t += Qv[v][i] * gcol[v];
+                    vr[i] = t;
+                }
+                d2v* vd = reinterpret_cast<d2v*>(&sh.VU[gc][0]);
+#pragma unroll
+                for (int i2 = 0; i2 < NX / 2; ++i2) vd[i2] = d2v{vr[2 * i2], vr[2 * i2 + 1]};
+                if (NX & 1) sh.VU[gc][NX - 1] = vr[NX - 1];
+            }
+            xsync<true>();
+            // ---- batch 3: transposed raw values (symmetrisation), gains of the terminal columns ----
+            if (gc >= 0) {
+                double tr[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) tr[i] = sh.VU[i][gc < NX ? gc : 0];
+                double* vfk = &AT(vf, k * VF);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    double t = vr[i];
+                    if (gc < NX && gc != i) t = 0.5 * (t + tr[i]);
+                    if (k == N && gc >= NX + 2) {
+                        const int c3 = gc - NX - 2;
+                        t = (c3 < nc && dm.tidx[c3] == i) ? 1.0 : 0.0;
+                    }
+                    sh.VE[i][gc] = t;
+                    vfk[i * NCOL + gc] = t;
+                }
+            }
+            // (4c) terminal system rows [Psi | psi_0 psi_1] (lanes of the terminal columns, registers)
+            if (own_pe) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const d2v* cs = reinterpret_cast<const d2v*>(&sh.cols[NX + 2 + c][0]);
+                    const d2v g01 = cs[0], g23 = cs[1];
+                    const double gv[4] = {g01.x, g01.y, g23.x, g23.y};
+                    double t = 0;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) t += q[NX + v] * gv[v];
+                    pe[c] += t;
+                }
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    if (k == N) {
+                        pe[NC + rr] = (a_pe < nc && mode == MODE_NEWTON) ? AT(rct, a_pe) : 0.0;
+                    } else {
+                        const d2v* cs = reinterpret_cast<const d2v*>(&sh.cols[NX + rr][0]);
+                        const d2v g01 = cs[0], g23 = cs[1];
+                        const double gv[4] = {g01.x, g01.y, g23.x, g23.y};
+                        double t = 0;
+#pragma unroll
+                        for (int qq = 0; qq < NX; ++qq) t += w[qq] * abc_nz(AB, qq);
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) t += q[NX + v] * gv[v];
+                        pe[NC + rr] += t;
+                    }
+                }
+            }
+            if (k > 0) put_st((k - 1) & 1, sf[1]);
+#pragma unroll
+            for (int r = 0; r + 1 < RING; ++r) {
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) pf[r][i] = pf[r + 1][i];
+#pragma unroll
+                for (int t = 0; t < NST; ++t) sf[r][t] = sf[r + 1][t];
+            }
+            load_stage(k - RING, pf[RING - 1], sf[RING - 1]);
+            xsync<true>();
+        }
+        if (own_pe)
+#pragma unroll
+            for (int c = 0; c < NC + 2; ++c) sh.PE[a_pe][c] = pe[c];
+        __syncthreads();  // gains (slot) and vf in HBM are read across lanes by the forward sweep
+        // terminal multipliers (every lane, identical): -Psi nu_r = G0' dx0 + psi_r, delta_c on the terminal block
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) nu_[rr][cc] = 0.0;
+        if (nc) {
+            double L[NC][NC];
+            int perm[NC], nneg;
+#pragma unroll
+            for (int i = 0; i < NC; ++i)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) L[i][c] = (i < nc && c < nc) ? -sh.PE[i][c] : 0.0;
+            int f = ldl_factor<NC>(L, nc, perm, &nneg);
+            if (f == 2 || nneg != negsum) {
+                const double dc = 1e-8 * pow(SC(SC_MU), 0.25);
+#pragma unroll
+                for (int i = 0; i < NC; ++i)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) L[i][c] = (i < nc && c < nc) ? -sh.PE[i][c] + (i == c ? dc : 0.0) : 0.0;
+                if (ldl_factor<NC>(L, nc, perm, &nneg)) return 1;
+                if (nneg != negsum) return 1;
+                if (l == 0) SC(SC_DC) = dc;
+            }
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                if (rr >= nr) break;
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) {
+                    double t = 0;
+                    if (cc < nc) {
+                        t = sh.PE[cc][NC + rr];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) t += sh.VE[r][NX + 2 + cc] * dx0[r];
+                    }
+                    nu_[rr][cc] = t;
+                }
+                ldl_solve1<NC>(L, nc, perm, nu_[rr]);
+            }
+        } else if (negsum) {
+            return 1;
+        }
+        return 0;
+    };
+
+    // delta_w enters the stage matrices linearly: H(dw) = H(0) + dw (I_nz + sum_q Jx_q Jx_q'),
+    // g(dw) = g(0) + dw sum_q Jx_q c_q, with Jx_q = (d d_q/d pose, 1 on the slack when it enters d_q) and
+    // c_q = rcq (stage(): D_q = v/t + dw).  A retry adds (dw_new - dw_old) times that to hg in place.
+    auto add_dw = [&](double ddw) {
+        const int M = dm.M, sd = dm.sd;
+        const bool hs = ns != 0;
+        for (int k = l; k <= N; k += G) {
+            double* o = &AT(hg, k * HG);
+            const int is = k < N ? NX + NU : NX, nz = is + (hs ? 1 : 0);
+            for (int i = 0; i < nz; ++i) o[i * (NZ + 2) + i] += ddw;
+            for (int qq = 0; qq < M; ++qq) {
+                double J[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + qq) * 3 + a);
+                const double r = ddw * AT(rcq, k * M + qq);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) o[a * (NZ + 2) + c] += ddw * J[a] * J[c];
+                    o[a * (NZ + 2) + NZ] += J[a] * r;
+                    if (nr > 1) o[a * (NZ + 2) + NZ + 1] += J[a] * r;
+                    if (sd) {
+                        o[is * (NZ + 2) + a] += ddw * J[a];
+                        o[a * (NZ + 2) + is] += ddw * J[a];
+                    }
+                }
+                if (sd) {
+                    o[is * (NZ + 2) + is] += ddw;
+                    o[is * (NZ + 2) + NZ] += r;
+                    if (nr > 1) o[is * (NZ + 2) + NZ + 1] += r;
+                }
+            }
+        }
+        __syncthreads();
+    };
+
+    // inertia correction (IPOPT): delta_w = 0, then 1e-4 (or last / 3), x100 (x8 once one was used)
+    double dw = 0.0, dw_in_hg = 0.0;
+    int fail = 0;
+#ifdef NLOT_PHASE_PROF
+    long long t_build = 0, t_back = 0;
+    int n_att = 0;
+    PROF_T(tr0);
+#endif
+    for (int attempt = 0;; ++attempt) {
+#ifdef NLOT_PHASE_PROF
+        PROF_T(ta);
+        ++n_att;
+#endif
+        if (attempt > 0) {
+            add_dw(dw - dw_in_hg);
+            dw_in_hg = dw;
+        }
+#ifdef NLOT_PHASE_PROF
+        PROF_T(tb);
+        t_build += tb - ta;
+#endif
+        fail = backward();
+#ifdef NLOT_PHASE_PROF
+        t_back += wall_clock64() - tb;
+#endif
+        if (!fail || mode != MODE_NEWTON) break;
+        dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
+        if (dw > 1e40) break;
+    }
+#ifdef NLOT_PHASE_PROF
+    PROF_T(tr1);
+#endif
+    if (fail) {
+        __syncthreads();
+        if (l == 0) {
+            if (mode == MODE_NEWTON) {
+                SC(SC_STATUS) = NLOT_NUMERIC;
+                SC(SC_PHASE) = PH_DONE;
+                SC(SC_RIC) = 0;
+            } else {
+                SC(SC_RIC) = 3;
+            }
+        }
+        return;
+    }
+
+    // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots, in place: row i of
+    // [A B 0 | c] becomes [Phi_i | B_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r)
+    static_assert(NU + 1 == NV, "slack is the last control column");
+    for (int k = l; k < N; k += G) {
+        double* slot = SL + (size_t)k * SLOT;
+        const double* GN = slot + sGN;
+        double dv[2][NU], Kt[NU][NX];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int v = 0; v < NU; ++v) {
+                double t = GN[(NX + rr) * NV + v];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
+                dv[rr][v] = t;
+            }
+#pragma unroll
+        for (int v = 0; v < NU; ++v)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Kt[v][c] = GN[c * NV + v];
+#pragma unroll 1
+        for (int i = 0; i < NX; ++i) {
+            double* r_ = slot + sAB + i * NAB;
+            double Bi[NU];
+#pragma unroll
+            for (int v = 0; v < NU; ++v) Bi[v] = r_[NX + v];
+            double o0 = r_[NZ], o1 = r_[NZ];
+#pragma unroll
+            for (int v = 0; v < NU; ++v) {
+                o0 += Bi[v] * dv[0][v];
+                o1 += Bi[v] * dv[1][v];
+            }
+#pragma unroll
+            for (int c = 0; c < NX; ++c) {
+                double t = r_[c];
+#pragma unroll
+                for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][c];
+                r_[c] = t;
+            }
+            r_[NX + NU] = o0;
+            r_[NZ] = o1;
+        }
+    }
+    __syncthreads();
+    // (F2) the chain dx_{k+1} = Phi_k dx_k + off_k: lane i < NX of the group carries dx[i] of both
+    //      right-hand sides; the other components arrive by group shuffles; rows prefetched a stage ahead
+    double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
+    double* dUo[2] = {&AT(dU, 0), &AT(dU2, 0)};
+    double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
+    {
+        const int li = l < NX ? l : 0;
+        double xv = 0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i)
+            if (i == l) xv = dx0[i];
+        double x[2] = {xv, xv};
+        constexpr int FRING = 4;  // rows of the next FRING knots in flight (HBM latency)
+        double row[NX + 2], rr_[FRING][NX + 2];
+        auto load_row = [&](int k, double* rw) {
+            if (k >= N) return;
+            const double* sl = SL + (size_t)k * SLOT + sAB + li * NAB;
+#pragma unroll
+            for (int c = 0; c < NX; ++c) rw[c] = sl[c];
+            rw[NX] = sl[NX + NU];
+            rw[NX + 1] = sl[NZ];
+        };
+#pragma unroll
+        for (int r = 0; r < FRING; ++r) load_row(r, rr_[r]);
+        for (int k = 0; k < N; ++k) {
+#pragma unroll
+            for (int c = 0; c < NX + 2; ++c) row[c] = rr_[0][c];
+#pragma unroll
+            for (int r = 0; r + 1 < FRING; ++r)
+#pragma unroll
+                for (int c = 0; c < NX + 2; ++c) rr_[r][c] = rr_[r + 1][c];
+            load_row(k + FRING, rr_[FRING - 1]);
+            if (l < NX) {
+                dXo[0][k * NX + l] = x[0];
+                if (nr > 1) dXo[1][k * NX + l] = x[1];
+            }
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                double t = row[NX + rr];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) t += row[c] * __shfl(x[rr], gb + c);
+                x[rr] = t;
+            }
+        }
+        if (l < NX) {
+            dXo[0][N * NX + l] = x[0];
+            if (nr > 1) dXo[1][N * NX + l] = x[1];
+        }
+    }
+    __syncthreads();  // dX visible to every lane
+    // (F3) controls and slacks in parallel over knots: dv_k = k_r + K dx_k + Kn nu_r
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        if (rr >= nr) break;
+        for (int k = l; k <= N; k += G) {
+            const double* GN = SL + (size_t)k * SLOT + sGN;
+            double dv[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                double t = GN[(NX + rr) * NV + v];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) t += GN[c * NV + v] * dXo[rr][k * NX + c];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
+                dv[v] = t;
+            }
+            if (k < N)
+#pragma unroll
+                for (int v = 0; v < NU; ++v) dUo[rr][k * NU + v] = dv[v];
+            if (ns) dSo[rr][k] = k < N ? dv[NU] : dv[0];
+        }
+    }
+    // equality multipliers in parallel over knots: y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k,
+    // y_init = -grad V_0(dx_0)
+    double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
+    double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
+    double* yto[2] = {&AT(yt_n, 0), &AT(yt2, 0)};
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        if (rr >= nr) break;
+        for (int k = l - 1; k < N; k += G) {
+            const double* v1 = &AT(vf, (k + 1) * VF);
+            double xn[NX];
+#pragma unroll
+            for (int c = 0; c < NX; ++c) xn[c] = dXo[rr][(k + 1) * NX + c];
+            double mx0 = 0, mx1 = 0;
+            if (k >= 0) {
+                const double* s0 = SL + (size_t)k * SLOT + sM;
+                const double d0 = dXo[rr][k * NX], d1 = dXo[rr][k * NX + 1];
+                mx0 = s0[0] * d0 + s0[2] * d1;
+                mx1 = s0[1] * d0 + s0[3] * d1;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double t = v1[i * NCOL + NX + rr];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) t += v1[i * NCOL + c] * xn[c];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += v1[i * NCOL + NX + 2 + cc] * nu_[rr][cc];
+                if (k < 0) {
+                    yio[rr][i] = -t;
+                } else {
+                    const double mt = i == 0 ? mx0 : (i == 1 ? mx1 : 0.0);
+                    yko[rr][k * NX + i] = -t - mt;
+                }
+            }
+        }
+        if (l < nc) {
+            double v = 0;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc)
+                if (cc == l) v = nu_[rr][cc];
+            yto[rr][l] = v;
+        }
+    }
+    __syncthreads();
+#ifdef NLOT_PHASE_PROF
+    if (b == 0 && l == 0 && SC(SC_ITERS) < 8)
+        printf("RICG it %d attempts %d build %lld backward %lld forward %lld total %lld (x10ns)\n", (int)SC(SC_ITERS),
+               n_att, t_build, t_back, wall_clock64() - tr1, wall_clock64() - tr0);
+#endif
+    if (l == 0) {
+        if (dw > 0.0 && mode == MODE_NEWTON) SC(SC_DWLAST) = dw;
+        SC(SC_DW) = dw;
+        SC(SC_RIC) = 2;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // kernels (one 64-lane workgroup = one instance; grid = active instances)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
@@ -1183,10 +1826,14 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
     return wsum(f) + p.slack_penalty * wsum(sq) + p.smooth_weight * wsum(uq);
 }
 
-template <int DYN, bool LDS>
-__global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
-                                                const int* __restrict__ active, const double* __restrict__ x0,
-                                                const double* __restrict__ xg) {
+// k_iter_a: evaluation, optimality test, barrier update, then the stage matrices of the Newton system
+// (k_ric solves it).  init_pass = 1 (first step only): slack push and the least-squares multiplier
+// system of the instances in INIT; init_pass = 0: everything else (INIT instances first take their
+// least-squares multipliers from k_ric's solve).
+template <int DYN>
+__global__ __launch_bounds__(64) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+                                               const int* __restrict__ active, const double* __restrict__ x0,
+                                               const double* __restrict__ xg, int init_pass) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -1195,9 +1842,8 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     const int b = active[blockIdx.x], lane = threadIdx.x;
     const int ph = (int)SC(SC_PHASE);
     if (ph != PH_INIT && ph != PH_EVAL) return;
-    __shared__ typename SV::Sh sh;
-    extern __shared__ double lds_slots[];  // (N+1) Riccati stage slots when they fit (LDS), else unused
-    double* SL = LDS ? lds_slots : &AT(stg, 0);
+    if (init_pass && ph != PH_INIT) return;
+    double* SL = &AT(stg, 0);
     const int N = dm.N, M = dm.M, nc = dm.nc;
     const int rank = (int)SC(SC_RANK);
     const double k1 = o.bound_push;
@@ -1232,15 +1878,25 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     };
 
     const double mu0 = SC(SC_MU);
-    if (ph == PH_INIT) {
+    if (ph == PH_INIT && init_pass) {
         eval_knots(false);
         for (int q = lane; q < (N + 1) * M; q += 64) {
             AT(T, q) = fmax(AT(dv, q), k1);  // slack push
             AT(yd, q) = 0.0;
         }
         wsync();
-        // least-squares equality multipliers (IPOPT LeastSquareMultipliers)
-        if (SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_LSQ, 0.0, mu0, 0.0, 1, sh, SL) == 0) {
+        // least-squares equality multipliers (IPOPT LeastSquareMultipliers): the system, solved by k_ric
+        SV::template build_stages<false>(p, dm, ws, b, lane, MODE_LSQ, 0.0, mu0, 0.0, 1, SL);
+        if (lane == 0) {
+            SC(SC_RMU0) = mu0;
+            SC(SC_RMU1) = 0.0;
+            SC(SC_RNR) = 1;
+            SC(SC_RIC) = 1;
+        }
+        return;
+    }
+    if (ph == PH_INIT) {
+        if ((int)SC(SC_RIC) == 2) {
             double ymax = 0;
             for (int k = lane; k <= N; k += 64)
                 for (int j = 0; j < M; ++j) {
@@ -1261,8 +1917,8 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
             zero_mults();
         }
         wsync();
+        if (lane == 0) SC(SC_RIC) = 0;
     }
-    PROF_T(t0);
     eval_knots(true);
     // residuals c(x) (IPOPT sign)
     for (int i = lane; i < NX; i += 64) AT(rci, i) = AT(X, i) - x0b[i];
@@ -1304,7 +1960,6 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
         if (fout) *fout = fo;
     };
-    PROF_T(t1);
     if (ph == PH_INIT) {
         double th0, p0;
         theta_phi(mu0, &th0, &p0);
@@ -1428,8 +2083,6 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     ysum = wsum(ysum);
     nzc = wsum(nzc);
     const double csum_w = wsum(csum), dsq_w = wsum(dsq), psq_w = wsum(psq);
-    const int n_dual_ = (N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M;
-    const int n_pri_ = NX + nc + N * NX + (N + 1) * M;
     const double ny = NX + N * NX + nc + (N + 1) * M;
     const double sd = fmax(100.0, (ysum + zsum) / (ny + nzc)) / 100.0;
     const double scc = fmax(100.0, zsum / nzc) / 100.0;
@@ -1556,13 +2209,69 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         if (reset_filter) SC(SC_NFILT) = 0;
     }
     wsync();
-    // ---- search direction with inertia correction (free mode: the affine-scaling step, mu = 0) ----
-    PROF_T(t2);
-    int n_ric = 1;
-    double dw = 0.0;
-    // One call site for every Newton solve (inertia-correction retries, and in free mode the affine then
-    // the centering solve with the same delta_w): riccati_wave is inlined once.
-    const double last_dw = SC(SC_DWLAST);
+    // ---- Newton system (free mode: affine mu = 0 and centering mu = avg right-hand sides): stage
+    //      matrices here, factorisation + inertia correction in k_ric, the rest in k_iter_b ----
+    SV::template build_stages<false>(p, dm, ws, b, lane, MODE_NEWTON, 0.0, use_qf ? 0.0 : mu, avg, use_qf ? 2 : 1, SL);
+    if (lane == 0) {
+        SC(SC_E0) = E0;
+        SC(SC_RMU0) = use_qf ? 0.0 : mu;
+        SC(SC_RMU1) = avg;
+        SC(SC_RNR) = use_qf ? 2 : 1;
+        SC(SC_USEQF) = use_qf ? 1.0 : 0.0;
+        SC(SC_AVG) = avg;
+        SC(SC_DSQ) = dsq_w;
+        SC(SC_PSQ) = psq_w;
+        SC(SC_NZC) = nzc;
+        SC(SC_RIC) = 1;
+    }
+}
+
+// k_iter_b: after k_ric's solve — the quality-function mu oracle (free mode: sigma search over the
+// affine and centering steps), recovery of the slack/bound-multiplier steps, fraction to the boundary
+// and the line-search reference values.
+template <int DYN>
+__global__ __launch_bounds__(64) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+                                               const int* __restrict__ active) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    using SV = Solver<DYN>;
+    constexpr int NX = SV::NX, NU = SV::NU;
+    const int b = active[blockIdx.x], lane = threadIdx.x;
+    if ((int)SC(SC_RIC) != 2) return;
+    const int N = dm.N, M = dm.M;
+    const double dw = SC(SC_DW), avg = SC(SC_AVG), dsq_w = SC(SC_DSQ), psq_w = SC(SC_PSQ), nzc = SC(SC_NZC);
+    const bool use_qf = SC(SC_USEQF) != 0.0;
+    double mu = SC(SC_MU), tau = SC(SC_TAU);
+    const int n_dual_ = (N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M;
+    const int n_pri_ = NX + dm.nc + N * NX + (N + 1) * M;
+    const int nc = dm.nc;
+    constexpr double kMuMin = 1e-11;
+    (void)o;
+    auto theta_phi = [&](double mu, double* th, double* phv, double* fout = nullptr) {
+        double t = 0, bar = 0, lin = 0;
+        for (int i = lane; i < NX; i += 64) t += fabs(AT(rci, i));
+        for (int i = lane; i < nc; i += 64) t += fabs(AT(rct, i));
+        for (int i = lane; i < N * NX; i += 64) t += fabs(AT(rcd, i));
+        for (int q = lane; q < (N + 1) * M; q += 64) {
+            t += fabs(AT(rcq, q));
+            bar += log(AT(T, q));
+            lin += AT(T, q);
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
+        }
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) {
+                bar += log(AT(S, k));
+                lin += AT(S, k);
+            }
+        *th = wsum(t);
+        const double fo = objective_w(p, dm, ws, b, lane, 0.0);
+        *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
+        if (fout) *fout = fo;
+    };
     // QualityFunctionMuOracle buffers: Riccati outputs + recovered slack/dual steps, affine (qa) and
     // centering minus affine (qc)
     {
@@ -1608,18 +2317,6 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
             }
             wsync();
         };
-        for (;;) {  // free mode: affine (mu = 0) and centering (mu = avg) right-hand sides in one solve
-            const int fail = SV::template riccati_wave<LDS>(p, dm, ws, b, lane, MODE_NEWTON, dw, use_qf ? 0.0 : mu,
-                                                            avg, use_qf ? 2 : 1, sh, SL);
-            if (!fail) {
-                if (dw > 0.0 && lane == 0) SC(SC_DWLAST) = dw;
-                break;
-            }
-            ++n_ric;
-            dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
-            if (dw > 1e40) return finish(NLOT_NUMERIC);
-        }
-        PROF_T(tq0);
         if (use_qf) {
         qf_store(0.0, false);
         qf_store(avg, true);
@@ -1825,13 +2522,8 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
         }
         wsync();
         }
-#ifdef NLOT_PHASE_PROF
-        PROF_T(tq1);
-        if (b == 0 && lane == 0 && iters < 4) printf("QF store+sigma+combine %lld (x10ns)\n", tq1 - tq0);
-#endif
     }
     // ---- recover dt, yd+, dz; fraction to the boundary; line-search reference values ----
-    PROF_T(t3);
     const double kappa_d = 1e-5;
     double amax = 1.0, az = 1.0, gd = 0;
     for (int k = lane; k <= N; k += 64) {
@@ -1896,17 +2588,8 @@ __global__ __launch_bounds__(64) void k_iterate(const NlotProblem* __restrict__ 
     }
     amin *= 0.05;
     wsync();
-#ifdef NLOT_PHASE_PROF
-    {
-        PROF_T(t4);
-        if (b == 0 && lane == 0)
-            printf("PROF it %d eval %lld opt %lld ric %lld n_ric %d rec %lld (x10ns)\n", iters, t1 - t0, t2 - t1,
-                   t3 - t2, n_ric, t4 - t3);
-    }
-#endif
     if (lane == 0) {
-        SC(SC_E0) = E0;
-        SC(SC_DW) = dw;
+        SC(SC_RIC) = 0;
         SC(SC_THETA) = theta;
         SC(SC_PHI) = phi;
         SC(SC_GD) = gd;
@@ -2171,14 +2854,8 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
         mo.sv = mo.sg = mo.sh = 1;
     }
-    // Riccati stage slots in LDS when (N+1) slots fit beside the static LDS (NLOT_SLOTS=global forces HBM)
-    const size_t slot_bytes = (size_t)(dm.N + 1) * slot_len(dm.nx, dm.nu) * sizeof(double);
-    bool slots_lds = slot_bytes + sizeof(typename Solver<DYN>::Sh) <= kLdsBudget;
-    if (const char* e = getenv("NLOT_SLOTS")) slots_lds = slots_lds && strcmp(e, "global") != 0;
-    if (slots_lds)
-        NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)k_iterate<DYN, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)slot_bytes));
-    g_stats.slots_in_lds = slots_lds ? 1 : 0;
+    g_stats.slots_in_lds = 0;  // stage slots live in the HBM workspace; k_ric stages them through LDS
+    const int ric_blocks_per = RicG<DYN>::IPW;
     int spec_threshold = 8192, spec_bulk = 1;  // measured best of {512, 2048, 8192} x {1, 2} (B = 65536)
     if (const char* e = getenv("NLOT_SPEC_THRESHOLD")) spec_threshold = atoi(e);
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
@@ -2200,10 +2877,15 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
         if (ev[4]) hipEventRecord(ev[4], st);
-        if (slots_lds)
-            hipLaunchKernelGGL((k_iterate<DYN, true>), dim3(n_active), dim3(64), slot_bytes, st, dP, dD, o, dW, act, x0, xg);
-        else
-            hipLaunchKernelGGL((k_iterate<DYN, false>), dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg);
+        if (step == 0) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1);
+            hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
+                               dP, dD, dW, act, n_active, (int)MODE_LSQ);
+        }
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0);
+        hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st, dP, dD,
+                           dW, act, n_active, (int)MODE_NEWTON);
+        hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act);
         if (ev[4]) hipEventRecord(ev[5], st);
         if (use_mlp) {
             hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1, nspec);
