@@ -82,12 +82,14 @@ static Dims make_dims(const NlotProblem& p) {
 //   vf (HBM): P (nx x nx) | p (2 x nx) | Gamma (nx x nc) — written by the backward sweep, read by the
 //     parallel multiplier pass.  (nz = nx + nu + 1, nv = nu + 1, nc = nx.)
 //   Layouts (row-major, ncol = nx + 2 + nc gain columns K | k_0 | k_1 | Kn):
-//     slot = [A B 0 | c] (nx x (nz+1)) | M | GN (ncol x nv);  hg = [H | g_0 g_1] (nz x (nz+2));
+//     slot = [A B 0 | c | pad] (nx x ab_row) | M | GN (ncol x nv);  hg = [H | g_0 g_1] (nz x (nz+2)) followed by
+//     the rows g_0', g_1' (so that row j < nz+2 holds what the Riccati lane of column j reads: H symmetric);
 //     vf = [P | p_0 p_1 | Gamma] (nx x ncol).
+__host__ __device__ constexpr int ab_row(int nx, int nu) { return (nx + nu + 2 + 1) & ~1; }  // [A B 0 | c], even
 __host__ __device__ constexpr int slot_len(int nx, int nu) {
-    return nx * (nx + nu + 2) + 4 + (nx + 2 + nx) * (nu + 1);
+    return nx * ab_row(nx, nu) + 4 + (nx + 2 + nx) * (nu + 1);
 }
-__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 3); }
+__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 3) * (nx + nu + 3); }
 __host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * (nx + 2 + nx); }
 // quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
 __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
@@ -122,10 +124,11 @@ struct Ws {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static size_t ws_doubles_per_instance(const Dims& d) {
+// doubles of all instance-major arrays for B instances, each array rounded up to 256 bytes
+static size_t ws_doubles(const Dims& d, int64_t B) {
     const int N = d.N, nx = d.nx, nu = d.nu, M = d.M;
     size_t n = 0;
-#define NLOT_CNT(name, cnt) n += (size_t)(cnt);
+#define NLOT_CNT(name, cnt) n += ((size_t)(cnt) * (size_t)B + 31) & ~(size_t)31;
     NLOT_WS_ARRAYS(NLOT_CNT)
 #undef NLOT_CNT
     return n;
@@ -136,7 +139,7 @@ constexpr size_t kHdr = 8192;  // device copies of NlotProblem, Dims, Ws (kernel
 constexpr size_t kHdrProblem = 0, kHdrDims = 2048, kHdrWs = 4096;
 
 static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
-    size_t b = kHdr + align256(ws_doubles_per_instance(d) * (size_t)B * sizeof(double));
+    size_t b = kHdr + align256(ws_doubles(d, B) * sizeof(double));
     if (mlp) {  // corner list and outputs sized for NSPEC line-search candidates per instance
         const size_t P = (size_t)d.ppk * (d.N + 1);
         b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
@@ -157,10 +160,10 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
 #define NLOT_TAKE(name, cnt)          \
     w.name = q;                       \
     w.L_##name = (int)(cnt);          \
-    q += (size_t)(cnt) * (size_t)B;
+    q += ((size_t)(cnt) * (size_t)B + 31) & ~(size_t)31;
     NLOT_WS_ARRAYS(NLOT_TAKE)
 #undef NLOT_TAKE
-    char* c = (char*)base + align256(ws_doubles_per_instance(d) * (size_t)B * sizeof(double));
+    char* c = (char*)base + align256(ws_doubles(d, B) * sizeof(double));
     if (mlp) {
         const size_t P = (size_t)d.ppk * (N + 1);
         w.pts = (float*)c;
@@ -498,6 +501,8 @@ struct Solver {
                 }
                 o[i * (NZ + 2) + NZ] = gi + mu0 * gm;
                 o[i * (NZ + 2) + NZ + 1] = nr > 1 ? gi + mu1 * gm : 0.0;
+                o[NZ * (NZ + 2) + i] = gi + mu0 * gm;
+                o[(NZ + 1) * (NZ + 2) + i] = nr > 1 ? gi + mu1 * gm : 0.0;
             }
         };
         if (k < N) emit(std::true_type{});
@@ -515,28 +520,16 @@ struct Solver {
         Mk[1][1] = -(r2 - dy * dy) / r3;
     }
 
-    // ---------------- wave-parallel Riccati ----------------
-    // Extended layouts make every phase one or two uniform index formulas:
-    //   slot: ABc = [A B 0 | c] (NX x (NZ+1)) | M (2x2) | GN[c][v] (NCOL x NV: K^T | k_0 | k_1 | Kn^T)
-    //   hg:   [H | g_0 g_1] (NZ x (NZ+2));  vf / VE: [P | p_0 p_1 | G] (NX x NCOL)
+    // ---------------- stage layouts of the Riccati recursion (k_ric) ----------------
+    //   slot: ABc = [A B 0 | c | pad] (NX x NAB) | M (2x2) | GN[c][v] (NCOL x NV: K^T | k_0 | k_1 | Kn^T)
+    //   hg:   [H | g_0 g_1] (NZ x (NZ+2)) | g_0' | g_1';  vf / VE: [P | p_0 p_1 | G] (NX x NCOL)
     //   QE:   [Q | q_0 q_1 | QN] (NZ x NQE);  W: [P AB | P c + p_0 | P c + p_1 | G] (NX x NQE)
-    //   PE:   [Psi | psi_0 psi_1] (NC x (NC+2));  R: minus the gain right-hand sides (NCOL x NV)
-    static constexpr int NCOL = NX + 2 + NC, NQE = NZ + 2 + NC, NAB = NZ + 1;
+    //   PE:   [Psi | psi_0 psi_1] (NC x (NC+2))
+    static constexpr int NCOL = NX + 2 + NC, NQE = NZ + 2 + NC, NAB = ab_row(NX, NU);
     static constexpr int SLOT = slot_len(NX, NU), HG = hg_len(NX, NU), VF = vf_len(NX, NU);
     static constexpr int sAB = 0, sM = NX * NAB, sGN = sM + 4;
     static_assert(sGN + NCOL * NV == SLOT, "slot layout");
-    static_assert(NZ * (NZ + 2) == HG && NX * NCOL == VF, "hg / vf layout");
-    static constexpr int NPH2 = NZ * NQE;             // phase-2 entries
-    static constexpr int NPRE = (NPH2 + 63) / 64;    // prefetched H/g entries per lane
-
-    struct Sh {
-        double VE[2][NX][NCOL];  // value function (double-buffered)
-        double PE[NC][NC + 2];   // terminal system
-        double W[NX][NQE];
-        double QE[NZ][NQE];
-        double R[NCOL][NV];      // -(right-hand sides) of the gain columns
-        double cols[NCOL][NV];   // gains, zero beyond nv / nc
-    };
+    static_assert((NZ + 2) * (NZ + 2) == HG && NX * NCOL == VF, "hg / vf layout");
 
     // gain column c <-> QE column
     __host__ __device__ static constexpr int qe_col(int c) { return c < NX ? c : NZ + (c - NX); }
@@ -572,6 +565,8 @@ struct Solver {
 #pragma unroll
                 for (int j = 0; j < NZ; ++j) o[sAB + i * NAB + j] = j < NX ? A[i][j] : (j < NX + NU ? Bu[i][j - NX] : 0.0);
                 o[sAB + i * NAB + NZ] = (k < N && mode == MODE_NEWTON) ? -AT(rcd, k * NX + i) : 0.0;
+#pragma unroll
+                for (int j = NZ + 1; j < NAB; ++j) o[sAB + i * NAB + j] = 0.0;
             }
             o[sM + 0] = Mk[0][0];
             o[sM + 1] = Mk[0][1];
@@ -581,461 +576,6 @@ struct Solver {
         __syncthreads();  // hg is in HBM: full fence
     }
 
-    // phase-2 entry e = (i, col): its H / g starting value (QN columns start at 0)
-    __device__ __forceinline__ static double hg_of(const double* hgk, int e, int nr) {
-        const int i = e / NQE, col = e % NQE;
-        return col < NZ + nr ? hgk[i * (NZ + 2) + col] : 0.0;
-    }
-
-    // Pivoted LDL^T of the symmetric 3x3 Q_vv held in QE (rows/cols NX..NX+2), identical in arithmetic
-    // and pivot order to the generic ldl_factor / the oracle's ldl(); the permutation is applied through
-    // the (uniform, broadcast) LDS addresses instead of register swaps.  Returns 0 or 2 (singular).
-    template <class ShT>
-    __device__ __forceinline__ static int ldl3(const ShT& sh, int o[3], double& d0, double& d1, double& d2,
-                                               double& l10, double& l20, double& l21, int& nneg) {
-        auto q = [&](int i, int j) { return sh.QE[NX + i][NX + j]; };
-        double scale = 1e-300;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) scale = fmax(scale, fabs(q(i, j)));
-        const double a00 = q(0, 0), a11 = q(1, 1), a22 = q(2, 2);
-        int pv = 0;
-        if (fabs(a11) > fabs(a00)) pv = 1;
-        if (fabs(a22) > fabs(pv == 1 ? a11 : a00)) pv = 2;
-        o[0] = pv;
-        o[1] = pv == 1 ? 0 : 1;
-        o[2] = pv == 2 ? 0 : 2;
-        nneg = 0;
-        d0 = q(o[0], o[0]);
-        if (!(fabs(d0) > 1e-13 * scale) || !isfinite(d0)) return 2;
-        if (d0 < 0) ++nneg;
-        const double c1 = q(o[1], o[0]), c2 = q(o[2], o[0]);
-        double b11 = q(o[1], o[1]) - c1 * c1 / d0;
-        double b21 = q(o[2], o[1]) - c2 * c1 / d0;
-        double b22 = q(o[2], o[2]) - c2 * c2 / d0;
-        l10 = c1 / d0;
-        l20 = c2 / d0;
-        if (fabs(b22) > fabs(b11)) {  // swap positions 1 and 2 (rows of L included)
-            const int t = o[1];
-            o[1] = o[2];
-            o[2] = t;
-            const double tb = b11;
-            b11 = b22;
-            b22 = tb;
-            const double tl = l10;
-            l10 = l20;
-            l20 = tl;
-        }
-        d1 = b11;
-        if (!(fabs(d1) > 1e-13 * scale) || !isfinite(d1)) return 2;
-        if (d1 < 0) ++nneg;
-        d2 = b22 - b21 * b21 / d1;
-        l21 = b21 / d1;
-        if (!(fabs(d2) > 1e-13 * scale) || !isfinite(d2)) return 2;
-        if (d2 < 0) ++nneg;
-        return 0;
-    }
-
-    // Returns 0, or 1 when the inertia test fails (uniform over the wave).  RHS 0 -> dX dU dS yi_n yk_n
-    // yt_n; RHS 1 (nr = 2, barrier parameter mu1) -> dX2 dU2 dS2 yi2 yk2 yt2.  delta_c uses SC(SC_MU).
-    // Per stage: 4 LDS barriers; Q_vv is factored redundantly in every lane's registers; the forward
-    // sweep carries dx in registers (no barriers); the multipliers are a parallel pass over knots.
-    template <bool LDS>
-    __device__ static int riccati_wave(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
-                                       double dw, double mu0, double mu1, int nr, Sh& sh, double* SL) {
-        const int N = dm.N, nc = dm.nc, ns = dm.ns;
-#ifdef NLOT_PHASE_PROF
-        long long pa = 0, pb = 0, pc = 0, pd = 0;
-#endif
-        PROF_T(r0);
-        build_stages<LDS>(p, dm, ws, b, lane, mode, dw, mu0, mu1, nr, SL);
-        PROF_T(r1);
-        int cur = 0, negsum = 0;
-        for (int e = lane; e < NX * NCOL + NC * (NC + 2); e += 64) {
-            if (e < NX * NCOL) sh.VE[0][e / NCOL][e % NCOL] = 0;
-            else { const int f = e - NX * NCOL; sh.PE[f / (NC + 2)][f % (NC + 2)] = 0; }
-        }
-        if (mode == MODE_NEWTON && lane == 0) SC(SC_DC) = 0.0;
-        double pre[NPRE];  // H/g of the next stage, prefetched into registers one stage ahead
-#pragma unroll
-        for (int j = 0; j < NPRE; ++j) {
-            const int e = lane + 64 * j;
-            pre[j] = e < NPH2 ? hg_of(&AT(hg, N * HG), e, nr) : 0.0;
-        }
-        xsync<true>();
-        for (int k = N; k >= 0; --k) {
-            const int nv = (k < N ? NU : 0) + ns, nxt = cur ^ 1;
-            double* slot = SL + (size_t)k * SLOT;
-            const double* ABc = slot + sAB;
-            const double* Mk = slot + sM;
-            double* vfk = &AT(vf, k * VF);
-            double hcur[NPRE];
-#pragma unroll
-            for (int j = 0; j < NPRE; ++j) hcur[j] = pre[j];
-            if (k > 0) {
-                const double* hgn = &AT(hg, (k - 1) * HG);
-#pragma unroll
-                for (int j = 0; j < NPRE; ++j) {
-                    const int e = lane + 64 * j;
-                    pre[j] = e < NPH2 ? hg_of(hgn, e, nr) : 0.0;
-                }
-            }
-            PROF_T(q0);
-            // (1) W = [P AB | P c + p_0 | P c + p_1 | G]
-            for (int e = lane; e < NX * NQE; e += 64) {
-                const int r = e / NQE, col = e % NQE;
-                double t;
-                if (col < NZ + 2) {
-                    const int cc = col < NZ ? col : NZ;
-                    t = col < NZ ? 0.0 : sh.VE[cur][r][NX + col - NZ];
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t += sh.VE[cur][r][q] * ABc[q * NAB + cc];
-                } else {
-                    t = sh.VE[cur][r][NX + 2 + col - NZ - 2];
-                }
-                sh.W[r][col] = t;
-            }
-            xsync<true>();
-            PROF_ACC(pa, q0);
-            PROF_T(q1);
-            // (2) QE = [H | g] + cross + AB' W  (cross: the path-length coupling dx_k' M dx_{k+1} with
-            //     dx_{k+1} = A dx + B dv + c substituted); rows of the controls also fill R
-#pragma unroll
-            for (int j = 0; j < NPRE; ++j) {
-                const int e = lane + 64 * j;
-                if (e >= NPH2) continue;
-                const int i = e / NQE, col = e % NQE;
-                double t = hcur[j];
-                if (col < NZ + 2) {
-                    const int cc = col < NZ ? col : NZ;
-                    if (i < 2) t += Mk[i * 2] * ABc[cc] + Mk[i * 2 + 1] * ABc[NAB + cc];
-                    if (col < 2) t += Mk[col * 2] * ABc[i] + Mk[col * 2 + 1] * ABc[NAB + i];
-                }
-#pragma unroll
-                for (int r = 0; r < NX; ++r) t += ABc[r * NAB + i] * sh.W[r][col];
-                sh.QE[i][col] = t;
-                if (i >= NX && (col < NX || col >= NZ)) sh.R[col < NX ? col : NX + col - NZ][i - NX] = -t;
-            }
-            xsync<true>();
-            PROF_ACC(pb, q1);
-            PROF_T(q2);
-            // (3) every lane factors Q_vv in registers (identical, uniform inertia decision); lane c solves
-            //     gain column c into LDS (value update) and the slot (forward sweep)
-            if (nv == 3 && NV == 3) {
-                int o[3], nneg;
-                double d0, d1, d2, l10, l20, l21;
-                if (ldl3(sh, o, d0, d1, d2, l10, l20, l21, nneg)) return 1;
-                negsum += nneg;
-                if (negsum > nc) return 1;
-                if (lane < NCOL) {
-                    const double x0 = -sh.R[lane][0], x1 = -sh.R[lane][1], x2 = -sh.R[lane][2];
-                    auto pick = [&](int i) { return i == 0 ? x0 : (i == 1 ? x1 : x2); };
-                    double t0 = pick(o[0]), t1 = pick(o[1]), t2 = pick(o[2]);
-                    t1 -= l10 * t0;
-                    t2 -= l20 * t0;
-                    t2 -= l21 * t1;
-                    t0 /= d0;
-                    t1 /= d1;
-                    t2 /= d2;
-                    t1 -= l21 * t2;
-                    t0 -= l10 * t1;
-                    t0 -= l20 * t2;
-                    double y[3];
-#pragma unroll
-                    for (int v = 0; v < 3; ++v) y[v] = o[0] == v ? t0 : (o[1] == v ? t1 : t2);
-#pragma unroll
-                    for (int v = 0; v < 3; ++v) {
-                        sh.cols[lane][v] = -y[v];
-                        slot[sGN + lane * NV + v] = -y[v];
-                    }
-                }
-            } else if (nv > 0) {
-                double L[NV][NV];
-                int perm[NV], nneg;
-#pragma unroll
-                for (int i = 0; i < NV; ++i)
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) L[i][j] = (i < nv && j < nv) ? sh.QE[NX + i][NX + j] : 0.0;
-                if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
-                negsum += nneg;
-                if (negsum > nc) return 1;
-                if (lane < NCOL) {
-                    double col[NV];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? sh.R[lane][v] : 0.0;
-                    ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        const double r = v < nv ? col[v] : 0.0;
-                        sh.cols[lane][v] = r;
-                        slot[sGN + lane * NV + v] = r;
-                    }
-                }
-            } else if (lane < NCOL) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    sh.cols[lane][v] = 0.0;
-                    slot[sGN + lane * NV + v] = 0.0;
-                }
-            }
-            xsync<true>();
-            PROF_ACC(pc, q2);
-            PROF_T(q3);
-            // (4) value function VE = [P | p_0 p_1 | G] (P symmetrised; the last knot carries the terminal
-            //     equality C x_N = xg_sel) and the terminal system PE = [Psi | psi_0 psi_1]
-            for (int e = lane; e < NX * NCOL + NC * (NC + 2); e += 64) {
-                if (e < NX * NCOL) {
-                    const int i = e / NCOL, c = e % NCOL;
-                    double t = sh.QE[i][qe_col(c)];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += sh.QE[i][NX + v] * sh.cols[c][v];
-                    if (c < NX && c != i) {
-                        double t2 = sh.QE[c][i];
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) t2 += sh.QE[c][NX + v] * sh.cols[i][v];
-                        t = 0.5 * (t + t2);
-                    }
-                    if (k == N && c >= NX + 2) {
-                        const int cc = c - NX - 2;
-                        t = (cc < nc && dm.tidx[cc] == i) ? 1.0 : 0.0;
-                    }
-                    sh.VE[nxt][i][c] = t;
-                    vfk[e] = t;
-                } else {
-                    const int f = e - NX * NCOL, a = f / (NC + 2), c = f % (NC + 2);
-                    if (c < NC) {  // Psi
-                        double t = 0;
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.QE[NX + v][NZ + 2 + a] * sh.cols[NX + 2 + c][v];
-                        sh.PE[a][c] += t;
-                    } else if (k == N) {
-                        sh.PE[a][c] = (a < nc && mode == MODE_NEWTON) ? AT(rct, a) : 0.0;
-                    } else {  // psi_r
-                        double t = 0;
-#pragma unroll
-                        for (int q = 0; q < NX; ++q) t += sh.VE[cur][q][NX + 2 + a] * ABc[q * NAB + NZ];
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) t += sh.QE[NX + v][NZ + 2 + a] * sh.cols[NX + c - NC][v];
-                        sh.PE[a][c] += t;
-                    }
-                }
-            }
-            cur = nxt;
-            xsync<true>();
-            PROF_ACC(pd, q3);
-        }
-        __syncthreads();  // slot (HBM in the fallback) and vf are read across lanes below
-        PROF_T(r2);
-        // terminal multipliers (every lane, identical): -Psi nu_r = G0' dx0 + psi_r, delta_c on the terminal block
-        double dx0[NX], nu_[2][NC];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-            for (int cc = 0; cc < NC; ++cc) nu_[rr][cc] = 0.0;
-        if (nc) {
-            double L[NC][NC];
-            int perm[NC], nneg;
-#pragma unroll
-            for (int i = 0; i < NC; ++i)
-#pragma unroll
-                for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.PE[i][j] : 0.0;
-            int f = ldl_factor<NC>(L, nc, perm, &nneg);
-            if (f == 2 || nneg != negsum) {
-                const double dc = 1e-8 * pow(SC(SC_MU), 0.25);
-#pragma unroll
-                for (int i = 0; i < NC; ++i)
-#pragma unroll
-                    for (int j = 0; j < NC; ++j) L[i][j] = (i < nc && j < nc) ? -sh.PE[i][j] + (i == j ? dc : 0.0) : 0.0;
-                if (ldl_factor<NC>(L, nc, perm, &nneg)) return 1;
-                if (nneg != negsum) return 1;
-                if (lane == 0) SC(SC_DC) = dc;
-            }
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                if (rr >= nr) break;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc) {
-                    double t = 0;
-                    if (cc < nc) {
-                        t = sh.PE[cc][NC + rr];
-#pragma unroll
-                        for (int r = 0; r < NX; ++r) t += sh.VE[cur][r][NX + 2 + cc] * dx0[r];
-                    }
-                    nu_[rr][cc] = t;
-                }
-                ldl_solve1<NC>(L, nc, perm, nu_[rr]);
-            }
-        } else if (negsum) {
-            return 1;
-        }
-        PROF_T(r3);
-        // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots, in place: row i of
-        // [A B 0 | c] becomes [Phi_i | B_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r)
-        // (the slack column of B is identically zero, so it can hold off_0)
-        static_assert(NU + 1 == NV, "slack is the last control column");
-        for (int k = lane; k < N; k += 64) {
-            double* slot = SL + (size_t)k * SLOT;
-            const double* GN = slot + sGN;
-            double dv[2][NU], Kt[NU][NX];
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-                for (int v = 0; v < NU; ++v) {
-                    double t = GN[(NX + rr) * NV + v];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
-                    dv[rr][v] = t;
-                }
-#pragma unroll
-            for (int v = 0; v < NU; ++v)
-#pragma unroll
-                for (int j = 0; j < NX; ++j) Kt[v][j] = GN[j * NV + v];
-#pragma unroll 1
-            for (int i = 0; i < NX; ++i) {
-                double* r_ = slot + sAB + i * NAB;
-                double Bi[NU];
-#pragma unroll
-                for (int v = 0; v < NU; ++v) Bi[v] = r_[NX + v];
-                double o0 = r_[NZ], o1 = r_[NZ];
-#pragma unroll
-                for (int v = 0; v < NU; ++v) {
-                    o0 += Bi[v] * dv[0][v];
-                    o1 += Bi[v] * dv[1][v];
-                }
-#pragma unroll
-                for (int j = 0; j < NX; ++j) {
-                    double t = r_[j];
-#pragma unroll
-                    for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][j];
-                    r_[j] = t;
-                }
-                r_[NX + NU] = o0;
-                r_[NZ] = o1;
-            }
-        }
-        if (LDS) xsync<true>(); else __syncthreads();
-        // (F2) the chain dx_{k+1} = Phi_k dx_k + off_k: lane i < NX carries dx[i] of both RHS; the other
-        //      components arrive by readlane (no LDS, no barrier); Phi rows are prefetched a stage ahead
-        double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
-        double* dUo[2] = {&AT(dU, 0), &AT(dU2, 0)};
-        double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
-        {
-            const int li = lane < NX ? lane : 0;
-            double x0 = 0;
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-                if (i == lane) x0 = dx0[i];
-            double x[2] = {x0, x0};
-            double row[NX + 2], nrow[NX + 2];
-            auto load_row = [&](int k, double* rw) {
-                const double* sl = SL + (size_t)k * SLOT + sAB + li * NAB;
-#pragma unroll
-                for (int j = 0; j < NX; ++j) rw[j] = sl[j];
-                rw[NX] = sl[NX + NU];
-                rw[NX + 1] = sl[NZ];
-            };
-            if (N > 0) load_row(0, nrow);
-            for (int k = 0; k < N; ++k) {
-#pragma unroll
-                for (int j = 0; j < NX + 2; ++j) row[j] = nrow[j];
-                if (k + 1 < N) load_row(k + 1, nrow);
-                if (lane < NX) {
-                    dXo[0][k * NX + lane] = x[0];
-                    if (nr > 1) dXo[1][k * NX + lane] = x[1];
-                }
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr) {
-                    double t = row[NX + rr];
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) t += row[j] * bcast_lane(x[rr], j);
-                    x[rr] = t;
-                }
-            }
-            if (lane < NX) {
-                dXo[0][N * NX + lane] = x[0];
-                if (nr > 1) dXo[1][N * NX + lane] = x[1];
-            }
-        }
-        wsync();  // dX visible to every lane
-        // (F3) controls and slacks in parallel over knots: dv_k = k_r + K dx_k + Kn nu_r
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            if (rr >= nr) break;
-            for (int k = lane; k <= N; k += 64) {
-                const int nv = (k < N ? NU : 0) + ns;
-                const double* GN = SL + (size_t)k * SLOT + sGN;
-                double dv[NV];
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double t = GN[(NX + rr) * NV + v];
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) t += GN[j * NV + v] * dXo[rr][k * NX + j];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
-                    dv[v] = t;
-                }
-                if (k < N)
-#pragma unroll
-                    for (int v = 0; v < NU; ++v) dUo[rr][k * NU + v] = dv[v];
-                if (ns) dSo[rr][k] = k < N ? dv[NU] : dv[0];
-                (void)nv;
-            }
-        }
-        // equality multipliers in parallel over knots: y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k,
-        // y_init = -grad V_0(dx_0)
-        double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
-        double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
-        double* yto[2] = {&AT(yt_n, 0), &AT(yt2, 0)};
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            if (rr >= nr) break;
-            for (int k = lane - 1; k < N; k += 64) {
-                const double* v1 = &AT(vf, (k + 1) * VF);
-                double xn[NX];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) xn[j] = dXo[rr][(k + 1) * NX + j];
-                double mx0 = 0, mx1 = 0;
-                if (k >= 0) {
-                    const double* s0 = SL + (size_t)k * SLOT + sM;
-                    const double d0 = dXo[rr][k * NX], d1 = dXo[rr][k * NX + 1];
-                    mx0 = s0[0] * d0 + s0[2] * d1;
-                    mx1 = s0[1] * d0 + s0[3] * d1;
-                }
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double t = v1[i * NCOL + NX + rr];
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) t += v1[i * NCOL + j] * xn[j];
-#pragma unroll
-                    for (int cc = 0; cc < NC; ++cc) t += v1[i * NCOL + NX + 2 + cc] * nu_[rr][cc];
-                    if (k < 0) {
-                        yio[rr][i] = -t;
-                    } else {
-                        const double mt = i == 0 ? mx0 : (i == 1 ? mx1 : 0.0);
-                        yko[rr][k * NX + i] = -t - mt;
-                    }
-                }
-            }
-            if (lane < nc) {
-                double v = 0;
-#pragma unroll
-                for (int cc = 0; cc < NC; ++cc)
-                    if (cc == lane) v = nu_[rr][cc];
-                yto[rr][lane] = v;
-            }
-        }
-        wsync();
-#ifdef NLOT_PHASE_PROF
-        PROF_T(r4);
-        if (b == 0 && lane == 0 && mode == MODE_NEWTON && SC(SC_ITERS) < 4)
-            printf("RIC nr %d build %lld back %lld [W %lld Q %lld gains %lld value %lld] nu %lld fwd+y %lld\n", nr,
-                   r1 - r0, r2 - r1, pa, pb, pc, pd, r3 - r2, r4 - r3);
-#endif
-        return 0;
-    }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1054,13 +594,18 @@ struct RicG {
     static constexpr int NCOL = SV::NCOL, NQE = SV::NQE, NAB = SV::NAB;
     static constexpr int G = NQE <= 16 ? 16 : 32;  // lanes per instance (>= one per QE column)
     static constexpr int IPW = 64 / G;             // instances per wavefront
-    static constexpr int NABM = NX * NAB + 4;      // [A B 0 | c] | M, contiguous at the start of a slot
-    static constexpr int NST = (NABM + G - 1) / G; // staged doubles per lane
+    static constexpr int NABM = NX * NAB + 4;      // [A B 0 | c | pad] | M, contiguous at the start of a slot
     static constexpr int ev(int n) { return n + (n & 1); }  // rows padded to 16 bytes
-    static constexpr int NABP = ev(NAB), NXP = ev(NX), NZP = ev(NZ), NCOLP = ev(NCOL);
-    static_assert(SV::sAB == 0 && SV::sM == NX * NAB && NCOL <= NQE && NQE <= G && NV <= 4, "RicG layout");
+    static constexpr int NXP = ev(NX), NZP = ev(NZ), NCOLP = ev(NCOL);
+    // Stage inputs arrive by global -> LDS DMA (global_load_lds_dwordx4: lane l of the wave lands 16 bytes
+    // at base + 16 l, i.e. G * 16 bytes per group per instruction), RING stages ahead; no VGPRs held.
+    static constexpr int DW = 2 * G;                       // doubles per group per DMA instruction
+    static constexpr int NDH = (SV::HG + DW - 1) / DW;     // DMA instructions for hg
+    static constexpr int NDA = (NABM + DW - 1) / DW;       // ... for [A B 0 | c] | M
+    static constexpr int NDMA = NDH + NDA, RING = 4;
+    static_assert(SV::sAB == 0 && SV::sM == NX * NAB && NCOL <= NQE && NQE <= G && NV <= 4 && NAB % 2 == 0,
+                  "RicG layout");
     struct alignas(16) Sh {  // per instance; every row starts on a 16-byte boundary
-        double ab[2][NX * NABP + 4];  // [A B 0 | c] rows (padded) | M
         double VE[NX][NCOLP];         // value function [P | p_0 p_1 | Gamma] of the stage after
         double QT[NV][NZP];           // columns NX .. NX+NV-1 of QE, transposed
         double VU[NCOL][NXP];         // value update before symmetrisation, column-major
@@ -1080,12 +625,14 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
     using R = RicG<DYN>;
     using SV = Solver<DYN>;
     constexpr int NX = R::NX, NU = R::NU, NV = R::NV, NZ = R::NZ, NC = R::NC, NCOL = R::NCOL, NQE = R::NQE;
-    constexpr int NAB = R::NAB, G = R::G, NABM = R::NABM, NST = R::NST, NABP = R::NABP, NCOLP = R::NCOLP;
+    constexpr int NAB = R::NAB, G = R::G, NABM = R::NABM, NCOLP = R::NCOLP, DW = R::DW, NDH = R::NDH, NDA = R::NDA;
+    constexpr int NDMA = R::NDMA, RING = R::RING;
     constexpr int SLOT = SV::SLOT, HG = SV::HG, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
     __shared__ typename R::Sh shg[R::IPW];
+    __shared__ __attribute__((aligned(16))) double ring[RING][NDMA][R::IPW][DW];  // DMA'd stage inputs
     const int grp = threadIdx.x / G, l = threadIdx.x % G, gb = grp * G;
     const int si = blockIdx.x * R::IPW + grp;
     if (si >= n_active) return;
@@ -1101,7 +648,6 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
     const int a_pe = j - (NZ + 2);                                              // [Psi | psi] row
     const bool own_pe = a_pe >= 0 && a_pe < NC;
     double nu_[2][NC], dx0[NX];
-    auto abc_nz = [&](const double* AB, int qq) { return AB[qq * R::NABP + NZ]; };
 
     // backward sweep + terminal multipliers; 0, or 1 on a wrong inertia (uniform within the group)
     auto backward = [&]() -> int {
@@ -1110,42 +656,70 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
 #pragma unroll
         for (int c = 0; c < NC + 2; ++c) pe[c] = 0.0;
         if (mode == MODE_NEWTON && l == 0) SC(SC_DC) = 0.0;
-        // Stage inputs from HBM (written by k_iter_a, read once): a register ring RING stages deep hides
-        // the load latency behind the recursion (slot 0 = stage k, slot s = stage k - s).
-        constexpr int RING = 2;
-        double pf[RING][NZ], sf[RING][NST], w[NX], q[NZ], gcol[NV], vr[NX];
-        auto load_stage = [&](int k, double* h, double* s) {
+        // Stage inputs from HBM (written by k_iter_a, read once) stream into the LDS ring by DMA, RING
+        // stages ahead.  Group grp's double e of a stage's hg lands at ring[slot][e / DW][grp][e % DW], the
+        // [A B 0 | c] | M block at ring[slot][NDH + e / DW][grp][e % DW].
+        double w[NX], q[NZ], gcol[NV], vr[NX];
+        auto issue = [&](int k) {  // DMA of stage k (every lane of the group; one 16-byte piece each)
             if (k < 0) return;
-            const double* hgk = &AT(hg, k * HG);  // hg column j ([H | g_0 g_1], zero beyond nr)
+            const int slot = k % RING;
+            const double* hgk = &AT(hg, k * HG);
+            const double* abk = SL + (size_t)k * SLOT;
 #pragma unroll
-            for (int i = 0; i < NZ; ++i) h[i] = j < NZ + nr ? hgk[i * (NZ + 2) + j] : 0.0;
-            const double* s0 = SL + (size_t)k * SLOT;
+            for (int t = 0; t < NDH; ++t) {
+                const int e = t * DW + 2 * l;
+                __builtin_amdgcn_global_load_lds((const void*)(hgk + (e < HG ? e : 0)),
+                                                 (__attribute__((address_space(3))) void*)&ring[slot][t][0][0], 16, 0, 0);
+            }
 #pragma unroll
-            for (int t = 0; t < NST; ++t) {
-                const int e = l + G * t;
-                s[t] = e < NABM ? s0[e] : 0.0;
+            for (int t = 0; t < NDA; ++t) {
+                const int e = t * DW + 2 * l;
+                __builtin_amdgcn_global_load_lds((const void*)(abk + (e < NABM ? e : 0)),
+                                                 (__attribute__((address_space(3))) void*)&ring[slot][NDH + t][0][0], 16, 0,
+                                                 0);
             }
         };
-        auto put_st = [&](int buf, const double* s) {  // slot order -> padded LDS rows
-#pragma unroll
-            for (int t = 0; t < NST; ++t) {
-                const int e = l + G * t;
-                if (e < NABM) sh.ab[buf][e < NX * NAB ? (e / NAB) * NABP + e % NAB : NX * NABP + (e - NX * NAB)] = s[t];
+        // wait until at most `n` DMA instructions (plus whatever vector-memory stores came after them) are
+        // outstanding: vmcnt counts stores too, so this is conservative (the ring stays ~2 stages ahead)
+        auto wait_dma = [&](int n) {
+            // s_waitcnt encoding (gfx9): vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] << 14
+            constexpr int base = (7 << 4) | (15 << 8);
+            switch (n) {
+                case 0: __builtin_amdgcn_s_waitcnt(base | 0); break;
+                default: __builtin_amdgcn_s_waitcnt(base | (((RING - 1) * NDMA) & 15) | ((((RING - 1) * NDMA) >> 4) << 14)); break;
             }
+            asm volatile("" ::: "memory");
         };
 #pragma unroll
-        for (int r = 0; r < RING; ++r) load_stage(N - r, pf[r], sf[r]);
-        put_st(N & 1, sf[0]);
+        for (int r = 0; r < RING; ++r) issue(N - r);
         int negsum = 0;
         const bool wcol = j < NZ + 2;              // W column j is P AB (+ p_r), not a Gamma pass-through
         const int cc = j < NZ ? j : NZ;            // AB column (the c column for the p_r columns)
         const int jc = j >= NZ && j < NQE ? NX + j - NZ : 0;  // VE column carried into W
         const bool vlane = j >= NX && j < NX + NV;  // control columns: Q_vv, Q_xv
         xsync<true>();
+#ifdef NLOT_PHASE_PROF
+        long long ph[5] = {0, 0, 0, 0, 0};
+#endif
         for (int k = N; k >= 0; --k) {
+#ifdef NLOT_PHASE_PROF
+            long long tq = wall_clock64();
+#endif
             const int nv = (k < N ? NU : 0) + ns;
-            const double* AB = sh.ab[k & 1];
-            const double* Mk = AB + NX * NABP;
+            wait_dma(k >= RING - 1 ? 1 : 0);  // stage k's DMA landed (the later RING-1 stages may be in flight)
+            const double* hrow = &ring[k % RING][0][grp][0];  // hg of stage k, element e at (e / DW) * IPW * DW + e % DW
+            auto HGe = [&](int e) { return hrow[(e / DW) * (R::IPW * DW) + e % DW]; };
+            const double* abase = &ring[k % RING][NDH][grp][0];
+            auto ABe = [&](int e) { return abase[(e / DW) * (R::IPW * DW) + e % DW]; };
+            double hcur[NZ];  // row j of hg: column j of [H | g_0 g_1] (H symmetric), zero beyond nr
+            {
+                const int jr = j < NZ + 2 ? j : 0;
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) {
+                    const double v = HGe(jr * (NZ + 2) + i);
+                    hcur[i] = j < NZ + nr ? v : 0.0;
+                }
+            }
             // ---- batch 1: P (rows of VE), this lane's VE column and AB column, M ----
             double P[NX][NX], vc[NX], abc[NX];
 #pragma unroll
@@ -1159,9 +733,9 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 }
                 if (NX & 1) P[r][NX - 1] = sh.VE[r][NX - 1];
                 vc[r] = sh.VE[r][jc];
-                abc[r] = AB[r * NABP + cc];
+                abc[r] = ABe(r * NAB + cc);
             }
-            const d2v m01 = reinterpret_cast<const d2v*>(Mk)[0], m23 = reinterpret_cast<const d2v*>(Mk)[1];
+            const d2v m01 = d2v{ABe(NX * NAB), ABe(NX * NAB + 1)}, m23 = d2v{ABe(NX * NAB + 2), ABe(NX * NAB + 3)};
             // (1) W[:, j] = [P AB | P c + p_0 | P c + p_1 | G][:, j]
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1176,8 +750,8 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
             for (int i = 0; i < NZ; ++i) {
                 double ab_i[NX];
 #pragma unroll
-                for (int r = 0; r < NX; ++r) ab_i[r] = AB[r * NABP + i];
-                double t = pf[0][i];
+                for (int r = 0; r < NX; ++r) ab_i[r] = ABe(r * NAB + i);
+                double t = hcur[i];
                 if (i < 2) {
                     const double x = (i == 0 ? m01.x : m23.x) * abc[0] + (i == 0 ? m01.y : m23.y) * abc[1];
                     t = wcol ? t + x : t;
@@ -1196,6 +770,9 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 for (int i2 = 0; i2 < NZ / 2; ++i2) dst[i2] = d2v{q[2 * i2], q[2 * i2 + 1]};
                 if (NZ & 1) sh.QT[j - NX][NZ - 1] = q[NZ - 1];
             }
+#ifdef NLOT_PHASE_PROF
+            { const long long t = wall_clock64(); ph[0] += t - tq; tq = t; }
+#endif
             xsync<true>();
             // ---- batch 2: the control columns of QE (Q_vv, Q_xv) ----
             double Qv[NV][NZ];
@@ -1210,6 +787,9 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 }
                 if (NZ & 1) Qv[v][NZ - 1] = sh.QT[v][NZ - 1];
             }
+#ifdef NLOT_PHASE_PROF
+            { const long long t = wall_clock64(); ph[1] += t - tq; tq = t; }
+#endif
             // (3) Q_vv factorised by every lane (identical, uniform inertia decision); lane j solves its
             //     gain column in registers
 #pragma unroll
@@ -1314,6 +894,9 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 for (int i2 = 0; i2 < NX / 2; ++i2) vd[i2] = d2v{vr[2 * i2], vr[2 * i2 + 1]};
                 if (NX & 1) sh.VU[gc][NX - 1] = vr[NX - 1];
             }
+#ifdef NLOT_PHASE_PROF
+            { const long long t = wall_clock64(); ph[2] += t - tq; tq = t; }
+#endif
             xsync<true>();
             // ---- batch 3: transposed raw values (symmetrisation), gains of the terminal columns ----
             if (gc >= 0) {
@@ -1355,24 +938,28 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                         const double gv[4] = {g01.x, g01.y, g23.x, g23.y};
                         double t = 0;
 #pragma unroll
-                        for (int qq = 0; qq < NX; ++qq) t += w[qq] * abc_nz(AB, qq);
+                        for (int qq = 0; qq < NX; ++qq) t += w[qq] * ABe(qq * NAB + NZ);
 #pragma unroll
                         for (int v = 0; v < NV; ++v) t += q[NX + v] * gv[v];
                         pe[NC + rr] += t;
                     }
                 }
             }
-            if (k > 0) put_st((k - 1) & 1, sf[1]);
-#pragma unroll
-            for (int r = 0; r + 1 < RING; ++r) {
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) pf[r][i] = pf[r + 1][i];
-#pragma unroll
-                for (int t = 0; t < NST; ++t) sf[r][t] = sf[r + 1][t];
-            }
-            load_stage(k - RING, pf[RING - 1], sf[RING - 1]);
+            xsync<true>();  // every read of slot k % RING is complete before the DMA refills it
+            issue(k - RING);
+#ifdef NLOT_PHASE_PROF
+            { const long long t = wall_clock64(); ph[3] += t - tq; tq = t; }
+#endif
             xsync<true>();
+#ifdef NLOT_PHASE_PROF
+            ph[4] += wall_clock64() - tq;
+#endif
         }
+#ifdef NLOT_PHASE_PROF
+        if (b == 0 && l == 0 && SC(SC_ITERS) < 3)
+            printf("RICG stage phases: WQ %lld syncA+Qv %lld ldl+gains+VU %lld sym+PE+stage %lld syncC %lld (x10ns, sum over stages)\n",
+                   ph[0], ph[1], ph[2], ph[3], ph[4]);
+#endif
         if (own_pe)
 #pragma unroll
             for (int c = 0; c < NC + 2; ++c) sh.PE[a_pe][c] = pe[c];
@@ -1443,7 +1030,11 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
 #pragma unroll
                     for (int c = 0; c < 3; ++c) o[a * (NZ + 2) + c] += ddw * J[a] * J[c];
                     o[a * (NZ + 2) + NZ] += J[a] * r;
-                    if (nr > 1) o[a * (NZ + 2) + NZ + 1] += J[a] * r;
+                    o[NZ * (NZ + 2) + a] += J[a] * r;
+                    if (nr > 1) {
+                        o[a * (NZ + 2) + NZ + 1] += J[a] * r;
+                        o[(NZ + 1) * (NZ + 2) + a] += J[a] * r;
+                    }
                     if (sd) {
                         o[is * (NZ + 2) + a] += ddw * J[a];
                         o[a * (NZ + 2) + is] += ddw * J[a];
@@ -1452,7 +1043,11 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 if (sd) {
                     o[is * (NZ + 2) + is] += ddw;
                     o[is * (NZ + 2) + NZ] += r;
-                    if (nr > 1) o[is * (NZ + 2) + NZ + 1] += r;
+                    o[NZ * (NZ + 2) + is] += r;
+                    if (nr > 1) {
+                        o[is * (NZ + 2) + NZ + 1] += r;
+                        o[(NZ + 1) * (NZ + 2) + is] += r;
+                    }
                 }
             }
         }
