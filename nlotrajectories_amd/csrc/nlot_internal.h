@@ -34,6 +34,7 @@ struct MlpDev {
     const float* W;     // [n_hidden][H][H] (out, in)
     const float* b;     // [n_hidden][H]
     const float* w_out; // [H]
+    const void* Wp;     // [3][H][H] bf16 planes (hi, mid, lo) of layer 0, for the split-bf16 value kernel
 };
 
 // Output addressing of the MLP kernel: element q of point i goes to ptr_q[i * stride_q].

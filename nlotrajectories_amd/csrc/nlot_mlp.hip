@@ -22,6 +22,10 @@
 //     lam*d2f/dp2 = A diag(g .* (-scale cos z)) A^T (g = df/dh0), for a ReLU input layer it is 0.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
 #include "nlot_internal.h"
 
 namespace nlot {
@@ -342,6 +346,238 @@ __global__ __launch_bounds__(mlp_threads(H, L, FULL), (FULL || L > 1) ? 1 : 2) v
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 MFMA kernels with fp32-equivalent products (Fourier / ReLU input layer, one HxH layer).
+// Both operands are split into three bf16 parts, x = x_hi + x_mid + x_lo (8 + 8 + 8 significant bits,
+// exact up to 2^-24 relative), and each 32x32x16 block takes the six products down to 2^-24:
+// hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid — every product exact in the fp32 accumulator, the dropped
+// ones below fp32 rounding.  6 v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) replace 8 v_mfma_f32_32x32x2_f32
+// (8 x 64 cycles) per 16 k.  The weight planes are split once at nlot_mlp_create (MlpDev::Wp) and staged
+// once per block as one row-major image; the forward GEMM reads it by rows (ds_read_b128), the reverse
+// sweep G = W^T (lam w_out .* mask) by transposed reads (ds_read_b64_tr_b16) — one image for both.  The
+// input-layer activations are split as they are computed, directly in the B-operand layout (lane l:
+// point l & 31, k = 16 s + 8 (l >> 5) + j); the reverse sweep's B operand is the forward accumulator
+// (mask and w_out) split in place (accumulator-as-operand k order).
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;  // exact
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);    // exact difference
+}
+
+// six split-bf16 products, smallest terms first
+__device__ __forceinline__ f32x16 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                        const bf16x8& bm, const bf16x8& bl, f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    return acc;
+}
+
+// A fragment (32x32x16) of W^T from the row-major plane image by two transposed reads: lane group
+// g = lane / 16 covers columns c0 = col0 + 16 (g & 1) .. +15 of W; lane 4q + p of the group supplies row
+// r0 + q, columns c0 + 4p .. +3, and receives its own column's 4 rows.  Rows follow the
+// accumulator-as-operand k order: element jj of lane half h is row jbase + 8 (jj >> 2) + 4 h + (jj & 3).
+template <int RS>
+__device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int col0, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+    const int c0 = col0 + 16 * (g & 1);
+    const __bf16* a0 = plane + (size_t)(jbase + 4 * h + q) * RS + c0 + 4 * p;
+    const __bf16* a1 = a0 + (size_t)8 * RS;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a0));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a1));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// value: 8 waves = 2 per SIMD share one weight image; FULL (value + reverse sweep, ~300 VGPRs): 1 per SIMD
+__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 256 : 512; }
+
+template <int H>
+__host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
+    return (size_t)3 * H * (H + 8) * 2 + (size_t)5 * H * 4;
+}
+
+template <int H, bool FULL>
+__global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+                                                            const int* __restrict__ cnt_dev, int P_per, int64_t ld,
+                                                            const float* __restrict__ lam, MlpOut out) {
+    constexpr int RS = H + 8;    // padded plane row (bf16): 16-byte rows offset by 4 banks
+    constexpr int NT = H / 32;   // 32-row tiles
+    constexpr int NKB = H / 16;  // 16-wide k blocks
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    __bf16* sWp = reinterpret_cast<__bf16*>(smem);                  // [3][H][RS]
+    float* sA0 = reinterpret_cast<float*>(sWp + (size_t)3 * H * RS);  // [H]
+    float* sA1 = sA0 + H;
+    float* sb0 = sA1 + H;
+    float* sb = sb0 + H;
+    float* sw = sb + H;
+    for (int idx = threadIdx.x; idx < 3 * H * H / 8; idx += blockDim.x) {  // 16-byte chunks of the planes
+        const int pr = idx / (H / 8), c8 = idx % (H / 8);                   // pr = plane * H + row
+        *reinterpret_cast<uint4*>(sWp + (size_t)pr * RS + c8 * 8) = reinterpret_cast<const uint4*>(w.Wp)[idx];
+    }
+    for (int idx = threadIdx.x; idx < H; idx += blockDim.x) {
+        sA0[idx] = w.A[idx];
+        sA1[idx] = w.A[H + idx];
+        sb0[idx] = w.b0[idx];
+        sb[idx] = w.b[idx];
+        sw[idx] = w.w_out[idx];
+    }
+    __syncthreads();
+
+    const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
+    const int64_t npts = cnt * P_per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int il = lane & 31, hl = lane >> 5;
+    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
+    const float scale = w.scale;
+    constexpr int TP = bf16_threads(FULL) / 2;  // points per block tile (32 per wave)
+
+    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += gridDim.x) {
+        const int64_t gi = tile * TP + wave * 32 + il;
+        const bool valid = gi < npts;
+        const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
+        float px = 0.f, py = 0.f;
+        if (valid) {
+            px = pts[2 * pi];
+            py = pts[2 * pi + 1];
+        }
+        // ---------------- input layer + hidden GEMM ----------------
+        f32x16 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll 2
+        for (int s = 0; s < NKB; ++s) {
+            bf16x8 bh, bm, bl;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const int k = 16 * s + 8 * hl + jj;
+                const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
+                float h0;
+                if (fourier) {
+                    float sn, cs;
+                    sincos_fourier(z, &sn, &cs);
+                    h0 = cs * scale;
+                } else {
+                    h0 = z > 0.f ? z : 0.f;
+                }
+                __bf16 a, b, c;
+                split3(h0, a, b, c);
+                bh[jj] = a;
+                bm[jj] = b;
+                bl[jj] = c;
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const __bf16* rowp = sWp + (size_t)(t * 32 + il) * RS + 16 * s + 8 * hl;
+                const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
+                const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
+                const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
+                acc[t] = mfma6(ah, am, al, bh, bm, bl, acc[t]);
+            }
+        }
+        // ---------------- bias + ReLU + output layer (accumulator layout of the f32 MFMA: acc_row) ----------------
+        float fpart = 0.f;
+        uint64_t mask = 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int j = t * 32 + acc_row(r, hl);
+                const float v = acc[t][r] + sb[j];
+                const bool on = v > 0.f;
+                fpart = fmaf(sw[j], on ? v : 0.f, fpart);
+                mask |= (uint64_t)on << (t * 16 + r);
+            }
+        const float f = fpart + __shfl_xor(fpart, 32) + w.b_out;
+        if constexpr (!FULL) {
+            if (valid && hl == 0) out.val[pi * out.sv] = f;
+        } else {
+            // ---------------- reverse sweep: G = W^T e, e = lam * w_out .* mask ----------------
+            const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
+            f32x16 g[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) g[t] = f32x16{};
+#pragma unroll 1
+            for (int tj = 0; tj < NT; ++tj)
+#pragma unroll 1
+                for (int sl = 0; sl < 2; ++sl) {
+                    // e split straight into the B fragment of k-step (tj, sl): element jj = accumulator
+                    // register 8 sl + jj (permuted k order)
+                    bf16x8 bh, bm, bl;
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const int r = 8 * sl + jj;
+                        const float e = ((mask >> (tj * 16 + r)) & 1) ? lm * sw[tj * 32 + acc_row(r, hl)] : 0.f;
+                        __bf16 a, b, c;
+                        split3(e, a, b, c);
+                        bh[jj] = a;
+                        bm[jj] = b;
+                        bl[jj] = c;
+                    }
+                    const int jbase = 32 * tj + 16 * sl;
+#pragma unroll
+                    for (int tk = 0; tk < NT; ++tk) {
+                        const bf16x8 ah = wt_frag<RS>(sWp, jbase, 32 * tk, lane);
+                        const bf16x8 am = wt_frag<RS>(sWp + (size_t)H * RS, jbase, 32 * tk, lane);
+                        const bf16x8 al = wt_frag<RS>(sWp + (size_t)2 * H * RS, jbase, 32 * tk, lane);
+                        g[tk] = mfma6(ah, am, al, bh, bm, bl, g[tk]);
+                    }
+                }
+            // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point)
+            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = t * 32 + acc_row(r, hl);
+                    const float ax = sA0[k], ay = sA1[k];
+                    const float z = fmaf(py, ay, px * ax) + sb0[k];
+                    const float d = g[t][r];
+                    float dz, c2;
+                    if (fourier) {
+                        float sn, cs;
+                        sincos_fourier(z, &sn, &cs);
+                        dz = d * (-scale * sn);
+                        c2 = d * (-scale * cs);
+                    } else {
+                        dz = z > 0.f ? d : 0.f;
+                        c2 = 0.f;
+                    }
+                    gx = fmaf(ax, dz, gx);
+                    gy = fmaf(ay, dz, gy);
+                    hxx = fmaf(ax * ax, c2, hxx);
+                    hxy = fmaf(ax * ay, c2, hxy);
+                    hyy = fmaf(ay * ay, c2, hyy);
+                }
+            gx += __shfl_xor(gx, 32);
+            gy += __shfl_xor(gy, 32);
+            hxx += __shfl_xor(hxx, 32);
+            hxy += __shfl_xor(hxy, 32);
+            hyy += __shfl_xor(hyy, 32);
+            if (valid && hl == 0) {
+                out.val[pi * out.sv] = f;
+                if (out.gx) {
+                    out.gx[pi * out.sg] = gx;
+                    out.gy[pi * out.sg] = gy;
+                }
+                if (out.hxx) {
+                    out.hxx[pi * out.sh] = hxx;
+                    out.hxy[pi * out.sh] = hxy;
+                    if (out.hyx != out.hxy) out.hyx[pi * out.sh] = hxy;
+                    out.hyy[pi * out.sh] = hyy;
+                }
+            }
+        }
+    }
+}
+
 static int g_num_cus = 0;
 
 static int num_cus() {
@@ -364,6 +600,27 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
         NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_kernel<H, L, FULL>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
+    }
+    if constexpr (L == 1 && H == 128) {
+        // split-bf16 MFMA kernels (fp32-equivalent products); NLOT_MLP=f32 selects the f32-MFMA kernels
+        static const bool use_bf16 = !(getenv("NLOT_MLP") && strcmp(getenv("NLOT_MLP"), "f32") == 0);
+        if (use_bf16 && w.Wp) {
+            constexpr size_t lv = mlp_bf16_lds_bytes<H>();
+            static bool attr_v = false;
+            if (!attr_v) {
+                NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_bf16<H, FULL>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv));
+                attr_v = true;
+            }
+            constexpr int NTB = bf16_threads(FULL);
+            const int64_t tiles = (n * P_per + NTB / 2 - 1) / (NTB / 2);
+            const int64_t cap = num_cus();
+            const int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
+            hipLaunchKernelGGL((mlp_bf16<H, FULL>), dim3(grid), dim3(NTB), lv, stream, w, pts, n, n_dev, P_per, ld,
+                               lam, out);
+            NLOT_HIP_CHECK(hipGetLastError());
+            return NLOT_OK;
+        }
     }
     constexpr int NTH = mlp_threads(H, L, FULL);
     int64_t tiles = (n * P_per + NTH / 2 - 1) / (NTH / 2);
@@ -418,7 +675,8 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     }
     const int H = d->hidden, L = d->n_hidden;
     const size_t nA = 2 * H, nb0 = H, nW = (size_t)L * H * H, nb = (size_t)L * H, nw = H;
-    const size_t total = nA + nb0 + nW + nb + nw;
+    const size_t nWp = (size_t)3 * H * H / 2;  // bf16 planes of layer 0, in float units
+    const size_t total = nA + nb0 + nW + nb + nw + nWp;
     float* blk = nullptr;
     if (hipMalloc(&blk, total * sizeof(float)) != hipSuccess) {
         set_error("nlot_mlp_create: hipMalloc failed");
@@ -443,6 +701,31 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     m->dev.W = put(d->W, nW);
     m->dev.b = put(d->b, nb);
     m->dev.w_out = put(d->w_out, nw);
+    {  // layer-0 weights split into three bf16 planes, round-to-nearest-even at each step (host, exact)
+        std::vector<uint16_t> planes((size_t)3 * H * H);
+        auto bf16_rne = [](float x) -> uint16_t {
+            uint32_t u;
+            memcpy(&u, &x, 4);
+            return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+        };
+        auto bf16_f = [](uint16_t h) -> float {
+            const uint32_t u = (uint32_t)h << 16;
+            float f;
+            memcpy(&f, &u, 4);
+            return f;
+        };
+        for (size_t i = 0; i < (size_t)H * H; ++i) {
+            const float x = d->W[i];
+            const uint16_t hi = bf16_rne(x);
+            const float r = x - bf16_f(hi);
+            const uint16_t mid = bf16_rne(r);
+            const uint16_t lo = bf16_rne(r - bf16_f(mid));
+            planes[i] = hi;
+            planes[(size_t)H * H + i] = mid;
+            planes[(size_t)2 * H * H + i] = lo;
+        }
+        m->dev.Wp = put(reinterpret_cast<const float*>(planes.data()), nWp);
+    }
     if (hipDeviceSynchronize() != hipSuccess) {
         set_error("nlot_mlp_create: copy failed");
         hipFree(blk);
