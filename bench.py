@@ -34,6 +34,11 @@ from nlotrajectories_amd.sampling import sample_start_goal  # noqa: E402
 from nlotrajectories_amd.solver import last_stats, set_timing, solve_batch  # noqa: E402
 
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = f32 vector peak (dense)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 MFMA, dense
+SPLIT_PRODUCTS = 6  # fp32-equivalent product = 6 bf16 MFMA products (nlot_mlp.hip, split-bf16 kernels)
+# the MLP kernels emulate fp32 products with 6 bf16 MFMAs: their MFMA roofline for the algorithmic
+# (fp32) FLOPs is the dense bf16 peak / 6
+PEAK_SPLIT_TFLOPS = PEAK_BF16_MFMA_TFLOPS / SPLIT_PRODUCTS
 PEAK_HBM_GBS = 8000.0
 
 
@@ -162,12 +167,15 @@ def main():
                 "riccati_slots": "lds" if slots_in_lds else "hbm",
             },
             "roofline": {
-                "kernel": "mlp_kernel<128,1,full> (SDF-MLP value+grad+Hessian, v_mfma_f32_32x32x2_f32)",
+                "kernel": "mlp_bf16<128,full> (SDF-MLP value+grad+Hessian; fp32-equivalent products as 6 split "
+                          "v_mfma_f32_32x32x16_bf16)",
                 "bound": "mfma",
                 "achieved": achieved,
-                "peak": PEAK_F32_MFMA_TFLOPS,
+                "peak": PEAK_SPLIT_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": achieved / PEAK_F32_MFMA_TFLOPS,
+                "frac": achieved / PEAK_SPLIT_TFLOPS,
+                "peak_note": "dense bf16 MFMA peak 2500 TFLOP/s / 6 split products per fp32-equivalent product; "
+                             "the f32-input MFMA peak would be 157.3",
                 "traffic": traffic,
                 "flop_per_point": flop_pt,
                 "points_per_launch": agg["mlp_points_full"] / n_l,

@@ -47,13 +47,28 @@ struct MlpOut {
     float* hyx;  // may alias hxy (SoA) or be the [1][0] slot of an AoS 2x2
     float* hyy;
     int sv, sg, sh;
+    uint32_t* mask;      // value launches: the hidden layer's ReLU pattern, 4 words per point (or null)
+    int64_t mask_plane;  // word w of point i at mask[w * mask_plane + i]
+};
+
+// Forward reuse for full launches: the instance with compaction rank r has, when src[r] >= 0, been
+// evaluated by a value launch at trial slot src[r] (tpts, tval, tmask: points, values, ReLU patterns of
+// that launch, point i of slot s at s * P_per + i).  Where the trial point equals the point, the full
+// kernel takes f and the pattern from there and skips the forward GEMM (same arithmetic: same result).
+struct MlpReuse {
+    const int* src;
+    const float* tpts;
+    const float* tval;
+    const uint32_t* tmask;
+    int64_t plane;
 };
 
 // Launch the MFMA SDF-MLP kernel on cnt * P_per points, cnt = *n_dev if n_dev else n (n = upper bound
 // that sizes the persistent grid).  Point g lives at g (ld == 0) or (g % cnt) + (g / cnt) * ld.
 // full = value + lam*grad + lam*hess; else value only.
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
-                       const float* lam, const MlpOut& out, bool full, hipStream_t stream);
+                       const float* lam, const MlpOut& out, bool full, hipStream_t stream,
+                       const MlpReuse* reuse = nullptr);
 
 }  // namespace nlot
 

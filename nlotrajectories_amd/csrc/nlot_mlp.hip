@@ -397,7 +397,7 @@ __device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int co
 }
 
 // value: 8 waves = 2 per SIMD share one weight image; FULL (value + reverse sweep, ~300 VGPRs): 1 per SIMD
-__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 256 : 512; }
+__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 512 : 512; }
 
 template <int H>
 __host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
@@ -407,7 +407,7 @@ __host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
 template <int H, bool FULL>
 __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
                                                             const int* __restrict__ cnt_dev, int P_per, int64_t ld,
-                                                            const float* __restrict__ lam, MlpOut out) {
+                                                            const float* __restrict__ lam, MlpOut out, MlpReuse ru) {
     constexpr int RS = H + 8;    // padded plane row (bf16): 16-byte rows offset by 4 banks
     constexpr int NT = H / 32;   // 32-row tiles
     constexpr int NKB = H / 16;  // 16-wide k blocks
@@ -448,11 +448,29 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
             px = pts[2 * pi];
             py = pts[2 * pi + 1];
         }
+        // ---------------- forward reuse (full launches after an accepted trial point) ----------------
+        float f = 0.f;
+        uint64_t mask = 0;
+        bool have = false;
+        if (FULL && ru.src && ld == 0) {
+            const int64_t rk = gi / P_per;
+            const int src = valid ? ru.src[rk] : -1;
+            if (src >= 0) {
+                const int64_t q = (int64_t)src * P_per + (gi - rk * P_per);
+                if (ru.tpts[2 * q] == px && ru.tpts[2 * q + 1] == py) {
+                    f = ru.tval[q];
+                    mask = (uint64_t)ru.tmask[(2 * hl) * ru.plane + q] |
+                           ((uint64_t)ru.tmask[(2 * hl + 1) * ru.plane + q] << 32);
+                    have = true;
+                }
+            }
+        }
+        if (!__all(have || !valid)) {  // wave-uniform: the forward for all 32 points of the wave
         // ---------------- input layer + hidden GEMM ----------------
         f32x16 acc[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-#pragma unroll 2
+#pragma unroll 1
         for (int s = 0; s < NKB; ++s) {
             bf16x8 bh, bm, bl;
 #pragma unroll
@@ -484,7 +502,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
         }
         // ---------------- bias + ReLU + output layer (accumulator layout of the f32 MFMA: acc_row) ----------------
         float fpart = 0.f;
-        uint64_t mask = 0;
+        uint64_t mk = 0;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -493,11 +511,22 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 const float v = acc[t][r] + sb[j];
                 const bool on = v > 0.f;
                 fpart = fmaf(sw[j], on ? v : 0.f, fpart);
-                mask |= (uint64_t)on << (t * 16 + r);
+                mk |= (uint64_t)on << (t * 16 + r);
             }
-        const float f = fpart + __shfl_xor(fpart, 32) + w.b_out;
+        const float fw = fpart + __shfl_xor(fpart, 32) + w.b_out;
+        if (!have) {
+            f = fw;
+            mask = mk;
+        }
+        }  // forward
         if constexpr (!FULL) {
-            if (valid && hl == 0) out.val[pi * out.sv] = f;
+            if (valid) {
+                if (hl == 0) out.val[pi * out.sv] = f;
+                if (out.mask) {
+                    out.mask[(2 * hl) * out.mask_plane + pi] = (uint32_t)mask;
+                    out.mask[(2 * hl + 1) * out.mask_plane + pi] = (uint32_t)(mask >> 32);
+                }
+            }
         } else {
             // ---------------- reverse sweep: G = W^T e, e = lam * w_out .* mask ----------------
             const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
@@ -530,15 +559,24 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                         g[tk] = mfma6(ah, am, al, bh, bm, bl, g[tk]);
                     }
                 }
-            // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point)
+            // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point); the
+            // four rows of a register quad are consecutive k: one 16-byte read per input-layer vector
             float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = t * 32 + acc_row(r, hl);
-                    const float ax = sA0[k], ay = sA1[k];
-                    const float z = fmaf(py, ay, px * ax) + sb0[k];
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int k0 = t * 32 + 8 * r4 + 4 * hl;
+                    const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
+                    const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
+                    const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int r = 4 * r4 + rr;
+                    const float ax = rr == 0 ? A0.x : rr == 1 ? A0.y : rr == 2 ? A0.z : A0.w;
+                    const float ay = rr == 0 ? A1.x : rr == 1 ? A1.y : rr == 2 ? A1.z : A1.w;
+                    const float bz = rr == 0 ? B0.x : rr == 1 ? B0.y : rr == 2 ? B0.z : B0.w;
+                    const float z = fmaf(py, ay, px * ax) + bz;
                     const float d = g[t][r];
                     float dz, c2;
                     if (fourier) {
@@ -555,6 +593,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                     hxx = fmaf(ax * ax, c2, hxx);
                     hxy = fmaf(ax * ay, c2, hxy);
                     hyy = fmaf(ay * ay, c2, hyy);
+                }
                 }
             gx += __shfl_xor(gx, 32);
             gy += __shfl_xor(gy, 32);
@@ -593,7 +632,7 @@ static int num_cus() {
 
 template <int H, int L, bool FULL>
 static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
-                    const float* lam, const MlpOut& out, hipStream_t stream) {
+                    const float* lam, const MlpOut& out, hipStream_t stream, const MlpReuse* reuse) {
     const size_t lds = sizeof(float) * mlp_lds_floats(H, L, FULL && mlp_staged(H, L));
     static bool attr_set = false;
     if (!attr_set) {
@@ -616,8 +655,9 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
             const int64_t tiles = (n * P_per + NTB / 2 - 1) / (NTB / 2);
             const int64_t cap = num_cus();
             const int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
+            const MlpReuse ru = reuse ? *reuse : MlpReuse{};
             hipLaunchKernelGGL((mlp_bf16<H, FULL>), dim3(grid), dim3(NTB), lv, stream, w, pts, n, n_dev, P_per, ld,
-                               lam, out);
+                               lam, out, ru);
             NLOT_HIP_CHECK(hipGetLastError());
             return NLOT_OK;
         }
@@ -633,7 +673,7 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
 }
 
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
-                       const float* lam, const MlpOut& out, bool full, hipStream_t stream) {
+                       const float* lam, const MlpOut& out, bool full, hipStream_t stream, const MlpReuse* reuse) {
     if (n <= 0) return NLOT_OK;
     if (w.n_hidden < 1 || w.n_hidden > kMaxResidentLayers) {
         set_error("MLP kernel: 1 or 2 hidden HxH layers are supported (DESIGN.md §7)");
@@ -641,8 +681,8 @@ int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* 
     }
 #define NLOT_MLP_CASE(HH, LL)                                                                      \
     if (w.H == HH && w.n_hidden == LL)                                                             \
-        return full ? launch_t<HH, LL, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream)        \
-                    : launch_t<HH, LL, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+        return full ? launch_t<HH, LL, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream, reuse) \
+                    : launch_t<HH, LL, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream, reuse);
     NLOT_MLP_CASE(64, 1)
     NLOT_MLP_CASE(64, 2)
     NLOT_MLP_CASE(128, 1)

@@ -45,6 +45,7 @@ enum Scal {
     // failed), its barrier parameters and right-hand-side count, and the optimality scalars the
     // quality-function oracle needs
     SC_RIC, SC_RMU0, SC_RMU1, SC_RNR, SC_USEQF, SC_AVG, SC_DSQ, SC_PSQ, SC_NZC,
+    SC_ACCSLOT,  // trial-list slot of the accepted line-search candidate (forward reuse), -1 if none
     SC_COUNT
 };
 constexpr int FILT_MAX = 64;
@@ -116,6 +117,10 @@ struct Ws {
 #undef NLOT_DECL
     float* pts;  // compacted corner list, rank-major [rank][P][2]
     float* mo;   // MLP outputs [6][cap * P] (rank-major within a plane)
+    float* tpts;      // trial corner list [slot][P][2] (slot = rank + candidate), cap * NSPEC slots
+    float* tval;      // its values [slot][P]
+    uint32_t* tmask;  // its hidden-layer ReLU patterns [4][slot][P]
+    int* tsrc;        // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
     int* cnt;    // [0] eval instances, [1] trial instances, [2] next active count
     int* act[2]; // active instance lists (ping-pong)
     int64_t cap;
@@ -144,6 +149,10 @@ static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
         const size_t P = (size_t)d.ppk * (d.N + 1);
         b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
         b += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
+        b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));  // tpts
+        b += align256(P * (size_t)B * NSPEC * sizeof(float));      // tval
+        b += align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));  // tmask
+        b += align256((size_t)B * sizeof(int));                    // tsrc
     }
     b += align256(2 * (size_t)B * sizeof(int));
     b += 256;  // counters
@@ -170,6 +179,14 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
         c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
         w.mo = (float*)c;
         c += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
+        w.tpts = (float*)c;
+        c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
+        w.tval = (float*)c;
+        c += align256(P * (size_t)B * NSPEC * sizeof(float));
+        w.tmask = (uint32_t*)c;
+        c += align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));
+        w.tsrc = (int*)c;
+        c += align256((size_t)B * sizeof(int));
     }
     w.act[0] = (int*)c;
     w.act[1] = (int*)c + B;
@@ -222,8 +239,14 @@ __device__ __forceinline__ void xsync() {
 // ---------------------------------------------------------------------------------------------
 // per-corner SDF: learned (MLP output of this step's compacted list) or analytic
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, int pidx, double cx, double cy) {
+__device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, int pidx, double cx, double cy,
+                                         bool trial = false) {
     if (p.sdf_kind == NLOT_SDF_ANALYTIC) return sdf_scene(p, cx, cy, true);
+    if (trial) {  // value launch of the trial list (slot = rank)
+        HD h{};
+        h.v = ws.tval[(int64_t)rank * ws.ppk * (p.N + 1) + pidx];
+        return h;
+    }
     // MLP outputs of this step's compacted list, rank-major: quantity q of point pidx of the
     // instance with compaction rank r at mo[q * plane + r * P + pidx]
     const int64_t P = (int64_t)ws.ppk * (p.N + 1);
@@ -242,10 +265,11 @@ __device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int
 // Inequality functions at a knot (geometry.py:63-67, 107-117; utils.py:18-33): values d[j]
 // (slack excluded), pose gradients g[j][3], and Hw = sum_j w[j] d2 d_j / dpose2 (if w != null).
 __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
-                                 const double* xk, double* d, double (*g)[3], const double* w, double* Hw) {
+                                 const double* xk, double* d, double (*g)[3], const double* w, double* Hw,
+                                 bool trial = false) {
     const double x = xk[0], y = xk[1];
     if (p.shape == NLOT_SHAPE_DOT) {
-        HD f = corner_sdf(p, ws, rank, k, x, y);
+        HD f = corner_sdf(p, ws, rank, k, x, y, trial);
         d[0] = f.v;
         if (g) { g[0][0] = f.gx; g[0][1] = f.gy; g[0][2] = 0; }
         if (Hw) {
@@ -263,7 +287,7 @@ __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, 
         const double bx = p.body[i][0], by = p.body[i][1];
         const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
         const double ex = -(cy - y), ey = cx - x;                            // d c / d theta
-        HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy);
+        HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, trial);
         phi[i] = f.v;
         gp[i][0] = f.gx;
         gp[i][1] = f.gy;
@@ -1316,6 +1340,7 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
         SC(SC_STATUS) = -1;
         SC(SC_ITERS) = 0;
         SC(SC_PHASE) = PH_INIT;
+        SC(SC_ACCSLOT) = -1;
         SC(SC_NFILT) = 0;
         SC(SC_E0) = 0;
         ws.act[0][b] = b;
@@ -1358,6 +1383,7 @@ __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ p
         rank = atomicAdd(&ws.cnt[trial ? 1 : 0], ncand);
         SC(SC_RANK) = rank;
         SC(SC_NCAND) = ncand;
+        if (!trial && ws.tsrc) ws.tsrc[rank] = (int)SC(SC_ACCSLOT);
     }
     rank = __shfl(rank, 0);
     const int nx = dm.nx, nb = dm.nb;
@@ -1380,8 +1406,9 @@ __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ p
             px = (float)(x + cs * bx - sn * by);
             py = (float)(y + sn * bx + cs * by);
         }
-        ws.pts[(base + e) * 2] = px;
-        ws.pts[(base + e) * 2 + 1] = py;
+        float* dst = trial ? ws.tpts : ws.pts;
+        dst[(base + e) * 2] = px;
+        dst[(base + e) * 2 + 1] = py;
     }
     }
 }
@@ -2245,7 +2272,7 @@ __global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ p
                 for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
             }
             double d[MMAX];
-            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr);
+            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, true);
             const double sk = AT(S, k) + al * AT(dS, k);
             for (int j = 0; j < M; ++j) {
                 const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
@@ -2341,6 +2368,7 @@ __global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ p
             if (lane == 0) {
                 SC(SC_ITERS) = SC(SC_ITERS) + 1;
                 SC(SC_PHASE) = PH_EVAL;
+                SC(SC_ACCSLOT) = rank0 + cnd - 1;  // the loop stepped past the accepted candidate
             }
         } else {
             const double na = ldexp(a0, -ncand);
@@ -2442,12 +2470,20 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (g_timing)
         for (auto& e : ev) hipEventCreate(&e);
-    MlpOut mo{};
+    MlpOut mo{}, mo_t{};
+    MlpReuse reuse{};
     if (use_mlp) {
         const int64_t plane = P * B * NSPEC;
         mo.val = ws.mo; mo.gx = ws.mo + plane; mo.gy = ws.mo + 2 * plane; mo.hxx = ws.mo + 3 * plane;
         mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
         mo.sv = mo.sg = mo.sh = 1;
+        // trial list: values + ReLU patterns, reused by the next full launch at the accepted point
+        mo_t.val = ws.tval;
+        mo_t.sv = 1;
+        mo_t.mask = ws.tmask;
+        mo_t.mask_plane = P * B * NSPEC;
+        static const bool no_reuse = getenv("NLOT_MLP_REUSE") && strcmp(getenv("NLOT_MLP_REUSE"), "0") == 0;
+        reuse = MlpReuse{no_reuse ? nullptr : ws.tsrc, ws.tpts, ws.tval, ws.tmask, P * B * NSPEC};
     }
     g_stats.slots_in_lds = 0;  // stage slots live in the HBM workspace; k_ric stages them through LDS
     const int ric_blocks_per = RicG<DYN>::IPW;
@@ -2464,7 +2500,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0, 1);
             if (ev[0]) hipEventRecord(ev[0], st);
             // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
-            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st);
+            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st, &reuse);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[1], st);
         }
@@ -2485,7 +2521,8 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         if (use_mlp) {
             hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1, nspec);
             if (ev[0]) hipEventRecord(ev[2], st);
-            rc = launch_mlp_strided(mlp->dev, ws.pts, (int64_t)n_active * NSPEC, ws.cnt + 1, (int)P, 0, nullptr, mo, false, st);
+            rc = launch_mlp_strided(mlp->dev, ws.tpts, (int64_t)n_active * NSPEC, ws.cnt + 1, (int)P, 0, nullptr, mo_t,
+                                    false, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[3], st);
             g_stats.mlp_full_launches++;

@@ -4,7 +4,7 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-names = {"k_iter_a": "ita", "k_ric": "ric", "k_iter_b": "itb", "k_iterate": "iter", "mlp_kernel<128, 1, true>": "full",
+names = {"k_iter_a": "ita", "k_ric": "ric", "k_iter_b": "itb", "k_iterate": "iter", "mlp_kernel<128, 1, true>": "full", "mlp_bf16<128, true>": "full", "mlp_bf16<128, false>": "val",
          "mlp_kernel<128, 1, false>": "val", "k_accept": "acc", "k_points": "pts"}
 per = collections.defaultdict(list)
 for r in rows:
