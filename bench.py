@@ -93,7 +93,8 @@ def main():
         step()
     set_timing(True)
     agg = dict(mlp_full_ms=0.0, mlp_full_launches=0, mlp_points_full=0, mlp_value_ms=0.0,
-               mlp_value_launches=0, mlp_points_value=0, iterations=0, iterate_ms=0.0)
+               mlp_value_launches=0, mlp_points_value=0, iterations=0, iterate_ms=0.0,
+               mlp_points_full_reused=0)
     slots_in_lds = None
     iters_all, solved_total = [], 0
     if world > 1:
@@ -117,11 +118,15 @@ def main():
     elapsed = max_over_ranks(elapsed, dev)
     solved_total = sum_over_ranks(solved_total, dev)
 
-    # roofline of the dominant kernel: the full (value + gradient + Hessian) SDF-MLP launch
+    # roofline of the dominant MFMA kernel: the full (value + gradient + Hessian) SDF-MLP launch.  FLOP are
+    # counted as executed: the reverse sweep at every point, the forward only where the launch did not take
+    # it from the accepted trial point's value launch (forward reuse)
     flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1
+    flop_fwd = w.flops_per_point_fwd      # 33,536
     n_l = max(agg["mlp_full_launches"], 1)
     avg_ms = agg["mlp_full_ms"] / n_l
-    flop_launch = agg["mlp_points_full"] * flop_pt / n_l
+    reused = agg["mlp_points_full_reused"]
+    flop_launch = (agg["mlp_points_full"] * flop_pt - reused * flop_fwd) / n_l
     achieved = flop_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     traffic = None
     tf = os.path.join(ROOT, "profiles", "mlp_full_traffic.json")
@@ -148,7 +153,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64 (interior-point solver) + f32 (SDF-MLP on f32 MFMA, as the reference's fp32 libtorch)",
+            "dtype": "f64 (interior-point solver) + f32 (SDF-MLP: fp32-equivalent split-bf16 MFMA products, as "
+                     "the reference's fp32 libtorch graph)",
             "data": "synthetic start/goal (seeded, SURVEY.md §8d); learned SDF = reference artefact weights",
             "config": {
                 "workload": "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
@@ -178,6 +184,8 @@ def main():
                              "the f32-input MFMA peak would be 157.3",
                 "traffic": traffic,
                 "flop_per_point": flop_pt,
+                "forward_reused_frac": reused / max(agg["mlp_points_full"], 1),
+                "flop_counting": "executed: 67,072 per point, less the 33,536 forward where it was reused",
                 "points_per_launch": agg["mlp_points_full"] / n_l,
                 "avg_launch_ms": avg_ms,
                 "launches": agg["mlp_full_launches"],

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 2
+#define NLOT_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -202,6 +202,7 @@ typedef struct NlotSolveStats {
     double iterate_ms;         /* summed device time of the solver-step (k_iterate) launches */
     int32_t slots_in_lds;      /* 1: Riccati stage slots held in LDS, 0: in the HBM workspace */
     int32_t pad_;
+    int64_t mlp_points_full_reused; /* full-launch points whose forward came from the accepted trial point */
 } NlotSolveStats;
 /* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
 void nlot_set_timing(int32_t enabled);

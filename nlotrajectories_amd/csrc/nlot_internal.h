@@ -61,6 +61,7 @@ struct MlpReuse {
     const float* tval;
     const uint32_t* tmask;
     int64_t plane;
+    int* nreused;  // if set: += the number of points whose forward was reused (statistics)
 };
 
 // Launch the MFMA SDF-MLP kernel on cnt * P_per points, cnt = *n_dev if n_dev else n (n = upper bound

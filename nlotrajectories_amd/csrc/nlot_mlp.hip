@@ -52,6 +52,18 @@ __device__ __forceinline__ void sincos_fourier(float x, float* sn, float* cs) {
     *cs = ((q + 1) & 2) ? -c0 : c0;
 }
 
+// Fourier-layer argument in turns for the transcendental unit (v_sin_f32 / v_cos_f32 give sin and cos of
+// 2 pi t): r = x - 2 pi j in [-pi, pi] by a two-part Cody-Waite reduction with FMA (the first product is
+// exact; the dropped third part, |j| * 3.4e-15, stays below 1e-12 for |x| <= 1e3), then r / (2 pi).  The
+// split-bf16 kernels use it: 4 instructions and one 8-cycle transcendental per sin or cos, against ~14 for
+// the polynomials and quadrant selects of sincos_fourier.
+__device__ __forceinline__ float turns_fourier(float x) {
+    const float j = rintf(x * 0.159154943091895336f);
+    float r = fmaf(j, -6.28318548202514648f, x);
+    r = fmaf(j, 1.74845560e-7f, r);
+    return r * 0.159154943091895336f;
+}
+
 // row index (hidden unit) held by register r of a 32x32 accumulator on lane-half hl
 __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
 
@@ -396,12 +408,16 @@ __device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int co
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// value: 8 waves = 2 per SIMD share one weight image; FULL (value + reverse sweep, ~300 VGPRs): 1 per SIMD
-__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 512 : 512; }
+// one weight image per CU: FULL (value + reverse sweep) runs 8 waves = 2 per SIMD; value-only launches
+// NLOT_MLP_VALUE_THREADS / 256 waves per SIMD
+#ifndef NLOT_MLP_VALUE_THREADS
+#define NLOT_MLP_VALUE_THREADS 512
+#endif
+__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 512 : NLOT_MLP_VALUE_THREADS; }
 
 template <int H>
 __host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
-    return (size_t)3 * H * (H + 8) * 2 + (size_t)5 * H * 4;
+    return (size_t)3 * H * (H + 8) * 2 + (size_t)8 * H * 4;
 }
 
 template <int H, bool FULL>
@@ -418,6 +434,10 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     float* sb0 = sA1 + H;
     float* sb = sb0 + H;
     float* sw = sb + H;
+    float* sAxx = sw + H;  // a_x^2, a_x a_y, a_y^2 of the input layer (Hessian contraction)
+    float* sAxy = sAxx + H;
+    float* sAyy = sAxy + H;
+    __shared__ int s_reused;
     for (int idx = threadIdx.x; idx < 3 * H * H / 8; idx += blockDim.x) {  // 16-byte chunks of the planes
         const int pr = idx / (H / 8), c8 = idx % (H / 8);                   // pr = plane * H + row
         *reinterpret_cast<uint4*>(sWp + (size_t)pr * RS + c8 * 8) = reinterpret_cast<const uint4*>(w.Wp)[idx];
@@ -428,7 +448,11 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
         sb0[idx] = w.b0[idx];
         sb[idx] = w.b[idx];
         sw[idx] = w.w_out[idx];
+        sAxx[idx] = w.A[idx] * w.A[idx];
+        sAxy[idx] = w.A[idx] * w.A[H + idx];
+        sAyy[idx] = w.A[H + idx] * w.A[H + idx];
     }
+    if (threadIdx.x == 0) s_reused = 0;
     __syncthreads();
 
     const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
@@ -465,7 +489,12 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 }
             }
         }
-        if (!__all(have || !valid)) {  // wave-uniform: the forward for all 32 points of the wave
+        const bool skip = __all(have || !valid);  // wave-uniform
+        if (FULL && skip && ru.nreused) {
+            const uint64_t vb = __ballot(valid && hl == 0);
+            if (lane == 0) atomicAdd(&s_reused, (int)__popcll(vb));
+        }
+        if (!skip) {  // the forward for all 32 points of the wave
         // ---------------- input layer + hidden GEMM ----------------
         f32x16 acc[NT];
 #pragma unroll
@@ -479,9 +508,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
                 float h0;
                 if (fourier) {
-                    float sn, cs;
-                    sincos_fourier(z, &sn, &cs);
-                    h0 = cs * scale;
+                    h0 = __builtin_amdgcn_cosf(turns_fourier(z)) * scale;
                 } else {
                     h0 = z > 0.f ? z : 0.f;
                 }
@@ -570,36 +597,42 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                     const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
                     const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
                     const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
+                    const float4 XX = *reinterpret_cast<const float4*>(sAxx + k0);
+                    const float4 XY = *reinterpret_cast<const float4*>(sAxy + k0);
+                    const float4 YY = *reinterpret_cast<const float4*>(sAyy + k0);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int r = 4 * r4 + rr;
                     const float ax = rr == 0 ? A0.x : rr == 1 ? A0.y : rr == 2 ? A0.z : A0.w;
                     const float ay = rr == 0 ? A1.x : rr == 1 ? A1.y : rr == 2 ? A1.z : A1.w;
                     const float bz = rr == 0 ? B0.x : rr == 1 ? B0.y : rr == 2 ? B0.z : B0.w;
+                    const float axx = rr == 0 ? XX.x : rr == 1 ? XX.y : rr == 2 ? XX.z : XX.w;
+                    const float axy = rr == 0 ? XY.x : rr == 1 ? XY.y : rr == 2 ? XY.z : XY.w;
+                    const float ayy = rr == 0 ? YY.x : rr == 1 ? YY.y : rr == 2 ? YY.z : YY.w;
                     const float z = fmaf(py, ay, px * ax) + bz;
                     const float d = g[t][r];
                     float dz, c2;
-                    if (fourier) {
-                        float sn, cs;
-                        sincos_fourier(z, &sn, &cs);
-                        dz = d * (-scale * sn);
-                        c2 = d * (-scale * cs);
+                    if (fourier) {  // the factor -scale is applied to the sums
+                        const float tz = turns_fourier(z);
+                        dz = d * __builtin_amdgcn_sinf(tz);
+                        c2 = d * __builtin_amdgcn_cosf(tz);
                     } else {
                         dz = z > 0.f ? d : 0.f;
                         c2 = 0.f;
                     }
                     gx = fmaf(ax, dz, gx);
                     gy = fmaf(ay, dz, gy);
-                    hxx = fmaf(ax * ax, c2, hxx);
-                    hxy = fmaf(ax * ay, c2, hxy);
-                    hyy = fmaf(ay * ay, c2, hyy);
+                    hxx = fmaf(axx, c2, hxx);
+                    hxy = fmaf(axy, c2, hxy);
+                    hyy = fmaf(ayy, c2, hyy);
                 }
                 }
-            gx += __shfl_xor(gx, 32);
-            gy += __shfl_xor(gy, 32);
-            hxx += __shfl_xor(hxx, 32);
-            hxy += __shfl_xor(hxy, 32);
-            hyy += __shfl_xor(hyy, 32);
+            const float sg = fourier ? -scale : 1.f;
+            gx = sg * (gx + __shfl_xor(gx, 32));
+            gy = sg * (gy + __shfl_xor(gy, 32));
+            hxx = sg * (hxx + __shfl_xor(hxx, 32));
+            hxy = sg * (hxy + __shfl_xor(hxy, 32));
+            hyy = sg * (hyy + __shfl_xor(hyy, 32));
             if (valid && hl == 0) {
                 out.val[pi * out.sv] = f;
                 if (out.gx) {
@@ -614,6 +647,10 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 }
             }
         }
+    }
+    if (FULL && ru.nreused) {  // statistics: full-launch points whose forward was reused
+        __syncthreads();
+        if (threadIdx.x == 0 && s_reused) atomicAdd(ru.nreused, s_reused);
     }
 }
 

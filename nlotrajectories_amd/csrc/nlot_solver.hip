@@ -37,6 +37,25 @@
 namespace nlot {
 
 enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3 };
+
+// Minimum waves per SIMD the per-instance kernels are compiled for (register budget 512 / w per lane),
+// and the depth of k_ric's stage ring (its LDS per wavefront sets k_ric's occupancy).  These kernels wait
+// on memory most of their cycles (SQ_WAIT_ANY 56-73 %), so residency is speed.
+#ifndef NLOT_WPE_A
+#define NLOT_WPE_A 1
+#endif
+#ifndef NLOT_WPE_B
+#define NLOT_WPE_B 1
+#endif
+#ifndef NLOT_WPE_ACC
+#define NLOT_WPE_ACC 2
+#endif
+#ifndef NLOT_WPE_RIC
+#define NLOT_WPE_RIC 1
+#endif
+#ifndef NLOT_RIC_RING
+#define NLOT_RIC_RING 4
+#endif
 enum Scal {
     SC_MU, SC_TAU, SC_DWLAST, SC_THMAX, SC_THMIN, SC_ALPHA, SC_AMAX, SC_AMIN, SC_AZ, SC_THETA, SC_PHI, SC_GD,
     SC_DW, SC_DC, SC_STATUS, SC_ITERS, SC_PHASE, SC_TRIALS, SC_NFILT, SC_RANK, SC_E0, SC_NCAND,
@@ -83,14 +102,14 @@ static Dims make_dims(const NlotProblem& p) {
 //   vf (HBM): P (nx x nx) | p (2 x nx) | Gamma (nx x nc) — written by the backward sweep, read by the
 //     parallel multiplier pass.  (nz = nx + nu + 1, nv = nu + 1, nc = nx.)
 //   Layouts (row-major, ncol = nx + 2 + nc gain columns K | k_0 | k_1 | Kn):
-//     slot = [A B 0 | c | pad] (nx x ab_row) | M | GN (ncol x nv);  hg = [H | g_0 g_1] (nz x (nz+2)) followed by
-//     the rows g_0', g_1' (so that row j < nz+2 holds what the Riccati lane of column j reads: H symmetric);
+//     slot = [A B 0 | c | pad] (nx x ab_row) | M | GN (ncol x nv);  hg = [H | g_0 g_1] (nz x (nz+2)) (the
+//     Riccati lane of column j reads row j, H being symmetric, or a g column top to bottom);
 //     vf = [P | p_0 p_1 | Gamma] (nx x ncol).
 __host__ __device__ constexpr int ab_row(int nx, int nu) { return (nx + nu + 2 + 1) & ~1; }  // [A B 0 | c], even
 __host__ __device__ constexpr int slot_len(int nx, int nu) {
     return nx * ab_row(nx, nu) + 4 + (nx + 2 + nx) * (nu + 1);
 }
-__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 3) * (nx + nu + 3); }
+__host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 3); }
 __host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * (nx + 2 + nx); }
 // quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
 __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
@@ -121,7 +140,7 @@ struct Ws {
     float* tval;      // its values [slot][P]
     uint32_t* tmask;  // its hidden-layer ReLU patterns [4][slot][P]
     int* tsrc;        // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
-    int* cnt;    // [0] eval instances, [1] trial instances, [2] next active count
+    int* cnt;    // [0] eval instances, [1] trial instances, [2] next active count, [3] reused forwards
     int* act[2]; // active instance lists (ping-pong)
     int64_t cap;
     int ppk;
@@ -525,8 +544,6 @@ struct Solver {
                 }
                 o[i * (NZ + 2) + NZ] = gi + mu0 * gm;
                 o[i * (NZ + 2) + NZ + 1] = nr > 1 ? gi + mu1 * gm : 0.0;
-                o[NZ * (NZ + 2) + i] = gi + mu0 * gm;
-                o[(NZ + 1) * (NZ + 2) + i] = nr > 1 ? gi + mu1 * gm : 0.0;
             }
         };
         if (k < N) emit(std::true_type{});
@@ -546,14 +563,14 @@ struct Solver {
 
     // ---------------- stage layouts of the Riccati recursion (k_ric) ----------------
     //   slot: ABc = [A B 0 | c | pad] (NX x NAB) | M (2x2) | GN[c][v] (NCOL x NV: K^T | k_0 | k_1 | Kn^T)
-    //   hg:   [H | g_0 g_1] (NZ x (NZ+2)) | g_0' | g_1';  vf / VE: [P | p_0 p_1 | G] (NX x NCOL)
+    //   hg:   [H | g_0 g_1] (NZ x (NZ+2));  vf / VE: [P | p_0 p_1 | G] (NX x NCOL)
     //   QE:   [Q | q_0 q_1 | QN] (NZ x NQE);  W: [P AB | P c + p_0 | P c + p_1 | G] (NX x NQE)
     //   PE:   [Psi | psi_0 psi_1] (NC x (NC+2))
     static constexpr int NCOL = NX + 2 + NC, NQE = NZ + 2 + NC, NAB = ab_row(NX, NU);
     static constexpr int SLOT = slot_len(NX, NU), HG = hg_len(NX, NU), VF = vf_len(NX, NU);
     static constexpr int sAB = 0, sM = NX * NAB, sGN = sM + 4;
     static_assert(sGN + NCOL * NV == SLOT, "slot layout");
-    static_assert((NZ + 2) * (NZ + 2) == HG && NX * NCOL == VF, "hg / vf layout");
+    static_assert(NZ * (NZ + 2) == HG && NX * NCOL == VF, "hg / vf layout");
 
     // gain column c <-> QE column
     __host__ __device__ static constexpr int qe_col(int c) { return c < NX ? c : NZ + (c - NX); }
@@ -626,7 +643,7 @@ struct RicG {
     static constexpr int DW = 2 * G;                       // doubles per group per DMA instruction
     static constexpr int NDH = (SV::HG + DW - 1) / DW;     // DMA instructions for hg
     static constexpr int NDA = (NABM + DW - 1) / DW;       // ... for [A B 0 | c] | M
-    static constexpr int NDMA = NDH + NDA, RING = 4;
+    static constexpr int NDMA = NDH + NDA, RING = NLOT_RIC_RING;
     static_assert(SV::sAB == 0 && SV::sM == NX * NAB && NCOL <= NQE && NQE <= G && NV <= 4 && NAB % 2 == 0,
                   "RicG layout");
     struct alignas(16) Sh {  // per instance; every row starts on a 16-byte boundary
@@ -639,11 +656,31 @@ struct RicG {
 };
 typedef double d2v __attribute__((ext_vector_type(2)));
 
+// k_ric's LDS hand-offs between the lanes of its single wavefront.  NLOT_RIC_INORDER relies on the LDS
+// unit executing one wavefront's DS instructions in issue order (a ds_read issued after a ds_write sees
+// it), so only the compiler's order is pinned; the default waits for the LDS queue and barriers.
+__device__ __forceinline__ void ric_sync() {
+#ifdef NLOT_RIC_INORDER
+    asm volatile("" ::: "memory");
+#else
+    xsync<true>();
+#endif
+}
+// before a DMA refills a ring slot: the slot's reads have returned
+__device__ __forceinline__ void ric_sync_reads() {
+#ifdef NLOT_RIC_INORDER
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt and expcnt not waited
+    asm volatile("" ::: "memory");
+#else
+    xsync<true>();
+#endif
+}
+
 // Newton (or least-squares) solve of the instances whose stage matrices k_iter_a built (SC_RIC = 1),
 // with IPOPT's inertia correction: on a wrong inertia the group rebuilds its stages with the next
 // delta_w and factorises again.  Outputs: dX dU dS yi_n yk_n yt_n (and the second right-hand side).
 template <int DYN>
-__global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
                                             int mode) {
     using R = RicG<DYN>;
@@ -721,7 +758,7 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
         const int cc = j < NZ ? j : NZ;            // AB column (the c column for the p_r columns)
         const int jc = j >= NZ && j < NQE ? NX + j - NZ : 0;  // VE column carried into W
         const bool vlane = j >= NX && j < NX + NV;  // control columns: Q_vv, Q_xv
-        xsync<true>();
+        ric_sync();
 #ifdef NLOT_PHASE_PROF
         long long ph[5] = {0, 0, 0, 0, 0};
 #endif
@@ -735,12 +772,13 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
             auto HGe = [&](int e) { return hrow[(e / DW) * (R::IPW * DW) + e % DW]; };
             const double* abase = &ring[k % RING][NDH][grp][0];
             auto ABe = [&](int e) { return abase[(e / DW) * (R::IPW * DW) + e % DW]; };
-            double hcur[NZ];  // row j of hg: column j of [H | g_0 g_1] (H symmetric), zero beyond nr
+            double hcur[NZ];  // column j of [H | g_0 g_1]: row j of the symmetric H, or a g column read down; zero
+                              // beyond nr
             {
-                const int jr = j < NZ + 2 ? j : 0;
+                const int jg = j < NZ + 2 ? j : NZ;
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) {
-                    const double v = HGe(jr * (NZ + 2) + i);
+                    const double v = HGe(j < NZ ? j * (NZ + 2) + i : i * (NZ + 2) + jg);
                     hcur[i] = j < NZ + nr ? v : 0.0;
                 }
             }
@@ -797,7 +835,7 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
 #ifdef NLOT_PHASE_PROF
             { const long long t = wall_clock64(); ph[0] += t - tq; tq = t; }
 #endif
-            xsync<true>();
+            ric_sync();
             // ---- batch 2: the control columns of QE (Q_vv, Q_xv) ----
             double Qv[NV][NZ];
 #pragma unroll
@@ -921,7 +959,7 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
 #ifdef NLOT_PHASE_PROF
             { const long long t = wall_clock64(); ph[2] += t - tq; tq = t; }
 #endif
-            xsync<true>();
+            ric_sync();
             // ---- batch 3: transposed raw values (symmetrisation), gains of the terminal columns ----
             if (gc >= 0) {
                 double tr[NX];
@@ -969,12 +1007,12 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                     }
                 }
             }
-            xsync<true>();  // every read of slot k % RING is complete before the DMA refills it
+            ric_sync_reads();  // every read of slot k % RING is complete before the DMA refills it
             issue(k - RING);
 #ifdef NLOT_PHASE_PROF
             { const long long t = wall_clock64(); ph[3] += t - tq; tq = t; }
 #endif
-            xsync<true>();
+            ric_sync();
 #ifdef NLOT_PHASE_PROF
             ph[4] += wall_clock64() - tq;
 #endif
@@ -1054,11 +1092,7 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
 #pragma unroll
                     for (int c = 0; c < 3; ++c) o[a * (NZ + 2) + c] += ddw * J[a] * J[c];
                     o[a * (NZ + 2) + NZ] += J[a] * r;
-                    o[NZ * (NZ + 2) + a] += J[a] * r;
-                    if (nr > 1) {
-                        o[a * (NZ + 2) + NZ + 1] += J[a] * r;
-                        o[(NZ + 1) * (NZ + 2) + a] += J[a] * r;
-                    }
+                    if (nr > 1) o[a * (NZ + 2) + NZ + 1] += J[a] * r;
                     if (sd) {
                         o[is * (NZ + 2) + a] += ddw * J[a];
                         o[a * (NZ + 2) + is] += ddw * J[a];
@@ -1067,11 +1101,7 @@ __global__ __launch_bounds__(64) void k_ric(const NlotProblem* __restrict__ pp_,
                 if (sd) {
                     o[is * (NZ + 2) + is] += ddw;
                     o[is * (NZ + 2) + NZ] += r;
-                    o[NZ * (NZ + 2) + is] += r;
-                    if (nr > 1) {
-                        o[is * (NZ + 2) + NZ + 1] += r;
-                        o[(NZ + 1) * (NZ + 2) + is] += r;
-                    }
+                    if (nr > 1) o[is * (NZ + 2) + NZ + 1] += r;
                 }
             }
         }
@@ -1387,29 +1417,28 @@ __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ p
     }
     rank = __shfl(rank, 0);
     const int nx = dm.nx, nb = dm.nb;
+    float* dst = trial ? ws.tpts : ws.pts;
     for (int cnd = 0; cnd < ncand; ++cnd) {
-    const double al = trial ? ldexp(a0, -cnd) : 0.0;
-    const size_t base = (size_t)(rank + cnd) * dm.ppk * (dm.N + 1);
-    for (int e = lane; e < (dm.N + 1) * nb; e += 64) {
-        const int k = e / nb, i = e % nb;
-        const double x = AT(X, k * nx) + al * AT(dX, k * nx);
-        const double y = AT(X, k * nx + 1) + al * AT(dX, k * nx + 1);
-        float px, py;
-        if (p.shape == NLOT_SHAPE_DOT) {
-            px = (float)x;  // CasADi double -> fp32 (gen/nn_sdf.cpp)
-            py = (float)y;
-        } else {
-            const double th = AT(X, k * nx + 2) + al * AT(dX, k * nx + 2);
-            double sn, cs;
-            sincos(th, &sn, &cs);
-            const double bx = p.body[i][0], by = p.body[i][1];
-            px = (float)(x + cs * bx - sn * by);
-            py = (float)(y + sn * bx + cs * by);
+        const double al = trial ? ldexp(a0, -cnd) : 0.0;
+        float* o0 = dst + (size_t)(rank + cnd) * dm.ppk * (dm.N + 1) * 2;
+        for (int k = lane; k <= dm.N; k += 64) {  // lane = knot: one sincos serves the knot's nb corners
+            const double x = AT(X, k * nx) + al * AT(dX, k * nx);
+            const double y = AT(X, k * nx + 1) + al * AT(dX, k * nx + 1);
+            float* o = o0 + (size_t)k * nb * 2;
+            if (p.shape == NLOT_SHAPE_DOT) {
+                o[0] = (float)x;  // CasADi double -> fp32 (gen/nn_sdf.cpp)
+                o[1] = (float)y;
+            } else {
+                const double th = AT(X, k * nx + 2) + al * AT(dX, k * nx + 2);
+                double sn, cs;
+                sincos(th, &sn, &cs);
+                for (int i = 0; i < nb; ++i) {
+                    const double bx = p.body[i][0], by = p.body[i][1];
+                    o[2 * i] = (float)(x + cs * bx - sn * by);
+                    o[2 * i + 1] = (float)(y + sn * bx + cs * by);
+                }
+            }
         }
-        float* dst = trial ? ws.tpts : ws.pts;
-        dst[(base + e) * 2] = px;
-        dst[(base + e) * 2 + 1] = py;
-    }
     }
 }
 
@@ -1453,7 +1482,7 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
 // system of the instances in INIT; init_pass = 0: everything else (INIT instances first take their
 // least-squares multipliers from k_ric's solve).
 template <int DYN>
-__global__ __launch_bounds__(64) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
                                                const double* __restrict__ xg, int init_pass) {
     const NlotProblem& p = *pp_;
@@ -1852,7 +1881,7 @@ __global__ __launch_bounds__(64) void k_iter_a(const NlotProblem* __restrict__ p
 // affine and centering steps), recovery of the slack/bound-multiplier steps, fraction to the boundary
 // and the line-search reference values.
 template <int DYN>
-__global__ __launch_bounds__(64) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -2225,7 +2254,7 @@ __global__ __launch_bounds__(64) void k_iter_b(const NlotProblem* __restrict__ p
 }
 
 template <int DYN>
-__global__ __launch_bounds__(64) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* __restrict__ next,
                                                const double* __restrict__ x0, const double* __restrict__ xg, int nspec) {
     const NlotProblem& p = *pp_;
@@ -2500,7 +2529,9 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0, 1);
             if (ev[0]) hipEventRecord(ev[0], st);
             // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
-            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st, &reuse);
+            MlpReuse ru = reuse;
+            ru.nreused = ws.cnt + 3;  // statistics: points whose forward was reused
+            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st, &ru);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[1], st);
         }
@@ -2535,6 +2566,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         g_stats.iterations = step + 1;
         g_stats.mlp_points_full += (int64_t)hcnt[0] * P;
         g_stats.mlp_points_value += (int64_t)hcnt[1] * P;
+        g_stats.mlp_points_full_reused += (int64_t)hcnt[3];
         if (ev[0] && use_mlp) {
             float a = 0, c = 0;
             hipEventElapsedTime(&a, ev[0], ev[1]);

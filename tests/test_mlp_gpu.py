@@ -52,6 +52,43 @@ def test_mlp_matches_oracle_and_value_path(dmlp, artefact):
         np.testing.assert_allclose(h, oh, atol=5e-5 * max(1, np.abs(oh).max()))
 
 
+def test_split_bf16_is_fp32_equivalent(dmlp, golden, artefact):
+    """The 2-128-128-1 kernels run the hidden GEMM as six split-bf16 MFMA products.
+    Their error against the fp64 truth must be no larger than an fp32 evaluation's: at most twice the
+    oracle's (plain fp32 FMA chain) error plus one fp32 ulp of max|f|, for f and for grad f."""
+    import oracle as O
+    from nlotrajectories_amd.ops import sdf_mlp_eval
+
+    pts = np.asarray(golden["p"], dtype=np.float32)
+    v, g, _ = (x.cpu().numpy().astype(np.float64) for x in sdf_mlp_eval(dmlp, torch.tensor(pts, device="cuda")))
+    ov, og, _ = O.mlp_eval(O.HostMlp(artefact), pts, np.ones(len(pts), np.float32))
+    f64, g64 = golden["f_f64"], golden["grad_f64"]
+    fs, gs = np.abs(f64).max(), np.abs(g64).max()
+    assert np.abs(v - f64).max() <= 2 * np.abs(ov - f64).max() + 1.2e-7 * fs
+    assert np.abs(g - g64).max() <= 2 * np.abs(og - g64).max() + 1.2e-7 * gs
+
+
+def test_relu_mlp_128_split_bf16_vs_torch():
+    """ReLU input layer, H = 128, one hidden layer: the split-bf16 kernels' other input-layer branch.
+    A plain bf16 GEMM would miss the value tolerance by ~100x."""
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    w = MlpWeights.random_relu_mlp(hidden=128, n_hidden=1, seed=4)
+    m = w.torch_module().double()
+    pts = torch.rand(3000, 2, dtype=torch.float64) * 2 - 0.5
+    pts.requires_grad_(True)
+    f = m(pts)[:, 0]
+    (g,) = torch.autograd.grad(f.sum(), pts)
+    dm = DeviceMlp(w)
+    v, gg, hh = sdf_mlp_eval(dm, pts.detach().float().cuda())
+    vv, _, _ = sdf_mlp_eval(dm, pts.detach().float().cuda(), derivatives=False)
+    np.testing.assert_array_equal(vv.cpu().numpy(), v.cpu().numpy())
+    np.testing.assert_allclose(v.cpu().numpy(), f.detach().numpy(), atol=1e-5 * max(1, f.abs().max().item()))
+    np.testing.assert_allclose(gg.cpu().numpy(), g.numpy(), atol=1e-4 * max(1, g.abs().max().item()))
+    assert float(hh.abs().max()) == 0.0
+
+
 def test_mlp_relu_two_layer_vs_torch():
     """l4casadi naive MLP (ReLU input layer, 2 hidden layers): value & grad vs torch fp64; hess = 0."""
     from nlotrajectories_amd.nn import MlpWeights
