@@ -408,16 +408,20 @@ __device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int co
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// one weight image per CU: FULL (value + reverse sweep) runs 8 waves = 2 per SIMD; value-only launches
-// NLOT_MLP_VALUE_THREADS / 256 waves per SIMD
+// one weight image per CU, shared by NLOT_MLP_*_THREADS / 256 waves per SIMD: value-only launches 3 (162
+// VGPRs); FULL (value + reverse sweep) 1, with the whole 512-register file (at 2 per SIMD it spills
+// ~440 B/lane and ran 3 % slower in the solve, profiles/r01/variants_v14.log)
 #ifndef NLOT_MLP_VALUE_THREADS
-#define NLOT_MLP_VALUE_THREADS 512
+#define NLOT_MLP_VALUE_THREADS 768
 #endif
-__host__ __device__ constexpr int bf16_threads(bool full) { return full ? 512 : NLOT_MLP_VALUE_THREADS; }
+#ifndef NLOT_MLP_FULL_THREADS
+#define NLOT_MLP_FULL_THREADS 256
+#endif
+__host__ __device__ constexpr int bf16_threads(bool full) { return full ? NLOT_MLP_FULL_THREADS : NLOT_MLP_VALUE_THREADS; }
 
 template <int H>
 __host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
-    return (size_t)3 * H * (H + 8) * 2 + (size_t)8 * H * 4;
+    return (size_t)3 * H * (H + 8) * 2 + (size_t)5 * H * 4;
 }
 
 template <int H, bool FULL>
@@ -434,9 +438,6 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     float* sb0 = sA1 + H;
     float* sb = sb0 + H;
     float* sw = sb + H;
-    float* sAxx = sw + H;  // a_x^2, a_x a_y, a_y^2 of the input layer (Hessian contraction)
-    float* sAxy = sAxx + H;
-    float* sAyy = sAxy + H;
     __shared__ int s_reused;
     for (int idx = threadIdx.x; idx < 3 * H * H / 8; idx += blockDim.x) {  // 16-byte chunks of the planes
         const int pr = idx / (H / 8), c8 = idx % (H / 8);                   // pr = plane * H + row
@@ -448,9 +449,6 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
         sb0[idx] = w.b0[idx];
         sb[idx] = w.b[idx];
         sw[idx] = w.w_out[idx];
-        sAxx[idx] = w.A[idx] * w.A[idx];
-        sAxy[idx] = w.A[idx] * w.A[H + idx];
-        sAyy[idx] = w.A[H + idx] * w.A[H + idx];
     }
     if (threadIdx.x == 0) s_reused = 0;
     __syncthreads();
@@ -597,18 +595,13 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                     const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
                     const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
                     const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
-                    const float4 XX = *reinterpret_cast<const float4*>(sAxx + k0);
-                    const float4 XY = *reinterpret_cast<const float4*>(sAxy + k0);
-                    const float4 YY = *reinterpret_cast<const float4*>(sAyy + k0);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int r = 4 * r4 + rr;
                     const float ax = rr == 0 ? A0.x : rr == 1 ? A0.y : rr == 2 ? A0.z : A0.w;
                     const float ay = rr == 0 ? A1.x : rr == 1 ? A1.y : rr == 2 ? A1.z : A1.w;
                     const float bz = rr == 0 ? B0.x : rr == 1 ? B0.y : rr == 2 ? B0.z : B0.w;
-                    const float axx = rr == 0 ? XX.x : rr == 1 ? XX.y : rr == 2 ? XX.z : XX.w;
-                    const float axy = rr == 0 ? XY.x : rr == 1 ? XY.y : rr == 2 ? XY.z : XY.w;
-                    const float ayy = rr == 0 ? YY.x : rr == 1 ? YY.y : rr == 2 ? YY.z : YY.w;
+                    const float axx = ax * ax, axy = ax * ay, ayy = ay * ay;
                     const float z = fmaf(py, ay, px * ax) + bz;
                     const float d = g[t][r];
                     float dz, c2;

@@ -41,20 +41,24 @@ enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3 };
 // Minimum waves per SIMD the per-instance kernels are compiled for (register budget 512 / w per lane),
 // and the depth of k_ric's stage ring (its LDS per wavefront sets k_ric's occupancy).  These kernels wait
 // on memory most of their cycles (SQ_WAIT_ANY 56-73 %), so residency is speed.
+// Defaults: the best of each knob measured alone at B = 65536 (profiles/r01/variants_v14.log).
 #ifndef NLOT_WPE_A
-#define NLOT_WPE_A 1
+#define NLOT_WPE_A 2
 #endif
 #ifndef NLOT_WPE_B
-#define NLOT_WPE_B 1
+#define NLOT_WPE_B 2
 #endif
 #ifndef NLOT_WPE_ACC
-#define NLOT_WPE_ACC 2
+#define NLOT_WPE_ACC 3
 #endif
 #ifndef NLOT_WPE_RIC
 #define NLOT_WPE_RIC 1
 #endif
 #ifndef NLOT_RIC_RING
-#define NLOT_RIC_RING 4
+#define NLOT_RIC_RING 2
+#endif
+#if !defined(NLOT_RIC_FENCED) && !defined(NLOT_RIC_INORDER)
+#define NLOT_RIC_INORDER
 #endif
 enum Scal {
     SC_MU, SC_TAU, SC_DWLAST, SC_THMAX, SC_THMIN, SC_ALPHA, SC_AMAX, SC_AMIN, SC_AZ, SC_THETA, SC_PHI, SC_GD,
@@ -656,9 +660,10 @@ struct RicG {
 };
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-// k_ric's LDS hand-offs between the lanes of its single wavefront.  NLOT_RIC_INORDER relies on the LDS
-// unit executing one wavefront's DS instructions in issue order (a ds_read issued after a ds_write sees
-// it), so only the compiler's order is pinned; the default waits for the LDS queue and barriers.
+// k_ric's LDS hand-offs between the lanes of its single wavefront.  NLOT_RIC_INORDER (the default) relies
+// on the LDS unit executing one wavefront's DS instructions in issue order (a ds_read issued after a
+// ds_write sees it), so only the compiler's order is pinned; NLOT_RIC_FENCED waits for the LDS queue and
+// barriers instead (same results, measured slower).
 __device__ __forceinline__ void ric_sync() {
 #ifdef NLOT_RIC_INORDER
     asm volatile("" ::: "memory");
