@@ -140,11 +140,14 @@ struct Ws {
 #undef NLOT_DECL
     float* pts;  // compacted corner list, rank-major [rank][P][2]
     float* mo;   // MLP outputs [6][cap * P] (rank-major within a plane)
-    float* tpts;      // trial corner list [slot][P][2] (slot = rank + candidate), cap * NSPEC slots
-    float* tval;      // its values [slot][P]
-    uint32_t* tmask;  // its hidden-layer ReLU patterns [4][slot][P]
-    int* tsrc;        // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
-    int* cnt;    // [0] eval instances, [1] trial instances, [2] next active count, [3] reused forwards
+    // trial lists by global-step parity q: the full launch of step s + 1 reuses step s's accepted
+    // candidate while k_accept of step s already emits the candidates of step s + 1
+    float* tpts[2];      // trial corner list [slot][P][2] (slot = rank + candidate), cap * NSPEC slots
+    float* tval[2];      // its values [slot][P]
+    uint32_t* tmask[2];  // its hidden-layer ReLU patterns [4][slot][P]
+    int* tsrc;           // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
+    int* cnt;  // counters of step parity q at cnt + 8 q: [0] evaluation ranks, [1] trial slots, [2] next active
+               // count, [3] full-launch points whose forward was reused
     int* act[2]; // active instance lists (ping-pong)
     int64_t cap;
     int ppk;
@@ -172,9 +175,9 @@ static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
         const size_t P = (size_t)d.ppk * (d.N + 1);
         b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
         b += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
-        b += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));  // tpts
-        b += align256(P * (size_t)B * NSPEC * sizeof(float));      // tval
-        b += align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));  // tmask
+        b += 2 * align256(P * (size_t)B * NSPEC * 2 * sizeof(float));     // tpts, per step parity
+        b += 2 * align256(P * (size_t)B * NSPEC * sizeof(float));         // tval
+        b += 2 * align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));  // tmask
         b += align256((size_t)B * sizeof(int));                    // tsrc
     }
     b += align256(2 * (size_t)B * sizeof(int));
@@ -202,12 +205,14 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
         c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
         w.mo = (float*)c;
         c += align256(6 * P * (size_t)B * NSPEC * sizeof(float));
-        w.tpts = (float*)c;
-        c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
-        w.tval = (float*)c;
-        c += align256(P * (size_t)B * NSPEC * sizeof(float));
-        w.tmask = (uint32_t*)c;
-        c += align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));
+        for (int q = 0; q < 2; ++q) {
+            w.tpts[q] = (float*)c;
+            c += align256(P * (size_t)B * NSPEC * 2 * sizeof(float));
+            w.tval[q] = (float*)c;
+            c += align256(P * (size_t)B * NSPEC * sizeof(float));
+            w.tmask[q] = (uint32_t*)c;
+            c += align256(4 * P * (size_t)B * NSPEC * sizeof(uint32_t));
+        }
         w.tsrc = (int*)c;
         c += align256((size_t)B * sizeof(int));
     }
@@ -263,11 +268,11 @@ __device__ __forceinline__ void xsync() {
 // per-corner SDF: learned (MLP output of this step's compacted list) or analytic
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int rank, int pidx, double cx, double cy,
-                                         bool trial = false) {
+                                         const float* tval = nullptr) {
     if (p.sdf_kind == NLOT_SDF_ANALYTIC) return sdf_scene(p, cx, cy, true);
-    if (trial) {  // value launch of the trial list (slot = rank)
+    if (tval) {  // value launch of this step's trial list (slot = rank)
         HD h{};
-        h.v = ws.tval[(int64_t)rank * ws.ppk * (p.N + 1) + pidx];
+        h.v = tval[(int64_t)rank * ws.ppk * (p.N + 1) + pidx];
         return h;
     }
     // MLP outputs of this step's compacted list, rank-major: quantity q of point pidx of the
@@ -289,10 +294,10 @@ __device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int
 // (slack excluded), pose gradients g[j][3], and Hw = sum_j w[j] d2 d_j / dpose2 (if w != null).
 __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
                                  const double* xk, double* d, double (*g)[3], const double* w, double* Hw,
-                                 bool trial = false) {
+                                 const float* tval = nullptr) {
     const double x = xk[0], y = xk[1];
     if (p.shape == NLOT_SHAPE_DOT) {
-        HD f = corner_sdf(p, ws, rank, k, x, y, trial);
+        HD f = corner_sdf(p, ws, rank, k, x, y, tval);
         d[0] = f.v;
         if (g) { g[0][0] = f.gx; g[0][1] = f.gy; g[0][2] = 0; }
         if (Hw) {
@@ -310,7 +315,7 @@ __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, 
         const double bx = p.body[i][0], by = p.body[i][1];
         const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
         const double ex = -(cy - y), ey = cx - x;                            // d c / d theta
-        HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, trial);
+        HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, tval);
         phi[i] = f.v;
         gp[i][0] = f.gx;
         gp[i][1] = f.gy;
@@ -1382,14 +1387,10 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
     }
 }
 
-// number of step lengths evaluated in this line-search round: alpha_max alone in the first round,
-// afterwards the next NSPEC halvings that stay >= alpha_min (speculative backtracking: the same
-// accepted alpha as sequential halving, because the acceptance test of one candidate does not
-// depend on the others)
-__device__ __forceinline__ int n_candidates(const Ws& ws, int b, int nspec) {
-    if (SC(SC_TRIALS) == 0) return 1;
-    const double amin = SC(SC_AMIN);
-    double a = SC(SC_ALPHA);
+// number of step lengths of a later line-search round starting at alpha a: a, a/2, ... while >= alpha_min,
+// at most nspec (speculative backtracking: the same accepted alpha as sequential halving, because the
+// acceptance test of one candidate does not depend on the others; the first round tries alpha_max alone)
+__device__ __forceinline__ int n_later(double a, double amin, int nspec) {
     int n = 1;
     for (int j = 1; j < nspec; ++j) {
         a *= 0.5;
@@ -1399,34 +1400,32 @@ __device__ __forceinline__ int n_candidates(const Ws& ws, int b, int nspec) {
     return n;
 }
 
-// corners of X (+ alpha dX) of instances in the wanted phase, appended to the compacted point list
-// nspec: step lengths per line-search round (host-chosen per global step; the accepted alpha does not
-// depend on it, only the number of rounds)
-__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, const int* __restrict__ active, int trial, int nspec) {
-    const NlotProblem& p = *pp_;
-    const Dims& dm = *dd_;
-    const int b = active[blockIdx.x], lane = threadIdx.x;
-    const int ph = (int)SC(SC_PHASE);
-    const bool want = trial ? ph == PH_LS : (ph == PH_INIT || ph == PH_EVAL);
-    if (!want) return;
-    // trial: the first round evaluates alpha_max; later rounds the next NSPEC halvings that stay
-    // >= alpha_min (speculative backtracking, identical outcome to sequential halving)
-    const int ncand = trial ? n_candidates(ws, b, nspec) : 1;
-    const double a0 = trial ? SC(SC_ALPHA) : 0.0;
+// Corners of X + a_c dX (a_c = a0 2^-c, c < ncand) of instance b, appended to a compacted point list:
+// the evaluation list pts (!trial; a0 = 0, ncand = 1) or the trial list tp.  Without a learned SDF there
+// are no lists: only the candidate count is recorded.  cnt: the counters of
+// the global step that evaluates them.  Called with uniform arguments by the kernel that moves the
+// instance into the phase needing them: k_iter_b (first line-search round), k_accept (accepted: the new
+// iterate; rejected: the next round), k_points (first step).  Lane = knot: one sincos per knot.
+__device__ void emit_points(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int* cnt,
+                            bool trial, float* tp, int ncand, double a0) {
+    if (!ws.pts) {
+        if (lane == 0) SC(SC_NCAND) = ncand;
+        return;
+    }
     int rank = 0;
     if (lane == 0) {
-        rank = atomicAdd(&ws.cnt[trial ? 1 : 0], ncand);
+        rank = atomicAdd(&cnt[trial ? 1 : 0], ncand);
         SC(SC_RANK) = rank;
         SC(SC_NCAND) = ncand;
         if (!trial && ws.tsrc) ws.tsrc[rank] = (int)SC(SC_ACCSLOT);
     }
     rank = __shfl(rank, 0);
     const int nx = dm.nx, nb = dm.nb;
-    float* dst = trial ? ws.tpts : ws.pts;
+    float* dst = trial ? tp : ws.pts;
     for (int cnd = 0; cnd < ncand; ++cnd) {
         const double al = trial ? ldexp(a0, -cnd) : 0.0;
         float* o0 = dst + (size_t)(rank + cnd) * dm.ppk * (dm.N + 1) * 2;
-        for (int k = lane; k <= dm.N; k += 64) {  // lane = knot: one sincos serves the knot's nb corners
+        for (int k = lane; k <= dm.N; k += 64) {
             const double x = AT(X, k * nx) + al * AT(dX, k * nx);
             const double y = AT(X, k * nx + 1) + al * AT(dX, k * nx + 1);
             float* o = o0 + (size_t)k * nb * 2;
@@ -1445,6 +1444,15 @@ __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ p
             }
         }
     }
+}
+
+// first global step: the corners of every instance (phase INIT)
+__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+                                               const Ws* __restrict__ ws_, const int* __restrict__ active, int* cnt) {
+    const Ws& ws = *ws_;
+    const int b = active[blockIdx.x];
+    if ((int)SC(SC_PHASE) != PH_INIT) return;
+    emit_points(*pp_, *dd_, ws, b, threadIdx.x, cnt, false, nullptr, 1, 0.0);
 }
 
 __device__ inline double frac_to_bound(double sl, double dsl, double tau, double amax) {
@@ -1887,7 +1895,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
 // and the line-search reference values.
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
-                                               const int* __restrict__ active) {
+                                               const int* __restrict__ active, int* cnt, float* tp) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -2256,12 +2264,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         SC(SC_TRIALS) = 0;
         SC(SC_PHASE) = PH_LS;
     }
+    // the first line-search round: alpha_max alone
+    wsync();  // dX complete
+    emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, amax);
 }
 
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* __restrict__ next,
-                                               const double* __restrict__ x0, const double* __restrict__ xg, int nspec) {
+                                               const double* __restrict__ x0, const double* __restrict__ xg, int* cnt,
+                                               int* cnt_next, float* tp_next, const float* tval, int nspec_next) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -2271,7 +2283,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
     if (ph == PH_LS) {
         const int N = dm.N, M = dm.M, nc = dm.nc;
         const double a0 = SC(SC_ALPHA), mu = SC(SC_MU);
-        const int rank0 = (int)SC(SC_RANK), ncand = n_candidates(ws, b, nspec);  // same count as k_points
+        const int rank0 = (int)SC(SC_RANK), ncand = (int)SC(SC_NCAND);  // as emitted
         int ok = 0, ftype = 0, armijo = 0, cnd = 0;
         double al = a0, th = 0, pht = 0;
         const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
@@ -2306,7 +2318,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                 for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
             }
             double d[MMAX];
-            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, true);
+            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
             const double sk = AT(S, k) + al * AT(dS, k);
             for (int j = 0; j < M; ++j) {
                 const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
@@ -2404,6 +2416,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                 SC(SC_PHASE) = PH_EVAL;
                 SC(SC_ACCSLOT) = rank0 + cnd - 1;  // the loop stepped past the accepted candidate
             }
+            // corners of the new iterate, for the next step's full launch
+            wsync();  // X complete
+            emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
         } else {
             const double na = ldexp(a0, -ncand);
             if (na < SC(SC_AMIN)) {
@@ -2412,13 +2427,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     SC(SC_STATUS) = NLOT_LS_FAILED;
                     SC(SC_PHASE) = PH_DONE;
                 }
-            } else if (lane == 0) {
-                SC(SC_ALPHA) = na;
-                SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
+            } else {
+                if (lane == 0) {
+                    SC(SC_ALPHA) = na;
+                    SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
+                }
+                emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
             }
         }
     }
-    if (ph != PH_DONE && lane == 0) next[atomicAdd(&ws.cnt[2], 1)] = b;
+    if (ph != PH_DONE && lane == 0) next[atomicAdd(&cnt[2], 1)] = b;
 }
 
 __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
@@ -2504,20 +2522,23 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (g_timing)
         for (auto& e : ev) hipEventCreate(&e);
-    MlpOut mo{}, mo_t{};
-    MlpReuse reuse{};
+    MlpOut mo{}, mo_t[2] = {};
+    MlpReuse reuse[2] = {};
     if (use_mlp) {
         const int64_t plane = P * B * NSPEC;
         mo.val = ws.mo; mo.gx = ws.mo + plane; mo.gy = ws.mo + 2 * plane; mo.hxx = ws.mo + 3 * plane;
         mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
         mo.sv = mo.sg = mo.sh = 1;
-        // trial list: values + ReLU patterns, reused by the next full launch at the accepted point
-        mo_t.val = ws.tval;
-        mo_t.sv = 1;
-        mo_t.mask = ws.tmask;
-        mo_t.mask_plane = P * B * NSPEC;
+        // trial lists (by step parity): values + ReLU patterns, reused by the next full launch at the
+        // accepted point
         static const bool no_reuse = getenv("NLOT_MLP_REUSE") && strcmp(getenv("NLOT_MLP_REUSE"), "0") == 0;
-        reuse = MlpReuse{no_reuse ? nullptr : ws.tsrc, ws.tpts, ws.tval, ws.tmask, P * B * NSPEC};
+        for (int q = 0; q < 2; ++q) {
+            mo_t[q].val = ws.tval[q];
+            mo_t[q].sv = 1;
+            mo_t[q].mask = ws.tmask[q];
+            mo_t[q].mask_plane = plane;
+            reuse[q] = MlpReuse{no_reuse ? nullptr : ws.tsrc, ws.tpts[q], ws.tval[q], ws.tmask[q], plane, nullptr};
+        }
     }
     g_stats.slots_in_lds = 0;  // stage slots live in the HBM workspace; k_ric stages them through LDS
     const int ric_blocks_per = RicG<DYN>::IPW;
@@ -2526,23 +2547,30 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
     const int max_steps = (o.max_iter + 2) * 64;
     int rc = NLOT_OK, n_active = Bi, cur = 0;
+    NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 16 * sizeof(int), st));
     for (int step = 0; step < max_steps && n_active > 0; ++step) {
         const int* act = ws.act[cur];
         int* nxt = ws.act[cur ^ 1];
-        NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 4 * sizeof(int), st));
-        if (use_mlp) {
-            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 0, 1);
-            if (ev[0]) hipEventRecord(ev[0], st);
-            // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
-            MlpReuse ru = reuse;
-            ru.nreused = ws.cnt + 3;  // statistics: points whose forward was reused
-            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, ws.cnt + 0, (int)P, 0, nullptr, mo, true, st, &ru);
-            if (rc) break;
-            if (ev[0]) hipEventRecord(ev[1], st);
-        }
+        // Point lists are appended to by the kernel that moves an instance into the phase needing them
+        // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
+        // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
+        const int q = step & 1;
+        int* C = ws.cnt + 8 * q;
+        int* Cn = ws.cnt + 8 * (q ^ 1);
+        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, 8 * sizeof(int), st));
         // speculative backtracking only while the GPU is latency-bound (few active instances); in the
         // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
+        if (use_mlp) {
+            if (step == 0) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
+            if (ev[0]) hipEventRecord(ev[0], st);
+            // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
+            MlpReuse ru = reuse[q ^ 1];  // the previous step's trial list
+            ru.nreused = C + 3;          // statistics: points whose forward was reused
+            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, C + 0, (int)P, 0, nullptr, mo, true, st, &ru);
+            if (rc) break;
+            if (ev[0]) hipEventRecord(ev[1], st);
+        }
         if (ev[4]) hipEventRecord(ev[4], st);
         if (step == 0) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
             hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1);
@@ -2552,21 +2580,24 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0);
         hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st, dP, dD,
                            dW, act, n_active, (int)MODE_NEWTON);
-        hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act);
+        hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
+                           use_mlp ? ws.tpts[q] : nullptr);
         if (ev[4]) hipEventRecord(ev[5], st);
         if (use_mlp) {
-            hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, ws, act, 1, nspec);
             if (ev[0]) hipEventRecord(ev[2], st);
-            rc = launch_mlp_strided(mlp->dev, ws.tpts, (int64_t)n_active * NSPEC, ws.cnt + 1, (int)P, 0, nullptr, mo_t,
-                                    false, st);
+            rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
+                                    mo_t[q], false, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[3], st);
             g_stats.mlp_full_launches++;
             g_stats.mlp_value_launches++;
         }
-        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, nspec);
+        // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
+        // starts at most one step late; the accepted alpha is the same either way)
+        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, C, Cn,
+                           use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
-        NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, ws.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+        NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, C, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         g_stats.iterations = step + 1;
         g_stats.mlp_points_full += (int64_t)hcnt[0] * P;
