@@ -3,25 +3,26 @@
 // restatement of IPOPT's primal-dual filter line-search algorithm (runner.py:113-133)
 // whose Newton systems are solved by a stage-wise Riccati recursion.
 //
-// MI355X mapping: ONE WAVEFRONT PER INSTANCE.
-//   * lanes over knots for everything that is per knot (SDF chain rule + soft-min, dynamics and their
-//     derivatives, condensed stage matrices, residuals, optimality measures); scalars of the
-//     algorithm come from wave reductions (shuffles), broadcast from lane 0 so every lane takes the
-//     same branch;
-//   * the Riccati recursion is sequential in the knot index: lanes go over the entries of the small
-//     stage matrices (P, [A B]'P[A B], gains), with the recursion state in LDS;
-//   * per-instance arrays are instance-major (a wave touches one contiguous block), the stage
-//     matrices of one Newton solve live in a per-instance scratch (L2-resident between passes);
+// MI355X mapping: ONE WAVEFRONT PER INSTANCE, except the Riccati solve.
+//   * k_iter_a / k_iter_b / k_accept: lanes over knots for everything that is per knot (SDF chain rule +
+//     soft-min, dynamics and their derivatives, condensed stage matrices, residuals, optimality
+//     measures); scalars of the algorithm come from wave reductions (shuffles), broadcast from lane 0 so
+//     every lane takes the same branch;
+//   * k_ric: 16 lanes per instance (one per column of the extended stage matrix), 4 instances per
+//     wavefront; the recursion is sequential in the knot index, stage inputs arrive by global->LDS DMA;
+//   * per-instance arrays are instance-major (a wave touches one contiguous block);
 //   * the learned-SDF corner points of all instances that need them in a step are compacted
 //     (rank-major) into one list and evaluated by the MFMA kernel (nlot_mlp.hip) in a single launch;
+//     the kernel that moves an instance into a phase appends the points that phase needs;
 //   * the host launches only the still-active instances (active list rebuilt every step).
 //
 // Per-instance phase machine (one global step = one launch of each kernel):
-//   INIT -> [corners, MLP full, k_iterate: slack push, least-squares multipliers, then EVAL work]
-//   EVAL -> [corners, MLP full, k_iterate: evaluate, converge?, mu update, inertia-corrected
-//            Newton step, step bounds]                                              -> LS
-//   LS   -> [trial corners, MLP value, k_accept: filter test at alpha; accept -> EVAL,
-//            reject -> alpha/2 (next step), alpha < alpha_min -> DONE(LS_FAILED)]
+//   INIT -> [corners (k_points), MLP full, k_iter_a: slack push, least-squares multipliers (k_ric), then
+//            the EVAL work]
+//   EVAL -> [MLP full, k_iter_a: evaluate, converge?, mu update, stage matrices; k_ric: inertia-corrected
+//            Newton step; k_iter_b: sigma choice, step bounds, first trial corners]          -> LS
+//   LS   -> [MLP value, k_accept: filter test at the candidates; accept -> EVAL (new corners),
+//            reject -> next halvings (next step), alpha < alpha_min -> DONE(LS_FAILED)]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
