@@ -49,11 +49,42 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step (SURVEY.md §8d config 3: 1024 / 16384 / 65536)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=48, help="instances for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="instances for the CPU baseline on all threads (0 = skip)")
+    ap.add_argument("--cpu-sample-1core", type=int, default=8, help="instances for the single-core CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
     return ap.parse_args()
+
+
+def timed_loop(step, steps, warmup, world, sync, device):
+    """W untimed warm-up steps, then EXACTLY `steps` timed steps bracketed by a barrier + device sync on
+    both sides; returns (per-step results, max-over-ranks elapsed seconds)."""
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    out = [step() for _ in range(steps)]
+    sync()
+    if world > 1:
+        dist.barrier()
+    return out, max_over_ranks(time.perf_counter() - t0, device)
+
+
+def ric_bytes_per_solve(prob, nr=2):
+    """Algorithmic HBM bytes of one instance's Newton solve in k_ric, from the stage layouts
+    of nlot_solver.hip: per knot it reads hg = [H | g0 g1] and [A B 0 | c] | M once, writes the gains
+    [K | k0 k1 | Kn] and the value function [P | p0 p1 | Gamma] and reads them back in the forward sweep,
+    and writes the step (dx, du, ds, y) of each of the nr right-hand sides."""
+    nx, nu = prob.nx, prob.nu
+    nz, nv, nc = nx + nu + 1, nu + 1, nx
+    nab = (nx + nu + 3) & ~1
+    ncol = nx + 2 + nc
+    hg, abm, gains, vf = nz * (nz + 2), nx * nab + 4, ncol * nv, nx * ncol
+    per_knot = hg + abm + 2 * (gains + vf) + nr * (nx + nu + 1 + nx)
+    return 8 * (prob.N + 1) * per_knot
 
 
 def main():
@@ -77,50 +108,54 @@ def main():
     xg = torch.tensor(xg, dtype=torch.float64, device=dev)
     opt = _abi.default_options() if a.mu_strategy == "adaptive" else \
         _abi.default_options(mu_strategy=0, barrier_tol_factor=10.0)
-    ws = None
-
-    def step():
-        r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws)
-        solved = (r["status"] == 0)
-        if world > 1:  # gather the solutions to every rank (RCCL over xGMI): the only collective
-            gather_solutions(r, keys=("X", "U", "cost", "status"))
-        return r, int(solved.sum().item())
 
     from nlotrajectories_amd.solver import workspace_bytes
 
     ws = torch.empty(workspace_bytes(prob, a.batch), dtype=torch.uint8, device=dev)
-    for _ in range(a.warmup):
-        step()
-    set_timing(True)
-    agg = dict(mlp_full_ms=0.0, mlp_full_launches=0, mlp_points_full=0, mlp_value_ms=0.0,
-               mlp_value_launches=0, mlp_points_value=0, iterations=0, iterate_ms=0.0,
-               mlp_points_full_reused=0)
-    slots_in_lds = None
-    iters_all, solved_total = [], 0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        r, ns = step()
-        solved_total += ns
-        st = last_stats()
-        for k in agg:
-            agg[k] += st[k]
-        slots_in_lds = bool(st["slots_in_lds"])
-        iters_all.append(r["iters"][r["status"] == 0].float().mean().item() if ns else 0.0)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    set_timing(False)
-    status_counts = torch.bincount(r["status"].long(), minlength=4).cpu().numpy().tolist()
-    elapsed = max_over_ranks(elapsed, dev)
-    solved_total = sum_over_ranks(solved_total, dev)
+    agg_keys = ("mlp_full_ms", "mlp_full_launches", "mlp_points_full", "mlp_value_ms", "mlp_value_launches",
+                "mlp_points_value", "iterations", "iterate_ms", "mlp_points_full_reused", "ric_ms", "ric_launches",
+                "ric_solves")
+    agg = {k: 0 for k in agg_keys}
+    timing = {"on": False}
 
-    # roofline of the dominant MFMA kernel: the full (value + gradient + Hessian) SDF-MLP launch.  FLOP are
-    # counted as executed: the reverse sweep at every point, the forward only where the launch did not take
-    # it from the accepted trial point's value launch (forward reuse)
+    def step():
+        r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws)
+        if timing["on"]:
+            st = last_stats()
+            for k in agg:
+                agg[k] += st[k]
+        if world > 1:  # gather the solutions to rank 0 (RCCL over xGMI): the only collective
+            gather_solutions(r, keys=("X", "U", "cost", "status"))
+        return r
+
+    def sync():
+        torch.cuda.synchronize()
+        timing["on"] = not timing["on"]  # hipEvent timing inside the timed steps only
+        set_timing(timing["on"])
+
+    results, elapsed = timed_loop(step, a.steps, a.warmup, world, sync, dev)
+    set_timing(False)
+    r = results[-1]
+    solved_total = sum_over_ranks(sum(int((x["status"] == 0).sum().item()) for x in results), dev)
+    iters_solved = [x["iters"][x["status"] == 0].float().mean().item() for x in results if (x["status"] == 0).any()]
+    status_counts = torch.bincount(r["status"].long(), minlength=4).cpu().numpy().tolist()
+
+    # rooflines.  Dominant kernel by device time: k_ric (the Newton solve, latency/occupancy-bound fp64 with
+    # ~2.8 KB of stage data per knot): HBM roofline on its algorithmic bytes.  The two SDF-MLP launches:
+    # split-bf16 MFMA roofline on executed FLOP.
+    n_r = max(agg["ric_launches"], 1)
+    ric_avg_ms = agg["ric_ms"] / n_r
+    ric_solves_per_launch = agg["ric_solves"] / n_r
+    ric_bytes = ric_bytes_per_solve(prob)
+    ric_achieved = ric_solves_per_launch * ric_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
+    ric_traffic = None
+    tf = os.path.join(ROOT, "profiles", "r02", "kric_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            per_solve = json.load(f).get("hbm_bytes_per_solve")
+        if per_solve is not None:
+            ric_traffic = per_solve * ric_solves_per_launch
+
     flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1
     flop_fwd = w.flops_per_point_fwd      # 33,536
     n_l = max(agg["mlp_full_launches"], 1)
@@ -135,13 +170,17 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch_per_point")
             if traffic is not None:
                 traffic = traffic * agg["mlp_points_full"] / n_l
+    n_v = max(agg["mlp_value_launches"], 1)
+    v_avg_ms = agg["mlp_value_ms"] / n_v
+    v_achieved = agg["mlp_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu = cpu_baseline(prob, w, x0.cpu().numpy()[: a.cpu_sample], xg.cpu().numpy()[: a.cpu_sample],
+        cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
                            a.cpu_threads, opt)
 
     if rank == 0:
+        B_all = a.batch * world
         line = {
             "metric": "solved trajectories/sec (50-knot unicycle+learned-SDF)",
             "value": solved_total / elapsed,
@@ -161,18 +200,34 @@ def main():
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
                 "mu_strategy": a.mu_strategy,
                 "instances_per_gpu": a.batch,
-                "global_batch": a.batch * world,
+                "global_batch": B_all,
                 "knots": prob.N + 1,
-                "parallelism": f"instances sharded over {world} GPU(s); RCCL all_gather of solutions",
+                "parallelism": f"instances sharded over {world} GPU(s); RCCL gather of solutions to rank 0",
                 "solved_per_step_rank0": int((r["status"] == 0).sum().item()),
                 "status_counts_rank0": status_counts,
-                "mean_iters_solved": float(np.mean(iters_all)),
+                "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / a.batch for i, c in enumerate(status_counts[:4])},
+                "mean_iters_solved": float(np.mean(iters_solved)) if iters_solved else 0.0,
                 "lockstep_global_steps": agg["iterations"] // max(a.steps, 1),
                 "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
+                "ric_ms_per_step": agg["ric_ms"] / max(a.steps, 1),
                 "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) / max(a.steps, 1),
-                "riccati_slots": "lds" if slots_in_lds else "hbm",
             },
             "roofline": {
+                "kernel": "k_ric (lane-group Riccati Newton solve, fp64; dominant kernel by device time)",
+                "bound": "hbm",
+                "achieved": ric_achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": ric_achieved / PEAK_HBM_GBS,
+                "traffic": ric_traffic,
+                "bytes_per_solve": ric_bytes,
+                "solves_per_launch": ric_solves_per_launch,
+                "avg_launch_ms": ric_avg_ms,
+                "launches": agg["ric_launches"],
+                "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
+                        "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline",
+            },
+            "roofline_mlp_full": {
                 "kernel": "mlp_bf16<128,full> (SDF-MLP value+grad+Hessian; fp32-equivalent products as 6 split "
                           "v_mfma_f32_32x32x16_bf16)",
                 "bound": "mfma",
@@ -190,6 +245,18 @@ def main():
                 "avg_launch_ms": avg_ms,
                 "launches": agg["mlp_full_launches"],
             },
+            "roofline_mlp_value": {
+                "kernel": "mlp_bf16<128,value> (line-search trial points, value only)",
+                "bound": "mfma",
+                "achieved": v_achieved,
+                "peak": PEAK_SPLIT_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": v_achieved / PEAK_SPLIT_TFLOPS,
+                "flop_per_point": flop_fwd,
+                "points_per_launch": agg["mlp_points_value"] / n_v,
+                "avg_launch_ms": v_avg_ms,
+                "launches": agg["mlp_value_launches"],
+            },
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
@@ -197,22 +264,37 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(prob, w, x0, xg, threads, opt):
-    """The oracle (C restatement, OpenMP over instances) on a bounded sample of the same workload."""
+def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt):
+    """The oracle (C restatement, OpenMP over instances) on bounded samples of the same workload: the first
+    n_all instances of rank 0's batch on `threads` host threads, and the first n_one on one thread."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    threads = max(1, min(threads, avail))
     hm = O.HostMlp(w)
-    t = time.perf_counter()
-    r = O.solve_batch(prob, x0, xg, hm, opt=opt, threads=threads)
-    dt = time.perf_counter() - t
-    ns = int((r["status"] == 0).sum())
-    return {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
-            "sample": f"{len(x0)} instances of the same seeded workload (first of rank 0's batch), "
-                      f"{ns} solved in {dt:.1f} s on {threads} OpenMP threads"}
+
+    def run(n, th):
+        t = time.perf_counter()
+        r = O.solve_batch(prob, x0[:n], xg[:n], hm, opt=opt, threads=th)
+        dt = time.perf_counter() - t
+        return int((r["status"] == 0).sum()), dt, np.bincount(r["status"], minlength=4).tolist()
+
+    ns, dt, sc = run(n_all, threads)
+    out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
+           "sample": f"first {n_all} instances of rank 0's seeded batch: {ns} solved (status counts {sc}) in "
+                     f"{dt:.1f} s on {threads} OpenMP threads (host: os.cpu_count() = {os.cpu_count()}, "
+                     f"affinity = {avail} CPUs; the box's CPU share is 16)"}
+    if n_one > 0:
+        ns1, dt1, _ = run(n_one, 1)
+        out["single_core"] = {"value": ns1 / dt1, "cores": 1,
+                              "sample": f"first {n_one} instances: {ns1} solved in {dt1:.1f} s on 1 thread"}
+    return out
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 3
+#define NLOT_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -203,6 +203,10 @@ typedef struct NlotSolveStats {
     int32_t slots_in_lds;      /* 1: Riccati stage slots held in LDS, 0: in the HBM workspace */
     int32_t pad_;
     int64_t mlp_points_full_reused; /* full-launch points whose forward came from the accepted trial point */
+    double ric_ms;             /* summed device time of the Newton-solve (k_ric) launches (hipEvents) */
+    int32_t ric_launches;
+    int32_t pad2_;
+    int64_t ric_solves;        /* instance Newton solves those launches performed */
 } NlotSolveStats;
 /* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
 void nlot_set_timing(int32_t enabled);

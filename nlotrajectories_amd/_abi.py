@@ -60,7 +60,8 @@ class NlotSolveStats(C.Structure):
         ("mlp_points_value", C.c_int64), ("mlp_full_ms", C.c_double), ("mlp_value_ms", C.c_double),
         ("mlp_full_launches", C.c_int32), ("mlp_value_launches", C.c_int32),
         ("iterate_ms", C.c_double), ("slots_in_lds", C.c_int32), ("pad_", C.c_int32),
-        ("mlp_points_full_reused", C.c_int64),
+        ("mlp_points_full_reused", C.c_int64), ("ric_ms", C.c_double), ("ric_launches", C.c_int32),
+        ("pad2_", C.c_int32), ("ric_solves", C.c_int64),
     ]
 
 

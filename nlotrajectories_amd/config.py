@@ -175,6 +175,7 @@ class Config(BaseModel):
             kw.update(length=float(b.length), width=float(b.width))
         if b.wheelbase is not None:
             kw["wheelbase"] = float(b.wheelbase)
-        if s.mode == "casadi":
-            kw["obstacles"] = self.obstacle_dicts()
+        # the exact scene travels with the problem in both modes (the analytic SDF in casadi mode; the
+        # learned SDF's training targets / sampling in l4casadi mode, where only the MLP enters the NLP)
+        kw["obstacles"] = self.obstacle_dicts()
         return Problem(**kw)

@@ -39,9 +39,10 @@ extern "C" void nlot_default_options(NlotSolverOptions* o) {
 // sparsity of gen/nn_sdf.cpp:36-37) on the GPU synchronously; CasADi owns arg/res (host doubles).
 // ------------------------------------------------------------------------------------------------
 namespace {
-const NlotMlp* g_bound = nullptr;
+const NlotMlp* g_bound = nullptr;  // cleared by nlot_mlp_destroy (casadi_unbind)
+int g_bound_dev = 0;               // device the bound model lives on
 std::mutex g_mu;
-float* g_dev = nullptr;  // [0..1] point, [2] lam, [3] val, [4..5] grad, [6..9] hess
+float* g_dev[64] = {};  // per device: [0..1] point, [2] lam, [3] val, [4..5] grad, [6..9] hess
 const casadi_int_t s_in0[3] = {1, 2, 1};
 const casadi_int_t s_out0[3] = {1, 1, 1};
 
@@ -51,7 +52,15 @@ int shim_eval(const double* x, const double* adj, double* val, double* grad, dou
         nlot::set_error("nn_sdf: no model bound (nlot_casadi_bind)");
         return 1;
     }
-    if (!g_dev && hipMalloc(&g_dev, 16 * sizeof(float)) != hipSuccess) return 1;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(g_bound_dev) != hipSuccess) return 1;
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{prev};
+    float*& scratch = g_dev[g_bound_dev & 63];
+    if (!scratch && hipMalloc(&scratch, 16 * sizeof(float)) != hipSuccess) return 1;
+    float* g_dev = scratch;
     float h[16] = {0};
     h[0] = (float)x[0];  // CasADi double -> fp32, as the TorchScript graph requires
     h[1] = (float)x[1];
@@ -76,7 +85,13 @@ int shim_eval(const double* x, const double* adj, double* val, double* grad, dou
 extern "C" int32_t nlot_casadi_bind(const NlotMlp* mlp) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_bound = mlp;
+    g_bound_dev = mlp ? mlp->device : 0;
     return NLOT_OK;
+}
+
+void nlot::casadi_unbind(const NlotMlp* m) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_bound == m) g_bound = nullptr;
 }
 
 extern "C" casadi_int_t nn_sdf_n_in(void) { return 1; }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -21,6 +22,24 @@ void set_error(const std::string& msg);
             return NLOT_ERR_HIP;                                                                   \
         }                                                                                          \
     } while (0)
+
+// One-time per-device kernel attribute (the dynamic-LDS limit): `done` is a bit mask over device ids
+// kept per kernel instantiation, so a process driving several GPUs sets it on each of them, and
+// concurrent callers at worst set it twice (idempotent).
+inline hipError_t set_lds_attr_once(std::atomic<uint64_t>& done, const void* fn, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
+// Compute units of the current device (cached per device id).
+int device_cus();
+// The CasADi shim drops its binding when the bound model is destroyed (nlot_capi.hip).
+void casadi_unbind(const NlotMlp* m);
 
 // Device-resident learned-SDF weights (opaque NlotMlp of the ABI).
 struct MlpDev {
@@ -76,4 +95,5 @@ int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* 
 struct NlotMlp {
     nlot::MlpDev dev;
     void* block;  // single device allocation holding all arrays
+    int device;   // HIP device the arrays live on
 };

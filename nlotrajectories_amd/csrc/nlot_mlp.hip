@@ -647,40 +647,35 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     }
 }
 
-static int g_num_cus = 0;
-
-static int num_cus() {
-    if (g_num_cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 256;
+int device_cus() {
+    static std::atomic<int> cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::atomic<int>& c = cus[dev & 63];
+    int v = c.load(std::memory_order_relaxed);
+    if (v == 0) {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
-        g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        v = (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) ? prop.multiProcessorCount
+                                                                                               : 256;
+        c.store(v, std::memory_order_relaxed);
     }
-    return g_num_cus;
+    return v;
 }
+static int num_cus() { return device_cus(); }
 
 template <int H, int L, bool FULL>
 static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                     const float* lam, const MlpOut& out, hipStream_t stream, const MlpReuse* reuse) {
     const size_t lds = sizeof(float) * mlp_lds_floats(H, L, FULL && mlp_staged(H, L));
-    static bool attr_set = false;
-    if (!attr_set) {
-        NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_kernel<H, L, FULL>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set{0};
+    NLOT_HIP_CHECK(set_lds_attr_once(attr_set, (const void*)mlp_kernel<H, L, FULL>, 160 * 1024));
     if constexpr (L == 1 && H == 128) {
         // split-bf16 MFMA kernels (fp32-equivalent products); NLOT_MLP=f32 selects the f32-MFMA kernels
         static const bool use_bf16 = !(getenv("NLOT_MLP") && strcmp(getenv("NLOT_MLP"), "f32") == 0);
         if (use_bf16 && w.Wp) {
             constexpr size_t lv = mlp_bf16_lds_bytes<H>();
-            static bool attr_v = false;
-            if (!attr_v) {
-                NLOT_HIP_CHECK(hipFuncSetAttribute((const void*)mlp_bf16<H, FULL>,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv));
-                attr_v = true;
-            }
+            static std::atomic<uint64_t> attr_v{0};
+            NLOT_HIP_CHECK(set_lds_attr_once(attr_v, (const void*)mlp_bf16<H, FULL>, (int)lv));
             constexpr int NTB = bf16_threads(FULL);
             const int64_t tiles = (n * P_per + NTB / 2 - 1) / (NTB / 2);
             const int64_t cap = num_cus();
@@ -761,6 +756,8 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     };
     NlotMlp* m = new NlotMlp;
     m->block = blk;
+    m->device = 0;
+    (void)hipGetDevice(&m->device);
     m->dev.in_kind = d->in_kind;
     m->dev.H = H;
     m->dev.n_hidden = L;
@@ -807,6 +804,7 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
 
 extern "C" void nlot_mlp_destroy(NlotMlp* m) {
     if (!m) return;
+    nlot::casadi_unbind(m);
     hipFree(m->block);
     delete m;
 }

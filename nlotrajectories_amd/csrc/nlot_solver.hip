@@ -1498,7 +1498,7 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
-                                               const double* __restrict__ xg, int init_pass) {
+                                               const double* __restrict__ xg, int init_pass, int* cnt) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -1888,6 +1888,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         SC(SC_PSQ) = psq_w;
         SC(SC_NZC) = nzc;
         SC(SC_RIC) = 1;
+        atomicAdd(&cnt[4], 1);  // statistics: Newton solves of this step (k_ric's work)
     }
 }
 
@@ -2518,11 +2519,21 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     g_stats = NlotSolveStats{};
     hipLaunchKernelGGL(k_init_state, dim3(Bi), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit);
     NLOT_HIP_CHECK(hipGetLastError());
-    int* hcnt = nullptr;
-    NLOT_HIP_CHECK(hipHostMalloc((void**)&hcnt, 4 * sizeof(int), hipHostMallocDefault));
-    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // host-side resources released on every return path (NLOT_HIP_CHECK returns early)
+    struct Res {
+        int* hcnt = nullptr;
+        hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        ~Res() {
+            for (auto& e : ev)
+                if (e) hipEventDestroy(e);
+            if (hcnt) hipHostFree(hcnt);
+        }
+    } res;
+    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, 8 * sizeof(int), hipHostMallocDefault));
+    int* const hcnt = res.hcnt;
+    hipEvent_t* const ev = res.ev;
     if (g_timing)
-        for (auto& e : ev) hipEventCreate(&e);
+        for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&ev[i]));
     MlpOut mo{}, mo_t[2] = {};
     MlpReuse reuse[2] = {};
     if (use_mlp) {
@@ -2574,13 +2585,15 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         }
         if (ev[4]) hipEventRecord(ev[4], st);
         if (step == 0) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
-            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1);
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C);
             hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
                                dP, dD, dW, act, n_active, (int)MODE_LSQ);
         }
-        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0);
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C);
+        if (ev[6]) hipEventRecord(ev[6], st);
         hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st, dP, dD,
                            dW, act, n_active, (int)MODE_NEWTON);
+        if (ev[6]) hipEventRecord(ev[7], st);
         hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
                            use_mlp ? ws.tpts[q] : nullptr);
         if (ev[4]) hipEventRecord(ev[5], st);
@@ -2598,7 +2611,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, C, Cn,
                            use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
-        NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, C, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+        NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, C, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         g_stats.iterations = step + 1;
         g_stats.mlp_points_full += (int64_t)hcnt[0] * P;
@@ -2612,16 +2625,17 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             g_stats.mlp_value_ms += c;
         }
         if (ev[4]) {
-            float a = 0;
+            float a = 0, r = 0;
             hipEventElapsedTime(&a, ev[4], ev[5]);
+            hipEventElapsedTime(&r, ev[6], ev[7]);
             g_stats.iterate_ms += a;
+            g_stats.ric_ms += r;
         }
+        g_stats.ric_launches++;
+        g_stats.ric_solves += hcnt[4];
         n_active = hcnt[2];
         cur ^= 1;
     }
-    for (auto& e : ev)
-        if (e) hipEventDestroy(e);
-    hipHostFree(hcnt);
     if (rc) return rc;
     hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);
     NLOT_HIP_CHECK(hipGetLastError());

@@ -2,7 +2,7 @@
 
 Instances are independent, so the data path has no collective: each rank samples its own seeded shard
 (`sampling.sample_start_goal(..., rank=r)`), solves it on its own GPU, and only the solutions are
-gathered afterwards (RCCL all_gather over xGMI for `nccl`, or gloo on CPU in the tests).  Timing is the
+gathered to rank 0 afterwards (RCCL gather over xGMI for `nccl`, or gloo on CPU in the tests).  Timing is the
 max over ranks, counts are summed.
 """
 from __future__ import annotations
@@ -19,15 +19,19 @@ def rank_world():
             int(os.environ.get("WORLD_SIZE", "1")))
 
 
-def gather_solutions(r: dict, keys=("X", "U", "S", "cost", "status", "iters")) -> dict:
-    """All-gather every rank's per-instance outputs (equal shard sizes), concatenated in rank order."""
+def gather_solutions(r: dict, keys=("X", "U", "S", "cost", "status", "iters"), dst: int = 0) -> dict:
+    """Gather every rank's per-instance outputs (equal shard sizes) to rank `dst`, concatenated in rank
+    order (RCCL gather over xGMI under `nccl`).  Other ranks get None per key: only the destination
+    needs the solutions, so nothing is broadcast back."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return {k: r[k] for k in keys}
+    world, me = dist.get_world_size(), dist.get_rank()
     out = {}
     for k in keys:
-        parts = [torch.empty_like(r[k]) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, r[k].contiguous())
-        out[k] = torch.cat(parts, 0)
+        t = r[k].contiguous()
+        parts = [torch.empty_like(t) for _ in range(world)] if me == dst else None
+        dist.gather(t, parts, dst=dst)
+        out[k] = torch.cat(parts, 0) if me == dst else None
     return out
 
 

@@ -3,7 +3,8 @@
 `FourierMLP` / `SIREN` restate the reference architectures (core/nn_architectures.py:8-100) as
 torch modules so users can train or load them; `MultiLayerPerceptron` restates l4casadi's naive
 MLP used for `model.type: mlp` (scripts/run_benchmark.py:64-65; external l4casadi, unpinned:
-Linear(in,H) -> act -> hidden_layers x [Linear(H,H) -> act] -> Linear(H,out)).
+Linear(in,H) -> act -> (hidden_layers - 1) x [Linear(H,H) -> act] -> Linear(H,out), SURVEY.md §8a a5;
+`hidden_layers` counts the hidden activations, so the YAMLs' num_hidden_layers: 2 is ONE HxH layer).
 
 `MlpWeights` is the flat fp32 form the HIP kernel consumes (NlotMlpDesc in include/nlot.h).
 """
@@ -61,21 +62,32 @@ class FourierMLP(nn.Module):
 
 
 class MultiLayerPerceptron(nn.Module):
-    """l4casadi.naive.MultiLayerPerceptron(in, hidden, out, hidden_layers, activation) restated."""
+    """l4casadi.naive.MultiLayerPerceptron(in, hidden, out, hidden_layers, activation) restated.
 
-    def __init__(self, in_features, hidden_features, out_features, hidden_layers, activation="ReLU"):
+    `hidden_layers` hidden activations: input Linear(in, H), then hidden_layers - 1 Linear(H, H), then
+    Linear(H, out) (l4casadi is external and unpinned, so the layer count is the
+    survey's record of its source).  The ReLU kernels consume it through MlpWeights.from_module."""
+
+    _ACTS = {"ReLU": F.relu, "Tanh": torch.tanh, "Sigmoid": torch.sigmoid, "LeakyReLU": F.leaky_relu,
+             None: lambda x: x}
+
+    def __init__(self, in_features, hidden_features, out_features, hidden_layers, activation=None):
         super().__init__()
-        if activation not in (None, "ReLU"):
-            raise ValueError("round-1 kernels support ReLU MLPs (see DESIGN.md §7)")
+        if hidden_layers < 1:
+            raise ValueError("There must be at least one hidden layer")
+        if activation not in self._ACTS:
+            raise ValueError(f"Unsupported activation: {activation}")
         self.input_layer = nn.Linear(in_features, hidden_features)
-        self.hidden_layers = nn.ModuleList([nn.Linear(hidden_features, hidden_features) for _ in range(hidden_layers)])
+        self.hidden_layers = nn.ModuleList([nn.Linear(hidden_features, hidden_features)
+                                            for _ in range(hidden_layers - 1)])
         self.output_layer = nn.Linear(hidden_features, out_features)
         self.activation = activation
+        self.act = self._ACTS[activation]
 
     def forward(self, x):
-        x = F.relu(self.input_layer(x))
+        x = self.act(self.input_layer(x))
         for layer in self.hidden_layers:
-            x = F.relu(layer(x))
+            x = self.act(layer(x))
         return self.output_layer(x)
 
 
@@ -146,7 +158,7 @@ class MlpWeights:
                 sd[f"layers.{l}.weight"] = self.arrays["W"][l]
                 sd[f"layers.{l}.bias"] = self.arrays["b"][l]
         else:
-            m = MultiLayerPerceptron(2, H, 1, self.n_hidden)
+            m = MultiLayerPerceptron(2, H, 1, self.n_hidden + 1, "ReLU")
             sd = {"input_layer.weight": self.arrays["A"].T, "input_layer.bias": self.arrays["b0"]}
             for l in range(self.n_hidden):
                 sd[f"hidden_layers.{l}.weight"] = self.arrays["W"][l]
@@ -173,6 +185,8 @@ class MlpWeights:
             return MlpWeights(_abi.MLP_IN_FOURIER, H, len(Ws), float(model.fourier.scale),
                               float(g(model.output_layer.bias)[0]), arrays)
         if hasattr(model, "input_layer") and hasattr(model, "hidden_layers"):
+            if getattr(model, "activation", "ReLU") != "ReLU":
+                raise ValueError("the SDF kernels support ReLU hidden layers (DESIGN.md §7)")
             H = model.input_layer.weight.shape[0]
             Ws = [g(l.weight) for l in model.hidden_layers]
             bs = [g(l.bias) for l in model.hidden_layers]
@@ -208,9 +222,10 @@ class MlpWeights:
 
     @staticmethod
     def random_relu_mlp(hidden=256, n_hidden=3, seed=0) -> "MlpWeights":
-        """Seeded kaiming-uniform ReLU MLP (the stress config; l4casadi.py:69-74)."""
+        """Seeded kaiming-uniform ReLU MLP with n_hidden HxH layers (the stress config 2-256x4-1 is
+        n_hidden = 3: four hidden activations; init as core/sdf/l4casadi.py:69-74)."""
         gen = torch.Generator().manual_seed(seed)
-        m = MultiLayerPerceptron(2, hidden, 1, n_hidden)
+        m = MultiLayerPerceptron(2, hidden, 1, n_hidden + 1, "ReLU")
         with torch.no_grad():
             for mod in m.modules():
                 if isinstance(mod, nn.Linear):

@@ -82,7 +82,8 @@ class Problem:
             raise ValueError("control_bounds must have one (min, max) pair per control")
         if self.sdf == "analytic" and not self.obstacles:
             raise ValueError("analytic SDF needs at least one obstacle")
-        if len(self.obstacles) > _abi.MAX_OBS:
+        obstacles = self.obstacles if self.sdf == "analytic" else []  # the learned SDF replaces the scene
+        if len(obstacles) > _abi.MAX_OBS:
             raise ValueError(f"at most {_abi.MAX_OBS} obstacles")
         p = _abi.NlotProblem()
         p.dynamics = _abi.DYNAMICS[self.dynamics]
@@ -105,8 +106,8 @@ class Problem:
             p.umin[i], p.umax[i] = float(lo), float(hi)
         p.softmin_alpha = float(self.softmin_alpha)
         p.path_eps = float(self.path_eps)
-        p.n_obs = len(self.obstacles)
-        for i, o in enumerate(self.obstacles):
+        p.n_obs = len(obstacles)
+        for i, o in enumerate(obstacles):
             t = o["type"]
             if t == "circle":
                 p.obs[i].type = _abi.OBS_CIRCLE

@@ -35,8 +35,10 @@ def solve_batch(problem: Problem, x0, xg, mlp: Optional[DeviceMlp] = None, optio
     if nx != problem.nx or xg.shape != x0.shape:
         raise ValueError(f"x0/xg must be [B, {problem.nx}]")
     N, nu = problem.N, problem.nu
+    if mlp is not None and not isinstance(mlp, DeviceMlp):
+        mlp = mlp.device_mlp  # an L4CasADi / NNObstacle (nlotrajectories_amd.l4casadi)
     if problem.sdf == "mlp" and mlp is None:
-        raise ValueError("learned-SDF problem needs a DeviceMlp")
+        raise ValueError("learned-SDF problem needs a DeviceMlp, L4CasADi or NNObstacle")
     Xi = None
     if X_init is not None:
         Xi = torch.as_tensor(X_init, dtype=torch.float64, device=device).contiguous()

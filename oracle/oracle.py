@@ -16,8 +16,8 @@ LIB_PATH = os.path.join(HERE, "liboracle_nlot.so")
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "nlot_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, "nlot_oracle.c"), os.path.join(HERE, "..", "include", "nlot.h")]
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
     return LIB_PATH
 

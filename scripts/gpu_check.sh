@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU check of the tree (run through gpurun): the -m gpu suite, the default bench line, and a
+# rocprofv3 kernel-trace summary of a short bench.  Every GPU step has its own time limit and the steps
+# are chained with &&, so the first failure ends the call.  OUT names the result directory.
+OUT=${OUT:-gpurun_out/check}
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+    > "$OUT/gpu_tests.log" 2>&1
+echo "pytest exit $?" >> "$OUT/gpu_tests.log"
+tail -3 "$OUT/gpu_tests.log"
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" && \
+  tail -c 1500 "$OUT/bench.json" && \
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run \
+      --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 0 --cpu-sample 0 \
+      > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2>&1) && \
+  find "$OUT/prof" -name "*kernel_stats*"
+fi

@@ -1,0 +1,103 @@
+"""GPU solver vs the CPU oracle on every built branch of the NLP: all six dynamics
+(run<DYN> instantiations), dot / rectangle / triangle footprints, slack and no-slack (per-corner)
+constraints, use_smooth, enforce_heading, circle + square scenes, and knot counts beyond one wavefront
+(N = 100 as benchmark 6, N = 256 as the stress config).
+
+Parity: the same algorithm runs on both sides in fp64 with the same analytic SDF, so after k accepted
+iterations the iterates agree to rounding (1e-7, growing along nonconvex paths: 1e-6 at k = 8).  Full
+solves of a small seeded batch must agree in outcome on >= 75 % of instances (tol 1e-4 termination
+points are path-sensitive) and every GPU-solved instance must satisfy its constraints."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    from nlotrajectories_amd.problem import BENCHMARKS, Problem, _circle, _square
+
+    b2, b5 = BENCHMARKS["b2"], BENCHMARKS["b5"]
+    scene = [_circle((0.5, 0.5), 0.2, 0.05), _square((0.2, 0.75), 0.15, 0.01)]
+    uni0, uni1 = [0.0, 0.0, 0.785], [1.0, 1.0, 0.785]
+    c = {
+        # the YAML's straight line from (0, 0) to (1, 1) runs through the circle's centre, where the circle SDF
+        # has no gradient (IPOPT stops with an invalid number, the oracle and the GPU with NLOT_NUMERIC):
+        # the goal is moved off the diagonal
+        "b1_dot_point2nd": (BENCHMARKS["b1"]["problem"], BENCHMARKS["b1"]["start"], [1.0, 0.9, 0.0, 0.0]),
+        "b5_ackermann2nd_squares": (b5["problem"], b5["start"], b5["goal"]),
+        "point1st_dot": (Problem(dynamics="point_1st", shape="dot", N=40, obstacles=scene,
+                                 control_bounds=((-1, 1), (-1, 1))), [0, 0, 0, 0], [1, 0.9, 0, 0]),
+        "unicycle_rect": (Problem(dynamics="unicycle", N=40, obstacles=scene), uni0, uni1),
+        "ackermann_rect": (Problem(dynamics="ackermann", length=0.1, width=0.1, wheelbase=0.1, N=40, obstacles=scene,
+                                   control_bounds=((-1, 1), (-2, 2))), uni0 + [0.0], uni1 + [0.0]),
+        "b2_no_slack": (b2["problem"].with_(use_slack=False), b2["start"], b2["goal"]),
+        "b2_smooth": (b2["problem"].with_(use_smooth=True, smooth_weight=0.5), b2["start"], b2["goal"]),
+        "b2_enforce_heading": (b2["problem"].with_(enforce_heading=True), b2["start"], b2["goal"]),
+        "b2_triangle": (b2["problem"].with_(shape="triangle"), b2["start"], b2["goal"]),
+        "b3_analytic_squares": (BENCHMARKS["b3"]["problem"], BENCHMARKS["b3"]["start"], BENCHMARKS["b3"]["goal"]),
+        # benchmark 6's solver settings (ackermann_2nd, no slack, smooth 0.5, dt 0.05) at the north_star's
+        # N = 100 on an analytic scene
+        "b6_settings_N100": (Problem(dynamics="ackermann_2nd", length=0.08, width=0.05, wheelbase=0.05, N=100, dt=0.05,
+                                    use_slack=False, slack_penalty=10, use_smooth=True, smooth_weight=0.5,
+                                    control_bounds=((-1, 1), (-2, 2)), obstacles=[_circle((0.5, 0.45), 0.12, 0.01)]),
+                             [0, 0.4, 0, 0, 0, 0, 0], [1, 0.4, 0, 0, 0, 0, 0]),
+        "unicycle2nd_N256": (b2["problem"].with_(N=256, dt=0.02), b2["start"], b2["goal"]),
+    }
+    return c
+
+
+CASES = list(_cases().keys())
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_iterates_match_oracle(name):
+    import oracle as O
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.solver import solve_batch
+
+    prob, x0, xg = _cases()[name]
+    for k in (1, 3, 8):
+        opt = _abi.default_options(max_iter=k)
+        rg = solve_batch(prob, np.array([x0], float), np.array([xg], float), options=opt)
+        rc = O.solve_one(prob, np.array(x0, float), np.array(xg, float), opt=opt)
+        assert rg["status"][0].item() == rc["status"], (name, k)
+        assert rg["iters"][0].item() == rc["iters"], (name, k)
+        dx = {n: float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U", "S")}
+        print(name, "k", k, "status", rc["status"], dx)
+        tol = 1e-7 if k <= 3 else 1e-6
+        for n, v in dx.items():
+            assert v <= tol, (name, k, n, v)
+
+
+@pytest.mark.parametrize("name", ["b1_dot_point2nd", "b5_ackermann2nd_squares", "b2_no_slack", "b2_smooth",
+                                  "b2_enforce_heading", "b6_settings_N100"])
+def test_full_solves_match_oracle(name):
+    import oracle as O
+    from nlotrajectories_amd.solver import solve_batch
+
+    prob, x0, xg = _cases()[name]
+    rng = np.random.default_rng(11)
+    B = 12
+    X0 = np.repeat(np.array([x0], float), B, 0)
+    XG = np.repeat(np.array([xg], float), B, 0)
+    X0[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
+    XG[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
+    rg = solve_batch(prob, X0, XG)
+    rc = O.solve_batch(prob, X0, XG, threads=8)
+    sg = rg["status"].cpu().numpy()
+    agree = (sg == rc["status"]).mean()
+    both = (sg == 0) & (rc["status"] == 0)
+    rel = np.abs(rg["cost"].cpu().numpy() - rc["cost"]) / np.abs(rc["cost"])
+    print(name, "gpu", sg.tolist(), "oracle", rc["status"].tolist(), "rel cost", np.round(rel[both], 8).tolist())
+    assert agree >= 0.75, (name, agree)
+    # GPU-solved trajectories satisfy the start / terminal / dynamics equalities and the bounds
+    X, U = rg["X"].cpu().numpy(), rg["U"].cpu().numpy()
+    term = [i for i in range(prob.nx) if prob.enforce_heading or i != 2]
+    for b in np.where(sg == 0)[0]:
+        assert np.abs(X[b, 0] - X0[b]).max() < 1e-4
+        assert np.abs(X[b, -1, term] - XG[b, term]).max() < 1e-4
+        F = X[b, :-1] + prob.dt * np.stack([O.dynamics(prob, X[b, k], U[b, k]) for k in range(prob.N)])
+        assert np.abs(X[b, 1:] - F).max() < 1e-4
+        lo = np.array([c[0] for c in prob.control_bounds])
+        hi = np.array([c[1] for c in prob.control_bounds])
+        assert (U[b] >= lo - 1e-9).all() and (U[b] <= hi + 1e-9).all()
