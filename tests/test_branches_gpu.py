@@ -4,7 +4,9 @@ constraints, use_smooth, enforce_heading, circle + square scenes, and knot count
 (N = 100 as benchmark 6, N = 256 as the stress config).
 
 Parity: the same algorithm runs on both sides in fp64 with the same analytic SDF, so after k accepted
-iterations the iterates agree to rounding (1e-7, growing along nonconvex paths: 1e-6 at k = 8).  Full
+iterations the iterates agree to rounding: 1e-7 (1e-6 at k = 8), or 20x the oracle's own response to a
+1e-13 perturbation of the start state where the path amplifies rounding more than that (the no-slack
+start inside the obstacle: 4e-7 at k = 3 for the perturbed oracle itself).  Full
 solves of a small seeded batch must agree in outcome on >= 75 % of instances (tol 1e-4 termination
 points are path-sensitive) and every GPU-solved instance must satisfy its constraints."""
 import numpy as np
@@ -60,11 +62,15 @@ def test_iterates_match_oracle(name):
         opt = _abi.default_options(max_iter=k)
         rg = solve_batch(prob, np.array([x0], float), np.array([xg], float), options=opt)
         rc = O.solve_one(prob, np.array(x0, float), np.array(xg, float), opt=opt)
+        xp = np.array(x0, float)
+        xp[0] += 1e-13
+        rp = O.solve_one(prob, xp, np.array(xg, float), opt=opt)
+        sens = max(float(np.abs(rp[n] - rc[n]).max()) for n in ("X", "U", "S"))
         assert rg["status"][0].item() == rc["status"], (name, k)
         assert rg["iters"][0].item() == rc["iters"], (name, k)
         dx = {n: float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U", "S")}
-        print(name, "k", k, "status", rc["status"], dx)
-        tol = 1e-7 if k <= 3 else 1e-6
+        print(name, "k", k, "status", rc["status"], dx, "oracle sensitivity", sens)
+        tol = max(1e-7 if k <= 3 else 1e-6, 20 * sens)
         for n, v in dx.items():
             assert v <= tol, (name, k, n, v)
 
