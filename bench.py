@@ -106,8 +106,8 @@ def main():
     x0, xg = sample_start_goal(prob, a.batch, seed=a.seed, sdf=sdf_gpu, rank=rank)
     x0 = torch.tensor(x0, dtype=torch.float64, device=dev)
     xg = torch.tensor(xg, dtype=torch.float64, device=dev)
-    opt = _abi.default_options() if a.mu_strategy == "adaptive" else \
-        _abi.default_options(mu_strategy=0, barrier_tol_factor=10.0)
+    opt = _abi.gpu_options() if a.mu_strategy == "adaptive" else \
+        _abi.gpu_options(mu_strategy=0, barrier_tol_factor=10.0)
 
     from nlotrajectories_amd.solver import workspace_bytes
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 4
+#define NLOT_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -40,8 +40,13 @@ extern "C" {
 /* ---- per-problem solve status (output array `status`) ----------------------------------- */
 #define NLOT_SOLVED 0             /* IPOPT "Solve_Succeeded" analogue: E_0 <= tol + abs. tols */
 #define NLOT_MAXITER 1            /* max_iter reached (IPOPT Maximum_Iterations_Exceeded)     */
-#define NLOT_LS_FAILED 2          /* alpha < alpha_min: IPOPT would enter restoration         */
+#define NLOT_LS_FAILED 2          /* alpha < alpha_min with restoration switched off (opt.resto = 0) */
 #define NLOT_NUMERIC 3            /* non-finite values / inertia correction failed            */
+#define NLOT_RESTO_FAILED 4       /* IPOPT Restoration_Failed: restoration line search failed, or it
+                                     converged to a feasible point the filter does not accept  */
+#define NLOT_INFEASIBLE 5         /* IPOPT Infeasible_Problem_Detected (restoration converged to a
+                                     point of local infeasibility)                              */
+#define NLOT_TINY_STEP 6          /* IPOPT Search_Direction_Becomes_Too_Small                  */
 
 /* ---- dynamics (core/dynamics.py:7-13, DYNAMICS_CLASS_MAP 151-158) ------------------------ */
 enum NlotDynamics {
@@ -122,7 +127,20 @@ typedef struct NlotSolverOptions {
     double bound_push;           /* 1e-2 */
     double bound_frac;           /* 1e-2 */
     int32_t max_soc;             /* second-order corrections per iteration (IPOPT default 4) */
+    int32_t resto;               /* 1: feasibility restoration phase on line-search failure (IPOPT) */
+    int32_t watchdog_shortened_iter_trigger; /* 10 (IPOPT default; 0 switches the watchdog off) */
+    int32_t watchdog_trial_iter_max;         /* 3 */
+    int32_t max_soft_resto_iters;            /* 10 */
     int32_t pad_;
+    double kappa_soc;                        /* 0.99 */
+    double tiny_step_tol;                    /* 10 eps = 2.22e-15 */
+    double tiny_step_y_tol;                  /* 1e-2 */
+    double soft_resto_pderror_reduction_factor; /* 0.9999 (0 switches the soft restoration off) */
+    double required_infeasibility_reduction; /* kappa_resto = 0.9 */
+    double resto_penalty_parameter;          /* rho = 1000 */
+    double resto_proximity_weight;           /* zeta = weight * sqrt(mu), weight 1 */
+    double bound_mult_reset_threshold;       /* 1000 */
+    double resto_failure_feasibility_threshold; /* 0 means 1e2 * tol (IPOPT default) */
 } NlotSolverOptions;
 
 /* Learned SDF: an l4casadi-wrappable torch model, flattened.

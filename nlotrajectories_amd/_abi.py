@@ -3,7 +3,9 @@ import ctypes as C
 
 NLOT_OK = 0
 NLOT_SOLVED, NLOT_MAXITER, NLOT_LS_FAILED, NLOT_NUMERIC = 0, 1, 2, 3
-STATUS_NAMES = {0: "solved", 1: "max_iter", 2: "line_search_failed", 3: "numeric"}
+NLOT_RESTO_FAILED, NLOT_INFEASIBLE, NLOT_TINY_STEP = 4, 5, 6
+STATUS_NAMES = {0: "solved", 1: "max_iter", 2: "line_search_failed", 3: "numeric", 4: "restoration_failed",
+                5: "infeasible", 6: "tiny_step"}
 
 # NlotDynamics (core/dynamics.py:7-13)
 DYNAMICS = {"point_1st": 0, "point_2nd": 1, "unicycle": 2, "unicycle_2nd": 3, "ackermann": 4,
@@ -41,7 +43,12 @@ class NlotSolverOptions(C.Structure):
         ("mu_init", C.c_double), ("barrier_tol_factor", C.c_double), ("dual_inf_tol", C.c_double),
         ("constr_viol_tol", C.c_double), ("compl_inf_tol", C.c_double),
         ("constr_mult_init_max", C.c_double), ("bound_push", C.c_double), ("bound_frac", C.c_double),
-        ("max_soc", C.c_int32), ("pad_", C.c_int32),
+        ("max_soc", C.c_int32), ("resto", C.c_int32), ("watchdog_shortened_iter_trigger", C.c_int32),
+        ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32), ("pad_", C.c_int32),
+        ("kappa_soc", C.c_double), ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
+        ("soft_resto_pderror_reduction_factor", C.c_double), ("required_infeasibility_reduction", C.c_double),
+        ("resto_penalty_parameter", C.c_double), ("resto_proximity_weight", C.c_double),
+        ("bound_mult_reset_threshold", C.c_double), ("resto_failure_feasibility_threshold", C.c_double),
     ]
 
 
@@ -65,12 +72,31 @@ class NlotSolveStats(C.Structure):
     ]
 
 
+# IPOPT's globalisation safeguards switched off: the round-1 algorithm (plain filter line search)
+SAFEGUARDS_OFF = dict(max_soc=0, resto=0, watchdog_shortened_iter_trigger=0, soft_resto_pderror_reduction_factor=0.0,
+                      tiny_step_tol=0.0)
+
+
 def default_options(**kw) -> NlotSolverOptions:
     """IPOPT settings of runner.py:113-125 plus IPOPT defaults."""
     o = NlotSolverOptions(tol=1e-4, max_iter=1000, mu_strategy=1, mu_init=0.1,
                           barrier_tol_factor=0.05, dual_inf_tol=1.0, constr_viol_tol=1e-4,
                           compl_inf_tol=1e-4, constr_mult_init_max=1e3, bound_push=1e-2,
-                          bound_frac=1e-2, max_soc=0)
+                          bound_frac=1e-2, max_soc=4, resto=1, watchdog_shortened_iter_trigger=10,
+                          watchdog_trial_iter_max=3, max_soft_resto_iters=10, kappa_soc=0.99,
+                          tiny_step_tol=10 * 2.220446049250313e-16, tiny_step_y_tol=1e-2,
+                          soft_resto_pderror_reduction_factor=0.9999, required_infeasibility_reduction=0.9,
+                          resto_penalty_parameter=1000.0, resto_proximity_weight=1.0,
+                          bound_mult_reset_threshold=1000.0, resto_failure_feasibility_threshold=0.0)
     for k, v in kw.items():
         setattr(o, k, v)
     return o
+
+
+def gpu_options(**kw) -> NlotSolverOptions:
+    """The IPOPT settings the GPU path runs: the defaults above (second-order corrections, watchdog, tiny-step
+    test) without the feasibility restoration phase and the soft restoration, which only the CPU oracle
+    implements: where IPOPT would restore, the GPU ends the instance with NLOT_LS_FAILED."""
+    base = dict(resto=0, soft_resto_pderror_reduction_factor=0.0)
+    base.update(kw)
+    return default_options(**base)

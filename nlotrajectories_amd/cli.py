@@ -80,7 +80,7 @@ def run_benchmark(config_path, initializer="yaml", weights=None, results_dir="re
     if x0.shape[1] != prob.nx or xg.shape[1] != prob.nx:
         raise ValueError(f"start/goal states must have {prob.nx} entries for {prob.dynamics}")
     X_init = np.zeros((1, prob.N + 1, prob.nx)) if init == "default" else None  # CasADi default guess
-    opt = options or _abi.default_options()
+    opt = options or _abi.gpu_options()
     torch.cuda.synchronize()
     t0 = time.time()
     r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, X_init=X_init)

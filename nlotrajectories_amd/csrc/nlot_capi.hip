@@ -30,7 +30,20 @@ extern "C" void nlot_default_options(NlotSolverOptions* o) {
     o->constr_mult_init_max = 1e3;
     o->bound_push = 1e-2;
     o->bound_frac = 1e-2;
-    o->max_soc = 0;
+    o->max_soc = 4;                          // IPOPT defaults from here on
+    o->resto = 1;
+    o->watchdog_shortened_iter_trigger = 10;
+    o->watchdog_trial_iter_max = 3;
+    o->max_soft_resto_iters = 10;
+    o->kappa_soc = 0.99;
+    o->tiny_step_tol = 10 * 2.220446049250313e-16;
+    o->tiny_step_y_tol = 1e-2;
+    o->soft_resto_pderror_reduction_factor = 0.9999;
+    o->required_infeasibility_reduction = 0.9;
+    o->resto_penalty_parameter = 1000.0;
+    o->resto_proximity_weight = 1.0;
+    o->bound_mult_reset_threshold = 1000.0;
+    o->resto_failure_feasibility_threshold = 0.0;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -37,7 +37,7 @@
 
 namespace nlot {
 
-enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3 };
+enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4 };
 
 // Minimum waves per SIMD the per-instance kernels are compiled for (register budget 512 / w per lane),
 // and the depth of k_ric's stage ring (its LDS per wavefront sets k_ric's occupancy).  These kernels wait
@@ -70,6 +70,16 @@ enum Scal {
     // quality-function oracle needs
     SC_RIC, SC_RMU0, SC_RMU1, SC_RNR, SC_USEQF, SC_AVG, SC_DSQ, SC_PSQ, SC_NZC,
     SC_ACCSLOT,  // trial-list slot of the accepted line-search candidate (forward reuse), -1 if none
+    // IPOPT's globalisation safeguards: second-order correction (count in progress, the
+    // original trial's alpha and alpha_z, theta of the last corrected trial), k_ric's fixed delta_w (-1: the
+    // inertia-correction loop), watchdog (active, shortened-step counter, trials, reference values and the
+    // saved line-search scalars), tiny step (this iteration, the previous one), max primal infeasibility
+    SC_SOCK, SC_SOCA, SC_SOCAZ, SC_SOCTH, SC_RICFIX,
+    SC_WD, SC_WDSHORT, SC_WDTRIAL, SC_WDTH, SC_WDPH, SC_WDGD, SC_WDAT, SC_WDAZ, SC_WDAMIN, SC_WDMU, SC_WDTAU,
+    SC_TINY, SC_TINYLAST, SC_PRIMAL,
+    // IPOPT's filter reset heuristic: last rejection of this line search was by the filter, successive such
+    // iterations, resets done
+    SC_LASTREJF, SC_NFREJ, SC_NFRES,
     SC_COUNT
 };
 constexpr int FILT_MAX = 64;
@@ -121,6 +131,12 @@ __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
     return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
 }
 
+// an iterate (X U S T yi yk yt yd zl zu zs vt) or a step (dX dU dS dT yi_n yk_n yt_n yd_n dzl dzu dzs dvt):
+// the save areas of the second-order correction and the watchdog
+__host__ __device__ constexpr int it_len(int N, int nx, int nu, int M) {
+    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + 8;
+}
+
 // instance-major arrays: (name, per-instance length)
 #define NLOT_WS_ARRAYS(X_)                                                                             \
     X_(X, (N + 1) * nx) X_(U, N * nu) X_(S, N + 1) X_(T, (N + 1) * M) X_(yi, nx) X_(yk, N * nx) X_(yt, 8) \
@@ -131,7 +147,9 @@ __host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
     X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1) X_(dvt, (N + 1) * M) X_(sc, SC_COUNT)               \
     X_(filt, 2 * FILT_MAX) X_(afilt, 2 * FILT_MAX) X_(qa, qf_len(N, nx, nu, M)) X_(qc, qf_len(N, nx, nu, M))  \
     X_(stg, (N + 1) * slot_len(nx, nu)) X_(hg, (N + 1) * hg_len(nx, nu)) X_(vf, (N + 1) * vf_len(nx, nu))   \
-    X_(dX2, (N + 1) * nx) X_(dU2, N * nu) X_(dS2, N + 1) X_(yi2, nx) X_(yk2, N * nx) X_(yt2, 8)
+    X_(dX2, (N + 1) * nx) X_(dU2, N * nu) X_(dS2, N + 1) X_(yi2, nx) X_(yk2, N * nx) X_(yt2, 8)         \
+    X_(sts, it_len(N, nx, nu, M)) X_(rcs, nx + N * nx + 8 + (N + 1) * M) X_(wdi, it_len(N, nx, nu, M))       \
+    X_(wdd, it_len(N, nx, nu, M))
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -227,6 +245,34 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
 // element i of instance b's array (instance-major)
 #define AT(arr, i) (ws.arr[(size_t)b * ws.L_##arr + (i)])
 #define SC(i) AT(sc, i)
+
+// save (to buf) or load (from buf) an iterate, a step, or the residual rows, lane-strided
+#define NLOT_ITER_ARRAYS(F_) F_(X) F_(U) F_(S) F_(T) F_(yi) F_(yk) F_(yt) F_(yd) F_(zl) F_(zu) F_(zs) F_(vt)
+#define NLOT_STEP_ARRAYS(F_) F_(dX) F_(dU) F_(dS) F_(dT) F_(yi_n) F_(yk_n) F_(yt_n) F_(yd_n) F_(dzl) F_(dzu) F_(dzs) F_(dvt)
+#define NLOT_RES_ARRAYS(F_) F_(rci) F_(rcd) F_(rct) F_(rcq)
+#define NLOT_IO(name)                                                              \
+    {                                                                              \
+        double* a_ = &AT(name, 0);                                                 \
+        const int n_ = ws.L_##name;                                                \
+        for (int i_ = lane; i_ < n_; i_ += 64) {                                   \
+            if (save) buf[off + i_] = a_[i_];                                      \
+            else a_[i_] = buf[off + i_];                                           \
+        }                                                                          \
+        off += n_;                                                                 \
+    }
+__device__ inline void iter_io(const Ws& ws, int64_t b, int lane, double* buf, bool save) {
+    int off = 0;
+    NLOT_ITER_ARRAYS(NLOT_IO)
+}
+__device__ inline void step_io(const Ws& ws, int64_t b, int lane, double* buf, bool save) {
+    int off = 0;
+    NLOT_STEP_ARRAYS(NLOT_IO)
+}
+__device__ inline void res_io(const Ws& ws, int64_t b, int lane, double* buf, bool save) {
+    int off = 0;
+    NLOT_RES_ARRAYS(NLOT_IO)
+}
+#undef NLOT_IO
 
 // ---- wave-level helpers (64 lanes; results broadcast from lane 0 so every lane branches alike) ----
 __device__ inline double wsum(double v) {
@@ -1120,7 +1166,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC
     };
 
     // inertia correction (IPOPT): delta_w = 0, then 1e-4 (or last / 3), x100 (x8 once one was used)
-    double dw = 0.0, dw_in_hg = 0.0;
+    const double fixdw = SC(SC_RICFIX);  // >= 0: second-order correction, stages built with this delta_w
+    const bool fixed = fixdw >= 0.0;
+    double dw = fixed ? fixdw : 0.0, dw_in_hg = dw;
     int fail = 0;
 #ifdef NLOT_PHASE_PROF
     long long t_build = 0, t_back = 0;
@@ -1144,7 +1192,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC
 #ifdef NLOT_PHASE_PROF
         t_back += wall_clock64() - tb;
 #endif
-        if (!fail || mode != MODE_NEWTON) break;
+        if (!fail || mode != MODE_NEWTON || fixed) break;
         dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
         if (dw > 1e40) break;
     }
@@ -1154,7 +1202,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC
     if (fail) {
         __syncthreads();
         if (l == 0) {
-            if (mode == MODE_NEWTON) {
+            if (fixed) {
+                SC(SC_RIC) = 4;  // the correction's solve failed: k_iter_b resumes the backtracking
+            } else if (mode == MODE_NEWTON) {
                 SC(SC_STATUS) = NLOT_NUMERIC;
                 SC(SC_PHASE) = PH_DONE;
                 SC(SC_RIC) = 0;
@@ -1331,7 +1381,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC
                n_att, t_build, t_back, wall_clock64() - tr1, wall_clock64() - tr0);
 #endif
     if (l == 0) {
-        if (dw > 0.0 && mode == MODE_NEWTON) SC(SC_DWLAST) = dw;
+        if (dw > 0.0 && mode == MODE_NEWTON && !fixed) SC(SC_DWLAST) = dw;
         SC(SC_DW) = dw;
         SC(SC_RIC) = 2;
     }
@@ -1384,6 +1434,16 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
         SC(SC_ACCSLOT) = -1;
         SC(SC_NFILT) = 0;
         SC(SC_E0) = 0;
+        SC(SC_SOCK) = 0;
+        SC(SC_RICFIX) = -1;
+        SC(SC_WD) = 0;
+        SC(SC_WDSHORT) = 0;
+        SC(SC_WDTRIAL) = 0;
+        SC(SC_TINY) = 0;
+        SC(SC_TINYLAST) = 0;
+        SC(SC_LASTREJF) = 0;
+        SC(SC_NFREJ) = 0;
+        SC(SC_NFRES) = 0;
         ws.act[0][b] = b;
     }
 }
@@ -1506,9 +1566,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     constexpr int NX = SV::NX, NU = SV::NU;
     const int b = active[blockIdx.x], lane = threadIdx.x;
     const int ph = (int)SC(SC_PHASE);
-    if (ph != PH_INIT && ph != PH_EVAL) return;
+    if (ph != PH_INIT && ph != PH_EVAL && ph != PH_SOC) return;
     if (init_pass && ph != PH_INIT) return;
     double* SL = &AT(stg, 0);
+    if (ph == PH_SOC) {
+        // second-order correction: the same Newton matrix (the iteration's delta_w, no inertia loop) with the
+        // corrected constraint residuals c_soc in rci/rcd/rct/rcq (written by k_accept)
+        const double dw = SC(SC_DW), mu = SC(SC_MU);
+        SV::template build_stages<false>(p, dm, ws, b, lane, MODE_NEWTON, dw, mu, 0.0, 1, SL);
+        if (lane == 0) {
+            SC(SC_RMU0) = mu;
+            SC(SC_RMU1) = 0.0;
+            SC(SC_RNR) = 1;
+            SC(SC_USEQF) = 0.0;
+            SC(SC_RICFIX) = dw;
+            SC(SC_RIC) = 1;
+            atomicAdd(&cnt[4], 1);
+        }
+        return;
+    }
     const int N = dm.N, M = dm.M, nc = dm.nc;
     const int rank = (int)SC(SC_RANK);
     const double k1 = o.bound_push;
@@ -1784,10 +1860,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         for (int q = lane; q < (N + 1) * M; q += 64) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - m));
         return wmax(cm);
     };
+    bool tiny_last = o.mu_strategy == 0 && SC(SC_TINYLAST) != 0.0;  // a tiny step forces a decrease
     auto barrier_decrease = [&](double cm) {  // Fiacco-McCormick: decrease while the barrier problem is solved
         for (;;) {
             const double Emu = fmax(fmax(dual / sd, primal), cm / scc);
-            if (Emu > kap * mu) break;
+            if (Emu > kap * mu && !tiny_last) break;
+            tiny_last = false;
             const double nm = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_floor);
             if (nm >= mu) break;
             mu = nm;
@@ -1887,6 +1965,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         SC(SC_DSQ) = dsq_w;
         SC(SC_PSQ) = psq_w;
         SC(SC_NZC) = nzc;
+        SC(SC_PRIMAL) = primal;
+        SC(SC_RICFIX) = -1.0;
         SC(SC_RIC) = 1;
         atomicAdd(&cnt[4], 1);  // statistics: Newton solves of this step (k_ric's work)
     }
@@ -1904,7 +1984,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     using SV = Solver<DYN>;
     constexpr int NX = SV::NX, NU = SV::NU;
     const int b = active[blockIdx.x], lane = threadIdx.x;
-    if ((int)SC(SC_RIC) != 2) return;
+    const int ric = (int)SC(SC_RIC);
+    if (ric == 4) {  // a second-order correction's solve failed: restore the step, halve the original alpha
+        double* rb = &AT(rcs, 0);
+        double* sb = &AT(sts, 0);
+        {
+            double* buf = rb;
+            const bool save = false;
+            res_io(ws, b, lane, buf, save);
+            buf = sb;
+            step_io(ws, b, lane, buf, save);
+        }
+        const double na = 0.5 * SC(SC_SOCA);
+        wsync();
+        if (lane == 0) {
+            SC(SC_RIC) = 0;
+            SC(SC_SOCK) = 0;
+            SC(SC_AZ) = SC(SC_SOCAZ);
+            SC(SC_TRIALS) = 1;
+            SC(SC_ALPHA) = na;
+            if (na < SC(SC_AMIN)) {
+                SC(SC_STATUS) = NLOT_LS_FAILED;
+                SC(SC_PHASE) = PH_DONE;
+            } else {
+                SC(SC_PHASE) = PH_LS;
+            }
+        }
+        if (!(na < SC(SC_AMIN))) emit_points(*pp_, *dd_, ws, b, lane, cnt, true, tp, 1, na);
+        return;
+    }
+    if (ric != 2) return;
+    const bool soc = (int)SC(SC_PHASE) == PH_SOC;
     const int N = dm.N, M = dm.M;
     const double dw = SC(SC_DW), avg = SC(SC_AVG), dsq_w = SC(SC_DSQ), psq_w = SC(SC_PSQ), nzc = SC(SC_NZC);
     const bool use_qf = SC(SC_USEQF) != 0.0;
@@ -2244,6 +2354,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     az = wmin(az);
     gd = wsum(gd);
     wsync();
+    if (soc) {  // second-order corrected direction: its fraction-to-boundary step is the one trial point
+        if (lane == 0) {
+            SC(SC_RIC) = 0;
+            SC(SC_ALPHA) = amax;
+            SC(SC_AZ) = az;
+            SC(SC_PHASE) = PH_LS;
+        }
+        wsync();
+        emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, amax);
+        return;
+    }
     double theta, phi;
     theta_phi(mu, &theta, &phi);
     const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3;
@@ -2253,6 +2374,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         if (theta <= SC(SC_THMIN)) amin = fmin(amin, delta * pow(theta, sth) / pow(-gd, sph));
     }
     amin *= 0.05;
+    // IPOPT DetectTinyStep (not while the watchdog runs): primal step tiny relative to the iterate, multiplier
+    // step small, nearly feasible -> the full step is taken without a line search
+    const bool in_wd = SC(SC_WD) != 0.0;
+    bool tiny = false;
+    if (o.tiny_step_tol > 0 && !in_wd) {
+        double mx = 0, my = 0, ya = 0;
+        for (int i = lane; i < (N + 1) * NX; i += 64) mx = fmax(mx, fabs(AT(dX, i)) / (1.0 + fabs(AT(X, i))));
+        for (int i = lane; i < N * NU; i += 64) mx = fmax(mx, fabs(AT(dU, i)) / (1.0 + fabs(AT(U, i))));
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) mx = fmax(mx, fabs(AT(dS, k)) / (1.0 + fabs(AT(S, k))));
+        for (int q = lane; q < (N + 1) * M; q += 64) mx = fmax(mx, fabs(AT(dT, q)) / (1.0 + fabs(AT(T, q))));
+        auto ystep = [&](double yn, double y) {
+            my = fmax(my, fabs(yn - y));
+            ya = fmax(ya, fabs(y));
+        };
+        for (int i = lane; i < NX; i += 64) ystep(AT(yi_n, i), AT(yi, i));
+        for (int i = lane; i < N * NX; i += 64) ystep(AT(yk_n, i), AT(yk, i));
+        for (int i = lane; i < nc; i += 64) ystep(AT(yt_n, i), AT(yt, i));
+        for (int q = lane; q < (N + 1) * M; q += 64) ystep(AT(yd_n, q), AT(yd, q));
+        mx = wmax(mx);
+        my = wmax(my);
+        ya = wmax(ya);
+        tiny = mx <= o.tiny_step_tol && my / (1.0 + ya) <= o.tiny_step_y_tol && SC(SC_PRIMAL) < 1e-4;
+    }
+    // IPOPT StartWatchDog: after watchdog_shortened_iter_trigger shortened steps in a row, remember the point,
+    // its direction and reference values; the next watchdog_trial_iter_max iterations try full steps only
+    const bool start_wd = !tiny && !in_wd && o.watchdog_shortened_iter_trigger > 0 &&
+                          SC(SC_WDSHORT) >= o.watchdog_shortened_iter_trigger;
+    if (start_wd) {
+        double* buf = &AT(wdi, 0);
+        iter_io(ws, b, lane, buf, true);
+        buf = &AT(wdd, 0);
+        step_io(ws, b, lane, buf, true);
+    }
     wsync();
     if (lane == 0) {
         SC(SC_RIC) = 0;
@@ -2264,11 +2419,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         SC(SC_AZ) = az;
         SC(SC_ALPHA) = amax;
         SC(SC_TRIALS) = 0;
+        SC(SC_SOCK) = 0;
+        SC(SC_LASTREJF) = 0;
+        SC(SC_TINY) = tiny ? 1.0 : 0.0;
         SC(SC_PHASE) = PH_LS;
+        if (start_wd) {
+            SC(SC_WD) = 1;
+            SC(SC_WDTRIAL) = 0;
+            SC(SC_WDTH) = theta;
+            SC(SC_WDPH) = phi;
+            SC(SC_WDGD) = gd;
+            SC(SC_WDAT) = amax;
+            SC(SC_WDAZ) = az;
+            SC(SC_WDAMIN) = amin;
+            SC(SC_WDMU) = mu;
+            SC(SC_WDTAU) = tau;
+        }
     }
-    // the first line-search round: alpha_max alone
+    // the first line-search round: alpha_max alone (none for a tiny step)
     wsync();  // dX complete
-    emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, amax);
+    emit_points(p, dm, ws, b, lane, cnt, true, tp, tiny ? 0 : 1, amax);
 }
 
 template <int DYN>
@@ -2286,86 +2456,222 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
         const int N = dm.N, M = dm.M, nc = dm.nc;
         const double a0 = SC(SC_ALPHA), mu = SC(SC_MU);
         const int rank0 = (int)SC(SC_RANK), ncand = (int)SC(SC_NCAND);  // as emitted
-        int ok = 0, ftype = 0, armijo = 0, cnd = 0;
-        double al = a0, th = 0, pht = 0;
-        const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
-        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
-        const int nf = (int)SC(SC_NFILT);
-        for (cnd = 0; cnd < ncand && !ok; ++cnd) {
-        al = ldexp(a0, -cnd);
-        const int rank = rank0 + cnd;
         const double* x0b = x0 + (size_t)b * NX;
         const double* xgb = xg + (size_t)b * NX;
-        // theta and phi at the trial point x + al d
-        double bar = 0, lin = 0;
-        th = 0;
-        for (int i = lane; i < NX; i += 64) th += fabs(AT(X, i) + al * AT(dX, i) - x0b[i]);
-        for (int cc = lane; cc < nc; cc += 64) {
-            const int ix = N * NX + dm.tidx[cc];
-            th += fabs(AT(X, ix) + al * AT(dX, ix) - xgb[dm.tidx[cc]]);
-        }
-        for (int k = lane; k <= N; k += 64) {
-            double xk[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i) + al * AT(dX, k * NX + i);
-            if (k < N) {
-                double u[NU], f[NX];
-#pragma unroll
-                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
-                Dyn<DYN>::f(xk, u, p.wheelbase, f);
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-                    th += fabs(AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]));
-#pragma unroll
-                for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
+        const int nf = (int)SC(SC_NFILT);
+        const bool in_wd = SC(SC_WD) != 0.0, tiny = SC(SC_TINY) != 0.0;
+        const int sock = (int)SC(SC_SOCK);
+        // theta and phi at the trial point x + al d (candidate trial-list slot `rank`); with `store`, the
+        // residual rows become keep * rc + c(x + al d) (the second-order correction's right-hand side)
+        auto trial = [&](double al, int rank, bool store, double keep, double* th_o, double* ph_o) {
+            double th = 0, bar = 0, lin = 0;
+            for (int i = lane; i < NX; i += 64) {
+                const double c = AT(X, i) + al * AT(dX, i) - x0b[i];
+                th += fabs(c);
+                if (store) AT(rci, i) = keep * AT(rci, i) + c;
             }
-            double d[MMAX];
-            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
-            const double sk = AT(S, k) + al * AT(dS, k);
-            for (int j = 0; j < M; ++j) {
-                const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
-                th += fabs(d[j] + (dm.sd ? sk : 0.0) - t);
-                bar += log(t);
-                lin += t;
+            for (int cc = lane; cc < nc; cc += 64) {
+                const int ix = N * NX + dm.tidx[cc];
+                const double c = AT(X, ix) + al * AT(dX, ix) - xgb[dm.tidx[cc]];
+                th += fabs(c);
+                if (store) AT(rct, cc) = keep * AT(rct, cc) + c;
             }
-            if (dm.ns) {
-                bar += log(sk);
-                lin += sk;
-            }
-        }
-        th = wsum(th);
-        const double fo = objective_w(p, dm, ws, b, lane, al);
-        pht = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
-        // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint
-        ok = isfinite(th) && isfinite(pht) && th <= SC(SC_THMAX);
-        ftype = gd < 0 && al * pow(-gd, sph) > delta * pow(theta, sth);
-        armijo = cmp_le(pht - phi, eta * al * gd, phi);
-        if (ok) {
-            if (ftype && theta <= SC(SC_THMIN)) {
-                ok = armijo;
-            } else {
-                ok = cmp_le(th, (1.0 - gt) * theta, theta) || cmp_le(pht - phi, -gp * theta, phi);
-                if (ok && pht > phi) {
-                    const double bas = fabs(phi) > 10.0 ? log10(fabs(phi)) : 1.0;
-                    if (log10(pht - phi) > 5.0 + bas) ok = 0;
+            for (int k = lane; k <= N; k += 64) {
+                double xk[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i) + al * AT(dX, k * NX + i);
+                if (k < N) {
+                    double u[NU], f[NX];
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
+                    Dyn<DYN>::f(xk, u, p.wheelbase, f);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        const double c = AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]);
+                        th += fabs(c);
+                        if (store) AT(rcd, k * NX + i) = keep * AT(rcd, k * NX + i) + c;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+                }
+                double d[MMAX];
+                knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
+                const double sk = AT(S, k) + al * AT(dS, k);
+                for (int j = 0; j < M; ++j) {
+                    const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
+                    const double c = d[j] + (dm.sd ? sk : 0.0) - t;
+                    th += fabs(c);
+                    if (store) AT(rcq, k * M + j) = keep * AT(rcq, k * M + j) + c;
+                    bar += log(t);
+                    lin += t;
+                }
+                if (dm.ns) {
+                    bar += log(sk);
+                    lin += sk;
                 }
             }
-        }
-        if (ok) {
-            int bad = 0;
-            for (int i = lane; i < nf; i += 64) {
-                const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
-                if (!(th <= ft || pht <= fp)) bad = 1;
+            *th_o = wsum(th);
+            const double fo = objective_w(p, dm, ws, b, lane, al);
+            *ph_o = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
+        };
+        // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint against reference values (rth, rph, rgd) with
+        // step size `at` for the switching condition / Armijo test
+        int rejf = 0;  // the last acceptance test failed on the filter after the sufficient-decrease test passed
+        auto acceptable = [&](double rth, double rph, double rgd, double at, double th, double pht, int* fa) {
+            int ok = isfinite(th) && isfinite(pht) && th <= SC(SC_THMAX);
+            const int ftype = rgd < 0 && at * pow(-rgd, sph) > delta * pow(rth, sth);
+            const int armijo = cmp_le(pht - rph, eta * at * rgd, rph);
+            if (ok) {
+                if (ftype && rth <= SC(SC_THMIN)) {
+                    ok = armijo;
+                } else {
+                    ok = cmp_le(th, (1.0 - gt) * rth, rth) || cmp_le(pht - rph, -gp * rth, rph);
+                    if (ok && pht > rph) {
+                        const double bas = fabs(rph) > 10.0 ? log10(fabs(rph)) : 1.0;
+                        if (log10(pht - rph) > 5.0 + bas) ok = 0;
+                    }
+                }
             }
-            ok = wmax((double)bad) == 0.0;
+            if (ok) {
+                int bad = 0;
+                for (int i = lane; i < nf; i += 64) {
+                    const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
+                    if (!(th <= ft || pht <= fp)) bad = 1;
+                }
+                ok = wmax((double)bad) == 0.0;
+                rejf = !ok;
+            } else {
+                rejf = 0;
+            }
+            *fa = ok && ftype && armijo;
+            return ok;
+        };
+        const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
+        double rth = theta, rph = phi, rgd = gd, at_fix = -1.0;
+        if (in_wd) {  // watchdog: the watchdog point's reference values and its alpha_max as the test step
+            rth = SC(SC_WDTH);
+            rph = SC(SC_WDPH);
+            rgd = SC(SC_WDGD);
+            at_fix = SC(SC_WDAT);
         }
-        }  // candidates
+        if (sock > 0) at_fix = SC(SC_SOCA);  // a corrected trial is tested with the original alpha
+        int ok = 0, fa = 0, cnd = 0;
+        double al = a0, th = 0, pht = 0;
+        int lastrej = (int)SC(SC_LASTREJF);
+        if (tiny) {
+            ok = 1;
+            al = SC(SC_AMAX);
+        } else {
+            for (cnd = 0; cnd < ncand && !ok; ++cnd) {
+                al = ldexp(a0, -cnd);
+                trial(al, rank0 + cnd, false, 0.0, &th, &pht);
+                ok = acceptable(rth, rph, rgd, at_fix >= 0 ? at_fix : al, th, pht, &fa);
+                if (!ok && sock == 0) lastrej = rejf;  // corrected trials do not count (as the oracle)
+            }
+        }
+        if (lane == 0) SC(SC_LASTREJF) = lastrej;
+        int next_round = 0;  // 1: emit the next backtracking round from SC_ALPHA; 2: PH_SOC
+        bool tentative = false;
+        wsync();
+        if (!ok) {
+            if (sock > 0) {  // a corrected trial was rejected
+                if (th > o.kappa_soc * SC(SC_SOCTH) || sock >= o.max_soc) {  // give up: the original step, halved
+                    double* buf = &AT(rcs, 0);
+                    res_io(ws, b, lane, buf, false);
+                    buf = &AT(sts, 0);
+                    step_io(ws, b, lane, buf, false);
+                    wsync();
+                    if (lane == 0) {
+                        SC(SC_SOCK) = 0;
+                        SC(SC_AZ) = SC(SC_SOCAZ);
+                        SC(SC_ALPHA) = 0.5 * SC(SC_SOCA);
+                        SC(SC_TRIALS) = 1;
+                    }
+                    next_round = 1;
+                } else {  // c_soc = alpha_soc c_soc + c(x + alpha_soc d_soc), solve again
+                    trial(a0, rank0, true, a0, &th, &pht);
+                    if (lane == 0) {
+                        SC(SC_SOCTH) = th;
+                        SC(SC_SOCK) = sock + 1;
+                    }
+                    next_round = 2;
+                }
+            } else if (in_wd) {
+                const int wt = (int)SC(SC_WDTRIAL) + 1;
+                if (wt > o.watchdog_trial_iter_max) {  // StopWatchDog: back to the watchdog point and direction
+                    double* buf = &AT(wdi, 0);
+                    iter_io(ws, b, lane, buf, false);
+                    buf = &AT(wdd, 0);
+                    step_io(ws, b, lane, buf, false);
+                    wsync();
+                    if (lane == 0) {
+                        SC(SC_WD) = 0;
+                        SC(SC_WDSHORT) = 0;
+                        SC(SC_LASTREJF) = 0;
+                        SC(SC_MU) = SC(SC_WDMU);
+                        SC(SC_TAU) = SC(SC_WDTAU);
+                        SC(SC_AMAX) = SC(SC_WDAT);
+                        SC(SC_AZ) = SC(SC_WDAZ);
+                        SC(SC_AMIN) = SC(SC_WDAMIN);
+                        SC(SC_THETA) = SC(SC_WDTH);
+                        SC(SC_PHI) = SC(SC_WDPH);
+                        SC(SC_GD) = SC(SC_WDGD);
+                        SC(SC_ALPHA) = 0.5 * SC(SC_WDAT);
+                        SC(SC_TRIALS) = 1;
+                    }
+                    next_round = 1;
+                } else {  // a tentative full step, accepted without the test
+                    if (lane == 0) SC(SC_WDTRIAL) = wt;
+                    ok = 1;
+                    tentative = true;
+                    al = SC(SC_AMAX);
+                    cnd = 1;
+                    fa = 0;
+                }
+            } else if ((int)SC(SC_TRIALS) == 0 && o.max_soc > 0 && th >= theta) {
+                // second-order correction of the rejected full step: save the step and the residuals, then
+                // c_soc = alpha c(x) + c(x + alpha d)
+                double* buf = &AT(sts, 0);
+                step_io(ws, b, lane, buf, true);
+                buf = &AT(rcs, 0);
+                res_io(ws, b, lane, buf, true);
+                wsync();
+                trial(a0, rank0, true, a0, &th, &pht);
+                if (lane == 0) {
+                    SC(SC_SOCAZ) = SC(SC_AZ);
+                    SC(SC_SOCA) = a0;
+                    SC(SC_SOCTH) = th;
+                    SC(SC_SOCK) = 1;
+                }
+                next_round = 2;
+            } else {
+                if (lane == 0) {
+                    SC(SC_ALPHA) = ldexp(a0, -ncand);
+                    SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
+                }
+                next_round = 1;
+            }
+        }
         wsync();
         if (ok) {
-            if (!(ftype && armijo) && lane == 0) {  // augment the filter: ((1-gt) theta, phi - gp theta)
+            // filter augmentation with the current point's values unless an f-type step met Armijo (or the
+            // step is tiny: IPOPT takes it without the filter)
+            // IPOPT filter reset heuristic (filter_reset_trigger 5, max_filter_resets 5): the filter is cleared
+            // when the last rejected trial of 5 successive line searches was rejected by the filter
+            if (!tiny && lane == 0 && SC(SC_NFRES) < 5) {
+                SC(SC_NFREJ) = lastrej ? SC(SC_NFREJ) + 1 : 0;
+                if (SC(SC_NFREJ) >= 5) {
+                    SC(SC_NFILT) = 0;
+                    SC(SC_NFRES) = SC(SC_NFRES) + 1;
+                    SC(SC_NFREJ) = 0;
+                }
+            }
+            if (!tiny && !fa && lane == 0) {
                 const double ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
+                const int nfc = (int)SC(SC_NFILT);
                 int w = 0;
-                for (int i = 0; i < nf; ++i) {
+                for (int i = 0; i < nfc; ++i) {
                     const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
                     if (!(ft >= ntv && fp >= npv)) {
                         AT(filt, 2 * w) = ft;
@@ -2412,17 +2718,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
             for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
             for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
-            ph = PH_EVAL;
+            const bool stop_tiny = tiny && SC(SC_TINYLAST) != 0.0;  // IPOPT STOP_AT_TINY_STEP
+            ph = stop_tiny ? PH_DONE : PH_EVAL;
             if (lane == 0) {
                 SC(SC_ITERS) = SC(SC_ITERS) + 1;
-                SC(SC_PHASE) = PH_EVAL;
-                SC(SC_ACCSLOT) = rank0 + cnd - 1;  // the loop stepped past the accepted candidate
+                SC(SC_PHASE) = ph;
+                if (stop_tiny) SC(SC_STATUS) = NLOT_TINY_STEP;
+                // the candidate the loop stepped past is the accepted one (no slot for a tiny step)
+                SC(SC_ACCSLOT) = tiny ? -1.0 : (double)(rank0 + cnd - 1);
+                if (in_wd && !tentative) SC(SC_WD) = 0;
+                if (!tiny) SC(SC_WDSHORT) = al < SC(SC_AMAX) ? SC(SC_WDSHORT) + 1 : 0;
+                SC(SC_SOCK) = 0;
+                SC(SC_TINYLAST) = tiny ? 1.0 : 0.0;
             }
             // corners of the new iterate, for the next step's full launch
             wsync();  // X complete
-            emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+            if (!stop_tiny) emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+        } else if (next_round == 2) {
+            ph = PH_SOC;
+            if (lane == 0) SC(SC_PHASE) = PH_SOC;
         } else {
-            const double na = ldexp(a0, -ncand);
+            const double na = SC(SC_ALPHA);
             if (na < SC(SC_AMIN)) {
                 ph = PH_DONE;
                 if (lane == 0) {
@@ -2430,10 +2746,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     SC(SC_PHASE) = PH_DONE;
                 }
             } else {
-                if (lane == 0) {
-                    SC(SC_ALPHA) = na;
-                    SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
-                }
                 emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
             }
         }
@@ -2493,7 +2805,16 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
     }
     for (int i = 0; i < p->nu; ++i)
         if (!(p->umin[i] < p->umax[i])) { set_error("control bounds must satisfy min < max"); return NLOT_ERR_INVALID; }
-    if (o->max_soc != 0) { set_error("max_soc > 0 is not implemented on the GPU path (DESIGN.md §4)"); return NLOT_ERR_INVALID; }
+    if (o->resto != 0 || o->soft_resto_pderror_reduction_factor > 0) {
+        set_error("the feasibility restoration phase (resto = 1, soft restoration) runs only in the CPU oracle; the GPU "
+                  "path ends an instance with NLOT_LS_FAILED where IPOPT would restore: pass resto = 0 and "
+                  "soft_resto_pderror_reduction_factor = 0 (DESIGN.md §4)");
+        return NLOT_ERR_INVALID;
+    }
+    if (o->max_soc < 0 || o->watchdog_shortened_iter_trigger < 0 || o->watchdog_trial_iter_max < 0) {
+        set_error("max_soc / watchdog options must be >= 0");
+        return NLOT_ERR_INVALID;
+    }
     if (o->mu_strategy != 0 && o->mu_strategy != 1) { set_error("mu_strategy: 0 monotone, 1 adaptive"); return NLOT_ERR_INVALID; }
     if (B <= 0 || B > (int64_t)1 << 26) { set_error("B out of range"); return NLOT_ERR_INVALID; }
     return NLOT_OK;

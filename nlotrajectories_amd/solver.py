@@ -28,7 +28,7 @@ def solve_batch(problem: Problem, x0, xg, mlp: Optional[DeviceMlp] = None, optio
     2 line-search failure, 3 numeric), iters [B]."""
     require_gpu()
     pc = problem.to_c()
-    opt = options or _abi.default_options()
+    opt = options or _abi.gpu_options()
     x0 = torch.as_tensor(x0, dtype=torch.float64, device=device).contiguous()
     xg = torch.as_tensor(xg, dtype=torch.float64, device=device).contiguous()
     B, nx = x0.shape

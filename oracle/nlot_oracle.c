@@ -558,8 +558,23 @@ typedef struct {
     double mu_max, af_f[FILT_MAX], af_th[FILT_MAX];
     double lin_resid; /* debug: max residual of the linear KKT system */
     double dc_used;   /* delta_c applied to the terminal block in the last solve */
+    /* ---- feasibility restoration problem (IPOPT MinC_1NrmRestorationPhase), active when resto = 1:
+     *   min rho sum(p + n) + zeta/2 ||D_R (x - x_R)||^2  s.t.  c(x) - p + n = 0,  p, n >= 0
+     * over every equality row (initial state, dynamics, terminal state, d(x) - t).  Row layout:
+     * [init nx][dynamics N*nx][terminal nc][inequality (N+1)*M]. */
+    int resto, ne;
+    int rej_filter, last_rej_filter, n_filt_rej, n_filt_resets; /* IPOPT filter reset heuristic (trigger 5, max 5) */
+    int n_soc_tried, n_soc_acc;                                  /* second-order corrections started / accepted */
+    double rho, zeta;
+    double *XR, *UR, *SR, *DRX, *DRU, *DRS; /* reference point and its proximity scaling */
+    double *rp, *rn, *rzp, *rzn;            /* p, n and their bound multipliers */
+    double *rdp, *rdn, *rdzp, *rdzn;        /* their steps */
+    double *Dsoft, *esoft;                  /* per row: compliance and offset of the soft equality */
     double *arena;
 } Sol;
+static int row_d(const Sol* s, int k, int i) { return s->nx + k * s->nx + i; }
+static int row_t(const Sol* s, int j) { return s->nx + s->N * s->nx + j; }
+static int row_q(const Sol* s, int q) { return s->nx + s->N * s->nx + s->nc + q; }
 
 static int nv_of(const Sol* s, int k) { return (k < s->N ? s->nu : 0) + s->ns; }
 
@@ -579,7 +594,11 @@ static int sol_alloc(Sol* s) {
     TAKE(cdef, N * nx) TAKE(dX, (N + 1) * nx) TAKE(dU, N * nu) TAKE(dS, (N + 1))                 \
     TAKE(dT, (N + 1) * M) TAKE(yi_n, nx) TAKE(yk_n, N * nx) TAKE(yt_n, CMAX)                     \
     TAKE(yd_n, (N + 1) * M) TAKE(dzl, N * nu) TAKE(dzu, N * nu) TAKE(dzs, (N + 1))               \
-    TAKE(dvt, (N + 1) * M) TAKE(rci, XMAX) TAKE(rcd, N * nx) TAKE(rct, CMAX) TAKE(rcq, (N + 1) * M)
+    TAKE(dvt, (N + 1) * M) TAKE(rci, XMAX) TAKE(rcd, N * nx) TAKE(rct, CMAX) TAKE(rcq, (N + 1) * M)         \
+    TAKE(XR, (N + 1) * nx) TAKE(UR, N * nu) TAKE(SR, N + 1) TAKE(DRX, (N + 1) * nx) TAKE(DRU, N * nu)           \
+    TAKE(DRS, N + 1) TAKE(rp, NE) TAKE(rn, NE) TAKE(rzp, NE) TAKE(rzn, NE) TAKE(rdp, NE) TAKE(rdn, NE)          \
+    TAKE(rdzp, NE) TAKE(rdzn, NE) TAKE(Dsoft, NE) TAKE(esoft, NE)
+    const int NE = nx + N * nx + CMAX + (N + 1) * M;
     ALLOCS
 #undef TAKE
     s->arena = (double*)calloc(n, sizeof(double));
@@ -615,6 +634,19 @@ static double objective(const Sol* s, const double* X, const double* U, const do
         f += p->smooth_weight * q;
     }
     return f;
+}
+
+/* Restoration objective rho sum(p + n) + zeta/2 ||D_R (x - x_R)||^2 over x = (X, U, S). */
+static double objective_resto(const Sol* s, const double* X, const double* U, const double* S, const double* p,
+                              const double* n) {
+    int nx = s->nx, nu = s->nu, N = s->N;
+    double a = 0, q = 0;
+    for (int i = 0; i < s->ne; ++i) a += p[i] + n[i];
+    for (int i = 0; i < (N + 1) * nx; ++i) q += pow(s->DRX[i] * (X[i] - s->XR[i]), 2);
+    for (int i = 0; i < N * nu; ++i) q += pow(s->DRU[i] * (U[i] - s->UR[i]), 2);
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) q += pow(s->DRS[k] * (S[k] - s->SR[k]), 2);
+    return s->rho * a + 0.5 * s->zeta * q;
 }
 
 /* Equality residuals c(x) (IPOPT sign) at a point; any output may be NULL. */
@@ -671,6 +703,51 @@ static void merit_r(const Sol* s, const double* X, const double* U, const double
     *theta = th;
     *phi = objective(s, X, U, S) - mu * bar + kappa_d * mu * lin;
 }
+/* Restoration merit at (x, t, p, n): theta_R = ||c(x) - p + n||_1 over every row (d - t included),
+ * phi_R = restoration objective - mu sum ln(bound slacks incl. p, n) + kappa_d mu sum(one-sided slacks). */
+static void merit_resto(const Sol* s, const double* X, const double* U, const double* S, const double* T,
+                        const double* pp, const double* nn, double mu, double* theta, double* phi, double* rci,
+                        double* rcd, double* rct, double* rcq) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double bi[XMAX], bt[CMAX];
+    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* bq = bd + N * nx;
+    if (!rci) rci = bi;
+    if (!rct) rct = bt;
+    if (!rcd) rcd = bd;
+    if (!rcq) rcq = bq;
+    residuals(s, X, U, S, T, rci, rcd, rct, rcq);
+    for (int i = 0; i < nx; ++i) rci[i] += -pp[i] + nn[i];
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nx; ++i) rcd[k * nx + i] += -pp[row_d(s, k, i)] + nn[row_d(s, k, i)];
+    for (int j = 0; j < s->nc; ++j) rct[j] += -pp[row_t(s, j)] + nn[row_t(s, j)];
+    for (int q = 0; q < (N + 1) * M; ++q) rcq[q] += -pp[row_q(s, q)] + nn[row_q(s, q)];
+    double th = 0, bar = 0, lin = 0;
+    for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
+    for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
+    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        th += fabs(rcq[q]);
+        bar += log(T[q]);
+        lin += T[q];
+    }
+    free(bd);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) {
+            bar += log(S[k]);
+            lin += S[k];
+        }
+    for (int i = 0; i < s->ne; ++i) {
+        bar += log(pp[i]) + log(nn[i]);
+        lin += pp[i] + nn[i];
+    }
+    *theta = th;
+    *phi = objective_resto(s, X, U, S, pp, nn) - mu * bar + 1e-5 * mu * lin;
+}
+
 static void merit(const Sol* s, const double* X, const double* U, const double* S, const double* T, double mu,
                   double* theta, double* phi, double* fout) {
     merit_r(s, X, U, S, T, mu, theta, phi, NULL, NULL, NULL, NULL);
@@ -713,6 +790,17 @@ static void eval_full(Sol* s) {
     }
     for (int i = 0; i < nx; ++i) s->rci[i] = s->X[i] - s->x0[i];
     for (int j = 0; j < s->nc; ++j) s->rct[j] = s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]];
+    if (s->resto) { /* c(x) - p + n, and the restoration objective's gradient (no path-length terms) */
+        for (int i = 0; i < nx; ++i) s->rci[i] += -s->rp[i] + s->rn[i];
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nx; ++i) s->rcd[k * nx + i] += -s->rp[row_d(s, k, i)] + s->rn[row_d(s, k, i)];
+        for (int j = 0; j < s->nc; ++j) s->rct[j] += -s->rp[row_t(s, j)] + s->rn[row_t(s, j)];
+        s->f = objective_resto(s, s->X, s->U, s->S, s->rp, s->rn);
+        for (int i = 0; i < (N + 1) * nx; ++i) s->gX[i] = s->zeta * s->DRX[i] * s->DRX[i] * (s->X[i] - s->XR[i]);
+        for (int i = 0; i < N * nu; ++i) s->gU[i] = s->zeta * s->DRU[i] * s->DRU[i] * (s->U[i] - s->UR[i]);
+        for (int k = 0; k <= N; ++k) s->gS[k] = s->ns ? s->zeta * s->DRS[k] * s->DRS[k] * (s->S[k] - s->SR[k]) : 0.0;
+        memset(s->Gs, 0, sizeof(double) * 4 * N);
+    }
     for (int k = 0; k <= N; ++k) {
         jet d[NLOT_MAX_BODY];
         knot_ineq(p, s->m, s->X + k * nx, 1, d);
@@ -721,6 +809,7 @@ static void eval_full(Sol* s) {
         for (int j = 0; j < M; ++j) {
             s->dv[k * M + j] = d[j].v + (s->sd ? s->S[k] : 0.0);
             s->rcq[k * M + j] = s->dv[k * M + j] - s->T[k * M + j];
+            if (s->resto) s->rcq[k * M + j] += -s->rp[row_q(s, k * M + j)] + s->rn[row_q(s, k * M + j)];
             for (int a = 0; a < 3; ++a) s->Jd[(k * M + j) * 3 + a] = d[j].g[a];
             double w = s->yd[k * M + j];
             for (int a = 0; a < 3; ++a)
@@ -735,14 +824,26 @@ typedef struct {
     /* for the quality-function mu oracle (IpQualityFunctionMuOracle, 2-norm-squared) */
     double dual_sq, primal_sq, avg_compl;
     int n_dual, n_pri, n_comp;
+    /* 1-norms for the primal-dual system error of the soft restoration phase */
+    double dual_1, primal_1, complmu_1;
 } Errs;
 
+/* The residual arrays rci/rcd/rct/rcq must hold c(x) (minus p plus n in the restoration problem), as
+ * eval_full leaves them. */
 static void errors(const Sol* s, Errs* e) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0;
-    double dsq = 0, psq = 0, csum = 0;
+    double dsq = 0, psq = 0, csum = 0, d1 = 0, p1 = 0, c1 = 0;
     int ny = 0, nzc = 0, ndual = 0, npri = 0;
+#define DUAL(v)                                                                                  \
+    do {                                                                                         \
+        double vv = (v);                                                                         \
+        dual = fmax(dual, fabs(vv));                                                             \
+        dsq += vv * vv;                                                                          \
+        d1 += fabs(vv);                                                                          \
+        ndual++;                                                                                 \
+    } while (0)
     /* dual infeasibility: grad L over x, u, s, t */
     for (int k = 0; k <= N; ++k) {
         double r[XMAX];
@@ -761,33 +862,20 @@ static void errors(const Sol* s, Errs* e) {
             for (int j = 0; j < s->nc; ++j) r[s->tidx[j]] += s->yt[j];
         for (int j = 0; j < M; ++j)
             for (int a = 0; a < 3; ++a) r[a] += s->Jd[(k * M + j) * 3 + a] * s->yd[k * M + j];
-        for (int i = 0; i < nx; ++i) {
-            dual = fmax(dual, fabs(r[i]));
-            dsq += r[i] * r[i];
-            ndual++;
-        }
+        for (int i = 0; i < nx; ++i) DUAL(r[i]);
         if (k < N)
             for (int i = 0; i < nu; ++i) {
                 double t = s->gU[k * nu + i] - s->zl[k * nu + i] + s->zu[k * nu + i];
                 for (int a = 0; a < nx; ++a) t -= s->B[k * nx * nu + a * nu + i] * s->yk[k * nx + a];
-                dual = fmax(dual, fabs(t));
-                dsq += t * t;
-                ndual++;
+                DUAL(t);
             }
         if (s->ns) {
             double t = s->gS[k] - s->zs[k];
             if (s->sd)
                 for (int j = 0; j < M; ++j) t += s->yd[k * M + j];
-            dual = fmax(dual, fabs(t));
-            dsq += t * t;
-            ndual++;
+            DUAL(t);
         }
-        for (int j = 0; j < M; ++j) {
-            double t = -s->yd[k * M + j] - s->vt[k * M + j];
-            dual = fmax(dual, fabs(t));
-            dsq += t * t;
-            ndual++;
-        }
+        for (int j = 0; j < M; ++j) DUAL(-s->yd[k * M + j] - s->vt[k * M + j]);
     }
     /* primal infeasibility (c, d - t) and unscaled constraint violation */
 #define PRI(v)                                                                                   \
@@ -795,18 +883,17 @@ static void errors(const Sol* s, Errs* e) {
         double vv = (v);                                                                         \
         primal = fmax(primal, fabs(vv));                                                         \
         psq += vv * vv;                                                                          \
+        p1 += fabs(vv);                                                                          \
         npri++;                                                                                  \
     } while (0)
-    for (int i = 0; i < nx; ++i) PRI(s->X[i] - s->x0[i]);
-    for (int j = 0; j < s->nc; ++j) PRI(s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]]);
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nx; ++i) PRI(s->X[(k + 1) * nx + i] - s->F[k * nx + i]);
+    for (int i = 0; i < nx; ++i) PRI(s->rci[i]);
+    for (int j = 0; j < s->nc; ++j) PRI(s->rct[j]);
+    for (int i = 0; i < N * nx; ++i) PRI(s->rcd[i]);
     cviol = primal;
-    for (int k = 0; k <= N; ++k)
-        for (int j = 0; j < M; ++j) {
-            PRI(s->dv[k * M + j] - s->T[k * M + j]);
-            cviol = fmax(cviol, fmax(0.0, -s->dv[k * M + j]));
-        }
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        PRI(s->rcq[q]);
+        cviol = fmax(cviol, fmax(0.0, -s->dv[q]));
+    }
 #undef PRI
     /* complementarity */
 #define COMPL(z, sl)                                                                             \
@@ -814,6 +901,7 @@ static void errors(const Sol* s, Errs* e) {
         double zz = (z), ss = (sl);                                                              \
         c0 = fmax(c0, fabs(zz * ss));                                                            \
         cmu = fmax(cmu, fabs(zz * ss - s->mu));                                                  \
+        c1 += fabs(zz * ss - s->mu);                                                             \
         csum += zz * ss;                                                                         \
         zsum += fabs(zz);                                                                        \
         nzc++;                                                                                   \
@@ -827,7 +915,19 @@ static void errors(const Sol* s, Errs* e) {
         for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k]);
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < M; ++j) COMPL(s->vt[k * M + j], s->T[k * M + j]);
+    if (s->resto) /* p and n rows: rho -+ y - z = 0, z p = mu, z n = mu */
+        for (int i = 0; i < s->ne; ++i) {
+            double y = i < nx ? s->yi[i]
+                       : i < row_t(s, 0) ? s->yk[i - nx]
+                       : i < row_q(s, 0) ? s->yt[i - row_t(s, 0)]
+                                         : s->yd[i - row_q(s, 0)];
+            DUAL(s->rho - y - s->rzp[i]);
+            DUAL(s->rho + y - s->rzn[i]);
+            COMPL(s->rzp[i], s->rp[i]);
+            COMPL(s->rzn[i], s->rn[i]);
+        }
 #undef COMPL
+#undef DUAL
     for (int i = 0; i < nx; ++i) ysum += fabs(s->yi[i]);
     for (int i = 0; i < N * nx; ++i) ysum += fabs(s->yk[i]);
     for (int j = 0; j < s->nc; ++j) ysum += fabs(s->yt[j]);
@@ -847,6 +947,16 @@ static void errors(const Sol* s, Errs* e) {
     e->n_pri = npri;
     e->n_comp = nzc;
     e->avg_compl = nzc ? csum / nzc : 0.0;
+    e->dual_1 = d1;
+    e->primal_1 = p1;
+    e->complmu_1 = c1;
+}
+
+/* IPOPT's primal-dual system error (soft restoration phase): mean absolute residual of the primal-dual
+ * system at barrier parameter mu, sum of 1-norms / element count.  errors() must have run with s->mu =
+ * the mu wanted. */
+static double pd_error(const Errs* e) {
+    return (e->dual_1 + e->primal_1 + e->complmu_1) / (double)(e->n_dual + e->n_pri + e->n_comp);
 }
 
 /* ============================================================================================ */
@@ -881,9 +991,16 @@ static void build(Sol* s, int mode, double dw) {
                     if (k < N) HH(a, b) += s->Gs[4 * k + 2 * a + b];
                     if (k > 0) HH(a, b) += s->Gs[4 * (k - 1) + 2 * a + b];
                 }
-            if (p->use_slack) HH(is, is) += 2.0 * p->slack_penalty;
-            if (p->use_smooth && k < N - 1)
-                for (int i = 0; i < nu; ++i) HH(iu + i, iu + i) += 2.0 * p->smooth_weight;
+            if (s->resto) { /* restoration objective: zeta D_R^2 (its only curvature besides the constraints) */
+                for (int i = 0; i < nx; ++i) HH(i, i) += s->zeta * s->DRX[k * nx + i] * s->DRX[k * nx + i];
+                if (k < N)
+                    for (int i = 0; i < nu; ++i) HH(iu + i, iu + i) += s->zeta * s->DRU[k * nu + i] * s->DRU[k * nu + i];
+                if (s->ns) HH(is, is) += s->zeta * s->DRS[k] * s->DRS[k];
+            } else {
+                if (p->use_slack) HH(is, is) += 2.0 * p->slack_penalty;
+                if (p->use_smooth && k < N - 1)
+                    for (int i = 0; i < nu; ++i) HH(iu + i, iu + i) += 2.0 * p->smooth_weight;
+            }
             /* dynamics constraint c_k = x_{k+1} - F_k: W += -sum_i y_i d2F_i */
             if (k < N)
                 for (int a = 0; a < nzd; ++a)
@@ -918,7 +1035,17 @@ static void build(Sol* s, int mode, double dw) {
             if (s->sd) J[is] = 1.0;
             double D, rhs;
             double t = s->T[k * M + j], v = s->vt[k * M + j];
-            if (mode == MODE_NEWTON) {
+            if (mode == MODE_NEWTON && s->resto) {
+                /* t, p and n of the row eliminated: y~ = (J dz + r - E) / C (restoration) */
+                const int r = row_q(s, k * M + j);
+                const double pp = s->rp[r], nn = s->rn[r], st = v / t + dw;
+                const double sp = s->rzp[r] / pp + dw, sn = s->rzn[r] / nn + dw;
+                const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+                const double E = (mu / t - kappa_d * mu) / st + (mu / pp - s->rho - kappa_d * mu) / sp -
+                                 (mu / nn - s->rho - kappa_d * mu) / sn;
+                D = 1.0 / C;
+                rhs = (s->rcq[k * M + j] - E) / C;
+            } else if (mode == MODE_NEWTON) {
                 D = v / t + dw;
                 rhs = D * s->rcq[k * M + j] + (-mu / t + kappa_d * mu);
             } else {
@@ -933,10 +1060,18 @@ static void build(Sol* s, int mode, double dw) {
 #undef HH
     }
     if (mode == MODE_NEWTON) {
-        for (int i = 0; i < nx; ++i) s->dx0[i] = -s->rci[i];
-        for (int j = 0; j < s->nc; ++j) s->rN[j] = -s->rct[j];
+        if (s->resto) /* soft equality rows: J dz - D y~ = -r + e (p, n eliminated) */
+            for (int i = 0; i < row_q(s, 0); ++i) {
+                const double pp = s->rp[i], nn = s->rn[i];
+                const double sp = s->rzp[i] / pp + dw, sn = s->rzn[i] / nn + dw;
+                s->Dsoft[i] = 1.0 / sp + 1.0 / sn;
+                s->esoft[i] = (mu / pp - s->rho - kappa_d * mu) / sp - (mu / nn - s->rho - kappa_d * mu) / sn;
+            }
+        for (int i = 0; i < nx; ++i) s->dx0[i] = -s->rci[i] + (s->resto ? s->esoft[i] : 0.0);
+        for (int j = 0; j < s->nc; ++j) s->rN[j] = -s->rct[j] + (s->resto ? s->esoft[row_t(s, j)] : 0.0);
         for (int k = 0; k < N; ++k)
-            for (int i = 0; i < nx; ++i) s->cdef[k * nx + i] = -s->rcd[k * nx + i];
+            for (int i = 0; i < nx; ++i)
+                s->cdef[k * nx + i] = -s->rcd[k * nx + i] + (s->resto ? s->esoft[row_d(s, k, i)] : 0.0);
     } else {
         memset(s->dx0, 0, sizeof s->dx0);
         memset(s->rN, 0, sizeof s->rN);
@@ -948,9 +1083,66 @@ static void build(Sol* s, int mode, double dw) {
 static void cross(const Sol* s, int mode, int k, double* Mk) {
     int nx = s->nx;
     memset(Mk, 0, sizeof(double) * XMAX * XMAX);
-    if (mode != MODE_NEWTON) return;
+    if (mode != MODE_NEWTON || s->resto) return; /* the restoration objective has no path-length term */
     for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) Mk[a * nx + b] = -s->Gs[4 * k + 2 * a + b];
+}
+
+/* Restoration rows (p, n eliminated) make the dynamics / initial-state equalities soft: x' = y + w with
+ * cost 1/2 w' D^{-1} w.  Minimising the value function (P, p + G nu, Psi, psi) of x' over w gives the
+ * value function of y:  P <- (I + P D)^{-1} P,  [p | G] <- (I + P D)^{-1} [p | G],
+ * Psi -= G' D (I + P D)^{-1} G,  psi -= G' D (I + P D)^{-1} p,  computed through the symmetric
+ * K = I + S P S (S = D^{1/2}): (I + P D)^{-1} X = S^{-1} K^{-1} S X,  D (I + P D)^{-1} = S K^{-1} S.
+ * Returns 1 if K is not positive definite (D^{-1} + P indefinite: wrong inertia). */
+static int soft_transform(int nx, int nc, const double* D, double* P, double* pv, double* G, double* Psi,
+                          double* psi) {
+    double S[XMAX], K[XMAX * XMAX], Z[XMAX * (XMAX + 1 + CMAX)];
+    int perm[XMAX], nneg, m = nx + 1 + nc;
+    for (int i = 0; i < nx; ++i) S[i] = sqrt(D[i]);
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j) K[i * nx + j] = (i == j ? 1.0 : 0.0) + S[i] * P[i * nx + j] * S[j];
+    if (ldl(K, nx, perm, &nneg) || nneg) return 1;
+    for (int i = 0; i < nx; ++i) {
+        for (int j = 0; j < nx; ++j) Z[i * m + j] = S[i] * P[i * nx + j];
+        Z[i * m + nx] = S[i] * pv[i];
+        for (int c = 0; c < nc; ++c) Z[i * m + nx + 1 + c] = S[i] * G[i * nc + c];
+    }
+    ldl_solve(K, nx, perm, Z, m); /* Z = K^{-1} S [P | p | G] */
+    for (int a = 0; a < nc; ++a) {
+        double t = 0;
+        for (int r = 0; r < nx; ++r) t += S[r] * G[r * nc + a] * Z[r * m + nx];
+        psi[a] -= t;
+        for (int b = 0; b < nc; ++b) {
+            double u = 0;
+            for (int r = 0; r < nx; ++r) u += S[r] * G[r * nc + a] * Z[r * m + nx + 1 + b];
+            Psi[a * nc + b] -= u;
+        }
+    }
+    for (int i = 0; i < nx; ++i) {
+        for (int j = 0; j < nx; ++j) P[i * nx + j] = Z[i * m + j] / S[i];
+        pv[i] = Z[i * m + nx] / S[i];
+        for (int c = 0; c < nc; ++c) G[i * nc + c] = Z[i * m + nx + 1 + c] / S[i];
+    }
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < i; ++j) P[i * nx + j] = P[j * nx + i] = 0.5 * (P[i * nx + j] + P[j * nx + i]);
+    return 0;
+}
+/* x' = y + w* = S K^{-1} (S^{-1} y - S (p + G nu)) for the value function (P, p, G) of x' (untransformed). */
+static void soft_forward(int nx, int nc, const double* D, const double* P, const double* pv, const double* G,
+                         const double* nu, const double* y, double* xo) {
+    double S[XMAX], K[XMAX * XMAX], r[XMAX];
+    int perm[XMAX], nneg;
+    for (int i = 0; i < nx; ++i) S[i] = sqrt(D[i]);
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j) K[i * nx + j] = (i == j ? 1.0 : 0.0) + S[i] * P[i * nx + j] * S[j];
+    ldl(K, nx, perm, &nneg);
+    for (int i = 0; i < nx; ++i) {
+        double q = pv[i];
+        for (int c = 0; c < nc; ++c) q += G[i * nc + c] * nu[c];
+        r[i] = y[i] / S[i] - S[i] * q;
+    }
+    ldl_solve(K, nx, perm, r, 1);
+    for (int i = 0; i < nx; ++i) xo[i] = S[i] * r[i];
 }
 
 /* Backward Riccati + terminal multiplier + forward sweep.  Returns 0, or 1 for wrong inertia. */
@@ -1003,6 +1195,7 @@ static int riccati(Sol* s, int mode) {
                 gp[i] += Mc[i];
             }
         }
+        if (s->resto && k < N && soft_transform(nx, nc, s->Dsoft + row_d(s, k, 0), Pn, pn, Gn, Psi, psi)) return 1;
         /* Q = H' + [A B]' P [A B] ; q = g' + [A B]'(P c + p) */
         double AB[XMAX * ZMAX], PAB[XMAX * ZMAX], Pcp[XMAX];
         for (int i = 0; i < nx; ++i) {
@@ -1044,6 +1237,7 @@ static int riccati(Sol* s, int mode) {
              * stage block; with Psi_0 below this gives the exact inertia of the Newton matrix. */
             int perm[VMAX], nneg;
             if (ldl(L, nv, perm, &nneg)) return 1; /* singular stage block */
+            if (s->resto && nneg) return 1;        /* every constraint is soft: the Hessian must be PD */
             negsum += nneg;
             if (negsum > nc) return 1; /* more negatives than the terminal block can absorb */
             for (int i = 0; i < nv; ++i) {
@@ -1108,7 +1302,20 @@ static int riccati(Sol* s, int mode) {
     /* terminal multiplier: -Psi_0 nu = Gamma_0' dx0 + psi_0 (IPOPT delta_c if singular) */
     double nu_[CMAX];
     s->dc_used = 0.0;
-    if (nc) {
+    if (s->resto && soft_transform(nx, nc, s->Dsoft, Pn, pn, Gn, Psi, psi)) return 1; /* soft initial state */
+    if (s->resto) { /* soft terminal rows: (-Psi + D_t) nu = Gamma' dx0 + psi, positive definite */
+        double L[CMAX * CMAX];
+        int perm[CMAX], nneg;
+        for (int i = 0; i < nc * nc; ++i) L[i] = -Psi[i];
+        for (int i = 0; i < nc; ++i) L[i * nc + i] += s->Dsoft[row_t(s, i)];
+        if (ldl(L, nc, perm, &nneg) || nneg) return 1;
+        for (int c = 0; c < nc; ++c) {
+            double t = psi[c];
+            for (int r = 0; r < nx; ++r) t += Gn[r * nc + c] * s->dx0[r];
+            nu_[c] = t;
+        }
+        ldl_solve(L, nc, perm, nu_, 1);
+    } else if (nc) {
         /* inertia (Sylvester over the Riccati eliminations): the Newton matrix has the wanted
          * inertia iff #neg(Psi_0) = nc - sum_k #neg(Q_vv,k) and Psi_0 is nonsingular. */
         double L[CMAX * CMAX];
@@ -1137,6 +1344,7 @@ static int riccati(Sol* s, int mode) {
     /* forward sweep */
     double dx[XMAX];
     memcpy(dx, s->dx0, sizeof(double) * nx);
+    if (s->resto) soft_forward(nx, nc, s->Dsoft, s->Pm, s->pv, s->Gm, nu_, s->dx0, dx);
     for (int k = 0; k <= N; ++k) {
         int nv = nv_of(s, k);
         const double *Kk = s->Kf + (size_t)k * VMAX * XMAX, *kk = s->kf + (size_t)k * VMAX,
@@ -1169,6 +1377,12 @@ static int riccati(Sol* s, int mode) {
                 for (int j = 0; j < nx; ++j) t += Ak[i * nx + j] * dx[j];
                 for (int j = 0; j < nu; ++j) t += s->B[(size_t)k * nx * nu + i * nu + j] * dvv[j];
                 dn[i] = t;
+            }
+            if (s->resto) { /* soft dynamics: dx_{k+1} = y + w* */
+                double y_[XMAX];
+                memcpy(y_, dn, sizeof(double) * nx);
+                soft_forward(nx, nc, s->Dsoft + row_d(s, k, 0), s->Pm + (size_t)(k + 1) * XMAX * XMAX,
+                             s->pv + (size_t)(k + 1) * XMAX, s->Gm + (size_t)(k + 1) * XMAX * CMAX, nu_, y_, dn);
             }
             /* dynamics multiplier y_k = -grad V_{k+1}(dx_{k+1}) - M_k' dx_k */
             const double *P = s->Pm + (size_t)(k + 1) * XMAX * XMAX, *pp = s->pv + (size_t)(k + 1) * XMAX,
@@ -1244,12 +1458,22 @@ static double linear_residual(Sol* s, int mode) {
     return res;
 }
 
-/* Recover dt, yd+, dz from the primal step (Newton mode). */
+/* Recover dt, yd+, dz from the primal step (Newton mode); in the restoration problem also dp, dn, dzp, dzn. */
 static void recover(Sol* s, double dw) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     const double kappa_d = 1e-5;
     double mu = s->mu;
+    /* p, n of one restoration row given its new multiplier y~ */
+    #define PN_STEP(r, yn)                                                                                 \
+    do {                                                                                                   \
+        const double pp_ = s->rp[r], nn_ = s->rn[r];                                                       \
+        const double sp_ = s->rzp[r] / pp_ + dw, sn_ = s->rzn[r] / nn_ + dw;                               \
+        s->rdp[r] = ((yn) - s->rho - kappa_d * mu + mu / pp_) / sp_;                                       \
+        s->rdn[r] = (-(yn) - s->rho - kappa_d * mu + mu / nn_) / sn_;                                      \
+        s->rdzp[r] = mu / pp_ - s->rzp[r] - (s->rzp[r] / pp_) * s->rdp[r];                                 \
+        s->rdzn[r] = mu / nn_ - s->rzn[r] - (s->rzn[r] / nn_) * s->rdn[r];                                 \
+    } while (0)
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < M; ++j) {
             int q = k * M + j;
@@ -1257,11 +1481,31 @@ static void recover(Sol* s, double dw) {
             for (int a = 0; a < 3 && a < nx; ++a) Jdz += s->Jd[q * 3 + a] * s->dX[k * nx + a];
             if (s->sd) Jdz += s->dS[k];
             double t = s->T[q], v = s->vt[q];
-            double dt = Jdz + s->rcq[q];
-            s->dT[q] = dt;
-            s->yd_n[q] = (v / t + dw) * dt + (-mu / t + kappa_d * mu);
-            s->dvt[q] = mu / t - v - (v / t) * dt;
+            if (s->resto) {
+                const int r = row_q(s, q);
+                const double pp = s->rp[r], nn = s->rn[r], st = v / t + dw;
+                const double sp = s->rzp[r] / pp + dw, sn = s->rzn[r] / nn + dw;
+                const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+                const double E = (mu / t - kappa_d * mu) / st + (mu / pp - s->rho - kappa_d * mu) / sp -
+                                 (mu / nn - s->rho - kappa_d * mu) / sn;
+                const double yn = (Jdz + s->rcq[q] - E) / C;
+                s->yd_n[q] = yn;
+                s->dT[q] = (yn + mu / t - kappa_d * mu) / st;
+                PN_STEP(r, yn);
+            } else {
+                double dt = Jdz + s->rcq[q];
+                s->dT[q] = dt;
+                s->yd_n[q] = (v / t + dw) * dt + (-mu / t + kappa_d * mu);
+            }
+            s->dvt[q] = mu / t - v - (v / t) * s->dT[q];
         }
+    if (s->resto) {
+        for (int i = 0; i < nx; ++i) PN_STEP(i, s->yi_n[i]);
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nx; ++i) PN_STEP(row_d(s, k, i), s->yk_n[k * nx + i]);
+        for (int j = 0; j < s->nc; ++j) PN_STEP(row_t(s, j), s->yt_n[j]);
+    }
+    #undef PN_STEP
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
@@ -1331,7 +1575,12 @@ static int ls_accept(const Sol* s, double theta, double phi, double gd, double a
             if (log10(pht - phi) > 5.0 + bas) ok = 0;
         }
     }
-    if (ok) ok = filter_ok(s, tht, pht);
+    if (ok) {
+        ok = filter_ok(s, tht, pht);
+        ((Sol*)s)->rej_filter = !ok; /* rejected by the filter after the sufficient-decrease test passed */
+    } else {
+        ((Sol*)s)->rej_filter = 0;
+    }
     if (ok) *armijo_ftype = ftype && armijo;
     return ok;
 }
@@ -1349,6 +1598,11 @@ static double primal_frac(const Sol* s, double tau) {
     if (s->ns)
         for (int k = 0; k <= N; ++k) a = frac_to_bound(s->S[k], s->dS[k], tau, a);
     for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->T[q], s->dT[q], tau, a);
+    if (s->resto)
+        for (int i = 0; i < s->ne; ++i) {
+            a = frac_to_bound(s->rp[i], s->rdp[i], tau, a);
+            a = frac_to_bound(s->rn[i], s->rdn[i], tau, a);
+        }
     return a;
 }
 static double dual_frac(const Sol* s, double tau) {
@@ -1361,6 +1615,11 @@ static double dual_frac(const Sol* s, double tau) {
     if (s->ns)
         for (int k = 0; k <= N; ++k) a = frac_to_bound(s->zs[k], s->dzs[k], tau, a);
     for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->vt[q], s->dvt[q], tau, a);
+    if (s->resto)
+        for (int i = 0; i < s->ne; ++i) {
+            a = frac_to_bound(s->rzp[i], s->rdzp[i], tau, a);
+            a = frac_to_bound(s->rzn[i], s->rdzn[i], tau, a);
+        }
     return a;
 }
 /* save (dir=0) / restore (dir=1) the full step */
@@ -1531,13 +1790,250 @@ static double qf_sigma(Sol* s, const QfCtx* q, double mu_min, double mu_max) {
     return qf_golden(s, q, sig_1m, q_1m, fmax(sig_lo, 1e-300), -1.0, 1);
 }
 
-/* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
- * seen, [4] = final mu, [5] = E_0 (scaled overall error) */
-int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
-                     const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
-                     int* iters_out, double* info) {
-    Sol sol, *s = &sol;
-    memset(s, 0, sizeof sol);
+/* ============================================================================================ */
+/* Globalisation safeguards of IPOPT's BacktrackingLineSearch (restated):           */
+/* second-order correction, watchdog, soft restoration, tiny-step test, and the feasibility       */
+/* restoration phase (MinC_1NrmRestorationPhase).                                                 */
+/* ============================================================================================ */
+/* iterate (primal + equality/bound multipliers; restoration p, n, zp, zn) save (dir 0) / load (dir 1) */
+static int iter_len(const Sol* s) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX + 4 * s->ne;
+}
+static void iter_io(Sol* s, double* buf, int dir) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double* arrs[] = {s->X, s->U, s->S, s->T, s->yi, s->yk, s->yt, s->yd, s->zl, s->zu, s->zs, s->vt,
+                      s->rp, s->rn, s->rzp, s->rzn};
+    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1,
+                  (N + 1) * M, s->ne, s->ne, s->ne, s->ne};
+    for (int i = 0; i < 16; ++i) {
+        if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
+        else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
+        buf += lens[i];
+    }
+}
+
+typedef struct { /* trial point buffers */
+    double *X, *U, *S, *T, *P, *N;
+} Trial;
+
+static void trial_primal(const Sol* s, double a, Trial* t) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    for (int i = 0; i < (N + 1) * nx; ++i) t->X[i] = s->X[i] + a * s->dX[i];
+    for (int i = 0; i < N * nu; ++i) t->U[i] = s->U[i] + a * s->dU[i];
+    for (int k = 0; k <= N; ++k) t->S[k] = s->S[k] + a * s->dS[k];
+    for (int q = 0; q < (N + 1) * M; ++q) t->T[q] = s->T[q] + a * s->dT[q];
+    if (s->resto)
+        for (int i = 0; i < s->ne; ++i) {
+            t->P[i] = s->rp[i] + a * s->rdp[i];
+            t->N[i] = s->rn[i] + a * s->rdn[i];
+        }
+}
+static void trial_merit(const Sol* s, const Trial* t, double mu, double* th, double* ph, double* rci, double* rcd,
+                        double* rct, double* rcq) {
+    if (s->resto) merit_resto(s, t->X, t->U, t->S, t->T, t->P, t->N, mu, th, ph, rci, rcd, rct, rcq);
+    else merit_r(s, t->X, t->U, t->S, t->T, mu, th, ph, rci, rcd, rct, rcq);
+}
+
+/* accept the trial point: primal (and equality multipliers, IPOPT alpha_for_y = primal) with alpha, bound
+ * multipliers with alpha_z and the kappa_Sigma safeguard */
+static void accept_step(Sol* s, double al, double az, const Trial* t) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    const double mu = s->mu, ks = 1e10;
+    memcpy(s->X, t->X, sizeof(double) * (N + 1) * nx);
+    memcpy(s->U, t->U, sizeof(double) * N * nu);
+    memcpy(s->S, t->S, sizeof(double) * (N + 1));
+    memcpy(s->T, t->T, sizeof(double) * (N + 1) * M);
+    for (int i = 0; i < nx; ++i) s->yi[i] += al * (s->yi_n[i] - s->yi[i]);
+    for (int i = 0; i < N * nx; ++i) s->yk[i] += al * (s->yk_n[i] - s->yk[i]);
+    for (int i = 0; i < s->nc; ++i) s->yt[i] += al * (s->yt_n[i] - s->yt[i]);
+    for (int i = 0; i < (N + 1) * M; ++i) s->yd[i] += al * (s->yd_n[i] - s->yd[i]);
+#define ZUPD(z, dz, sl)                                                                          \
+    do {                                                                                         \
+        double zn = (z) + az * (dz), sv = (sl);                                                  \
+        zn = fmax(fmin(zn, ks * mu / sv), mu / (ks * sv));                                       \
+        (z) = zn;                                                                                \
+    } while (0)
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int q = k * nu + i;
+            ZUPD(s->zl[q], s->dzl[q], s->U[q] - p->umin[i]);
+            ZUPD(s->zu[q], s->dzu[q], p->umax[i] - s->U[q]);
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k]);
+    for (int q = 0; q < (N + 1) * M; ++q) ZUPD(s->vt[q], s->dvt[q], s->T[q]);
+    if (s->resto) {
+        memcpy(s->rp, t->P, sizeof(double) * s->ne);
+        memcpy(s->rn, t->N, sizeof(double) * s->ne);
+        for (int i = 0; i < s->ne; ++i) {
+            ZUPD(s->rzp[i], s->rdzp[i], s->rp[i]);
+            ZUPD(s->rzn[i], s->rdzn[i], s->rn[i]);
+        }
+    }
+#undef ZUPD
+}
+
+/* directional derivative of the barrier merit along the step (IPOPT gradBarrTDelta) */
+static double barrier_gd(const Sol* s) {
+    const NlotProblem* p = s->p;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    const double kappa_d = 1e-5, mu = s->mu;
+    double gd = 0;
+    for (int i = 0; i < (N + 1) * nx; ++i) gd += s->gX[i] * s->dX[i];
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int q = k * nu + i;
+            gd += (s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) gd += (s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
+    for (int q = 0; q < (N + 1) * M; ++q) gd += (-mu / s->T[q] + kappa_d * mu) * s->dT[q];
+    if (s->resto)
+        for (int i = 0; i < s->ne; ++i)
+            gd += (s->rho + kappa_d * mu - mu / s->rp[i]) * s->rdp[i] + (s->rho + kappa_d * mu - mu / s->rn[i]) * s->rdn[i];
+    return gd;
+}
+
+/* Newton step with IPOPT's inertia correction (delta_w); 0 ok, 1 failed */
+static int newton_step(Sol* s, double* dw_out) {
+    double dw = 0.0;
+    build(s, MODE_NEWTON, dw);
+    if (riccati(s, MODE_NEWTON)) {
+        dw = s->dw_last == 0.0 ? 1e-4 : fmax(1e-20, s->dw_last / 3.0);
+        for (;;) {
+            build(s, MODE_NEWTON, dw);
+            if (!riccati(s, MODE_NEWTON)) break;
+            dw *= (s->dw_last == 0.0) ? 100.0 : 8.0;
+            if (dw > 1e40) return 1;
+        }
+        s->dw_last = dw;
+    }
+    *dw_out = dw;
+    return 0;
+}
+
+typedef struct { /* line-search reference values (the current point, or the watchdog's) */
+    double theta, phi, gd, alpha_test;
+    int fixed_test; /* 1: acceptance uses alpha_test instead of the trial's alpha (watchdog) */
+} LsRef;
+
+/* IPOPT DoBacktrackingLineSearch: alpha = amax, amax/2, ... down to amin; on the first trial, if theta did
+ * not decrease, up to max_soc second-order corrections (not in the restoration problem).  Returns 1 when a
+ * point was accepted (alpha, az, the f-type/Armijo flag out; the step arrays hold the accepted step). */
+static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double amin, double tau, int skip_first,
+                     int only_full, double dw, Trial* t, double* alpha_out, double* az_out, int* ftype_armijo) {
+    const NlotSolverOptions* o = s->o;
+    int nx = s->nx, N = s->N, M = s->M;
+    const int nsave = (N + 1) * nx + 3 * N * s->nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX;
+    const int nres = XMAX + N * nx + CMAX + (N + 1) * M;
+    double tri[XMAX], trt[CMAX];
+    double* trd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* trq = trd + N * nx;
+    double alpha = skip_first ? 0.5 * amax : amax, az = az0;
+    int accepted = 0, ntr = skip_first ? 1 : 0;
+    s->last_rej_filter = 0;
+    for (;;) {
+        ++ntr;
+        trial_primal(s, alpha, t);
+        double tht, pht;
+        trial_merit(s, t, s->mu, &tht, &pht, tri, trd, trt, trq);
+        const double at = ref->fixed_test ? ref->alpha_test : alpha;
+        if (ls_accept(s, ref->theta, ref->phi, ref->gd, at, tht, pht, ftype_armijo)) {
+            accepted = 1;
+            break;
+        }
+        s->last_rej_filter = s->rej_filter;
+        if (only_full) break;
+        /* second-order correction (IPOPT max_soc, kappa_soc): c_soc = alpha c(x) + c(x + alpha d) */
+        if (ntr == 1 && !s->resto && o->max_soc > 0 && tht >= ref->theta) {
+            int soc_ok = 0;
+            s->n_soc_tried++;
+            double* save = (double*)malloc(sizeof(double) * (nsave + nres));
+            double* c0 = save + nsave;
+            step_save(s, save, 0);
+            res_save(s, c0, 0);
+            double *ci = s->rci, *cd = s->rcd, *ct = s->rct, *cq = s->rcq;
+            for (int i = 0; i < nx; ++i) ci[i] = alpha * ci[i] + tri[i];
+            for (int i = 0; i < N * nx; ++i) cd[i] = alpha * cd[i] + trd[i];
+            for (int i = 0; i < s->nc; ++i) ct[i] = alpha * ct[i] + trt[i];
+            for (int i = 0; i < (N + 1) * M; ++i) cq[i] = alpha * cq[i] + trq[i];
+            double th_old = tht;
+            for (int pc = 0; pc < o->max_soc; ++pc) {
+                build(s, MODE_NEWTON, dw);
+                if (riccati(s, MODE_NEWTON)) break; /* same matrix: cannot fail, but be safe */
+                recover(s, dw);
+                const double asoc = primal_frac(s, tau);
+                trial_primal(s, asoc, t);
+                double ths, phs;
+                trial_merit(s, t, s->mu, &ths, &phs, tri, trd, trt, trq);
+                if (ls_accept(s, ref->theta, ref->phi, ref->gd, alpha, ths, phs, ftype_armijo)) {
+                    soc_ok = 1;
+                    alpha = asoc;
+                    az = dual_frac(s, tau);
+                    break;
+                }
+                if (ths > o->kappa_soc * th_old) break;
+                th_old = ths;
+                for (int i = 0; i < nx; ++i) ci[i] = asoc * ci[i] + tri[i];
+                for (int i = 0; i < N * nx; ++i) cd[i] = asoc * cd[i] + trd[i];
+                for (int i = 0; i < s->nc; ++i) ct[i] = asoc * ct[i] + trt[i];
+                for (int i = 0; i < (N + 1) * M; ++i) cq[i] = asoc * cq[i] + trq[i];
+            }
+            res_save(s, c0, 1);
+            if (!soc_ok) step_save(s, save, 1);
+            free(save);
+            if (soc_ok) {
+                s->n_soc_acc++;
+                accepted = 1;
+                break;
+            }
+        }
+        alpha *= 0.5;
+        if (alpha < amin) break;
+    }
+    free(trd);
+    *alpha_out = alpha;
+    *az_out = az;
+    return accepted;
+}
+
+/* IPOPT DetectTinyStep: primal step tiny relative to the iterate, multiplier step small, nearly feasible */
+static int tiny_step(const Sol* s, const Errs* e) {
+    const NlotSolverOptions* o = s->o;
+    if (!(o->tiny_step_tol > 0)) return 0;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    double mx = 0, my = 0, ya = 0;
+    for (int i = 0; i < (N + 1) * nx; ++i) mx = fmax(mx, fabs(s->dX[i]) / (1.0 + fabs(s->X[i])));
+    for (int i = 0; i < N * nu; ++i) mx = fmax(mx, fabs(s->dU[i]) / (1.0 + fabs(s->U[i])));
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) mx = fmax(mx, fabs(s->dS[k]) / (1.0 + fabs(s->S[k])));
+    for (int q = 0; q < (N + 1) * M; ++q) mx = fmax(mx, fabs(s->dT[q]) / (1.0 + fabs(s->T[q])));
+    if (mx > o->tiny_step_tol) return 0;
+    for (int i = 0; i < nx; ++i) {
+        my = fmax(my, fabs(s->yi_n[i] - s->yi[i]));
+        ya = fmax(ya, fabs(s->yi[i]));
+    }
+    for (int i = 0; i < N * nx; ++i) {
+        my = fmax(my, fabs(s->yk_n[i] - s->yk[i]));
+        ya = fmax(ya, fabs(s->yk[i]));
+    }
+    for (int i = 0; i < s->nc; ++i) {
+        my = fmax(my, fabs(s->yt_n[i] - s->yt[i]));
+        ya = fmax(ya, fabs(s->yt[i]));
+    }
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        my = fmax(my, fabs(s->yd_n[q] - s->yd[q]));
+        ya = fmax(ya, fabs(s->yd[q]));
+    }
+    if (my / (1.0 + ya) > o->tiny_step_y_tol) return 0;
+    return e->primal < 1e-4;
+}
+
+static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m,
+                      const double* x0, const double* xg) {
+    memset(s, 0, sizeof *s);
     s->p = p;
     s->m = m;
     s->o = o;
@@ -1552,12 +2048,224 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         if (p->enforce_heading || i != 2) s->tidx[s->nc++] = i;
     memcpy(s->x0, x0, sizeof(double) * p->nx);
     memcpy(s->xg, xg, sizeof(double) * p->nx);
+    s->ne = s->nx + s->N * s->nx + s->nc + (s->N + 1) * s->M;
+}
+
+/* IPOPT MinC_1NrmRestorationPhase (Waechter & Biegler 2006 §3.3, IPOPT's documented defaults), run on the
+ * restoration workspace r for the current point of s.  Returns 0 when it found a point acceptable to the
+ * original filter (s then holds it: equality multipliers 0 as constr_mult_reset_threshold = 0, bound
+ * multipliers by one complementarity Newton step over the whole restoration, reset to 1 above
+ * bound_mult_reset_threshold), else a status.  *iter counts restoration iterations (max_iter covers both). */
+static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
+    const NlotProblem* p = s->p;
+    const NlotSolverOptions* o = s->o;
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    const double kappa_d = 1e-5, gt = 1e-5, gp = 1e-8;
+    /* reference point x_R and the original merit there */
+    double th_R, ph_R;
+    merit(s, s->X, s->U, s->S, s->T, s->mu, &th_R, &ph_R, NULL);
+    residuals(s, s->X, s->U, s->S, s->T, s->rci, s->rcd, s->rct, s->rcq);
+    double cmax = 0;
+    for (int i = 0; i < nx; ++i) cmax = fmax(cmax, fabs(s->rci[i]));
+    for (int i = 0; i < N * nx; ++i) cmax = fmax(cmax, fabs(s->rcd[i]));
+    for (int j = 0; j < s->nc; ++j) cmax = fmax(cmax, fabs(s->rct[j]));
+    for (int q = 0; q < (N + 1) * M; ++q) cmax = fmax(cmax, fabs(s->rcq[q]));
+    memcpy(r->X, s->X, sizeof(double) * (N + 1) * nx);
+    memcpy(r->U, s->U, sizeof(double) * N * nu);
+    memcpy(r->S, s->S, sizeof(double) * (N + 1));
+    memcpy(r->T, s->T, sizeof(double) * (N + 1) * M);
+    memcpy(r->XR, s->X, sizeof(double) * (N + 1) * nx);
+    memcpy(r->UR, s->U, sizeof(double) * N * nu);
+    memcpy(r->SR, s->S, sizeof(double) * (N + 1));
+    for (int i = 0; i < (N + 1) * nx; ++i) r->DRX[i] = fmin(1.0, 1.0 / fabs(r->XR[i]));
+    for (int i = 0; i < N * nu; ++i) r->DRU[i] = fmin(1.0, 1.0 / fabs(r->UR[i]));
+    for (int k = 0; k <= N; ++k) r->DRS[k] = fmin(1.0, 1.0 / fabs(r->SR[k]));
+    const double mu = fmax(s->mu, cmax);
+    r->mu = mu;
+    r->mu_dc = mu;
+    r->tau = fmax(0.99, 1.0 - mu);
+    r->rho = o->resto_penalty_parameter;
+    r->zeta = o->resto_proximity_weight * sqrt(mu);
+    /* p, n minimising the restoration barrier problem for fixed x (IPOPT eq. (33)) */
+    for (int i = 0; i < r->ne; ++i) {
+        const double c = i < nx ? s->rci[i]
+                         : i < row_t(s, 0) ? s->rcd[i - nx]
+                         : i < row_q(s, 0) ? s->rct[i - row_t(s, 0)]
+                                           : s->rcq[i - row_q(s, 0)];
+        const double a = (mu - r->rho * c) / (2.0 * r->rho);
+        const double n = a + sqrt(a * a + mu * c / (2.0 * r->rho));
+        r->rn[i] = n;
+        r->rp[i] = c + n;
+        r->rzp[i] = mu / r->rp[i];
+        r->rzn[i] = mu / r->rn[i];
+    }
+    for (int i = 0; i < N * nu; ++i) {
+        r->zl[i] = fmin(r->rho, s->zl[i]);
+        r->zu[i] = fmin(r->rho, s->zu[i]);
+    }
+    for (int k = 0; k <= N; ++k) r->zs[k] = fmin(r->rho, s->zs[k]);
+    for (int q = 0; q < (N + 1) * M; ++q) r->vt[q] = fmin(r->rho, s->vt[q]);
+    memset(r->yi, 0, sizeof(double) * nx);
+    memset(r->yk, 0, sizeof(double) * N * nx);
+    memset(r->yt, 0, sizeof(double) * CMAX);
+    memset(r->yd, 0, sizeof(double) * (N + 1) * M);
+    r->nfilt = 0;
+    r->dw_last = 0;
+    {
+        double th0, ph0;
+        merit_resto(r, r->X, r->U, r->S, r->T, r->rp, r->rn, r->mu, &th0, &ph0, NULL, NULL, NULL, NULL);
+        r->theta_max = 1e4 * fmax(1.0, th0);
+        r->theta_min = 1e-4 * fmax(1.0, th0);
+    }
+    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M + 2 * r->ne;
+    double* tb = (double*)malloc(sizeof(double) * ntr);
+    Trial t = {tb, tb + (N + 1) * nx, tb + (N + 1) * nx + N * nu, tb + (N + 1) * nx + N * nu + N + 1,
+               tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M, tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M + r->ne};
+    const double kap = o->barrier_tol_factor;
+    const double mu_floor = fmin(o->tol, o->compl_inf_tol) / (kap + 1.0);
+    int status = NLOT_RESTO_FAILED, first = 1;
+    Errs e;
+    for (;;) {
+        eval_full(r);
+        errors(r, &e);
+        double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
+        if (!isfinite(E0)) {
+            status = NLOT_NUMERIC;
+            break;
+        }
+        if (!first) { /* RestoConvergenceCheck: back to the regular iteration? */
+            double th_o, ph_o;
+            merit(s, r->X, r->U, r->S, r->T, s->mu, &th_o, &ph_o, NULL);
+            if (th_o <= o->required_infeasibility_reduction * th_R && filter_ok(s, th_o, ph_o) &&
+                (cmp_le(th_o, (1.0 - gt) * th_R, th_R) || cmp_le(ph_o - ph_R, -gp * th_R, ph_R))) {
+                status = 0;
+                break;
+            }
+            if (E0 <= o->tol) { /* the restoration problem converged to an unacceptable point */
+                const double thr = o->resto_failure_feasibility_threshold > 0 ? o->resto_failure_feasibility_threshold
+                                                                              : 1e2 * o->tol;
+                double pinf = 0;
+                residuals(s, r->X, r->U, r->S, r->T, s->rci, s->rcd, s->rct, s->rcq);
+                for (int i = 0; i < nx; ++i) pinf = fmax(pinf, fabs(s->rci[i]));
+                for (int i = 0; i < N * nx; ++i) pinf = fmax(pinf, fabs(s->rcd[i]));
+                for (int j = 0; j < s->nc; ++j) pinf = fmax(pinf, fabs(s->rct[j]));
+                for (int q = 0; q < (N + 1) * M; ++q) pinf = fmax(pinf, fabs(s->rcq[q]));
+                status = pinf <= thr ? NLOT_RESTO_FAILED : NLOT_INFEASIBLE;
+                break;
+            }
+        }
+        first = 0;
+        if (*iter >= o->max_iter) {
+            status = NLOT_MAXITER;
+            break;
+        }
+        /* monotone barrier update inside the restoration phase */
+        for (;;) {
+            double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+            if (Emu > kap * r->mu) break;
+            double nm = fmax(fmin(0.2 * r->mu, pow(r->mu, 1.5)), mu_floor);
+            if (nm >= r->mu) break;
+            r->mu = nm;
+            r->tau = fmax(0.99, 1.0 - nm);
+            r->nfilt = 0;
+            errors(r, &e);
+        }
+        r->mu_dc = r->mu;
+        double dw;
+        if (newton_step(r, &dw)) {
+            status = NLOT_NUMERIC;
+            break;
+        }
+        recover(r, dw);
+        const double tau = r->tau, amax = primal_frac(r, tau), az = dual_frac(r, tau);
+        double theta, phi;
+        merit_resto(r, r->X, r->U, r->S, r->T, r->rp, r->rn, r->mu, &theta, &phi, NULL, NULL, NULL, NULL);
+        const double gd = barrier_gd(r);
+        double amin = 1e-5;
+        if (gd < 0) {
+            amin = fmin(1e-5, 1e-8 * theta / (-gd));
+            if (theta <= r->theta_min) amin = fmin(amin, pow(theta, 1.1) / pow(-gd, 2.3));
+        }
+        amin *= 0.05;
+        LsRef ref = {theta, phi, gd, 0.0, 0};
+        double alpha, azz;
+        int fa = 0;
+        int ok = backtrack(r, &ref, amax, az, amin, tau, 0, 0, dw, &t, &alpha, &azz, &fa);
+        if (getenv("NLOT_VERBOSE"))
+            fprintf(stderr, "  resto it %3d mu %.2e fR %.6f thR %.2e E0 %.2e a %.2e\n", *iter, r->mu, r->f, theta, E0, alpha);
+        if (!ok) {
+            status = NLOT_RESTO_FAILED;
+            break;
+        }
+        if (!fa) filter_add(r, theta, phi);
+        accept_step(r, alpha, azz, &t);
+        ++*iter;
+    }
+    free(tb);
+    (void)lin_resid;
+    if (status) return status;
+    /* back to the regular problem */
+    double* zold = (double*)malloc(sizeof(double) * 4 * (2 * N * nu + (N + 1) + (N + 1) * M));
+    const double mu0 = s->mu;
+    double az = 1.0;
+#define DZ(z, so, sn) ((mu0 - (z) * (sn)) / (so))
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int q = k * nu + i;
+            s->dzl[q] = DZ(s->zl[q], s->U[q] - p->umin[i], r->U[q] - p->umin[i]);
+            s->dzu[q] = DZ(s->zu[q], p->umax[i] - s->U[q], p->umax[i] - r->U[q]);
+        }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) s->dzs[k] = DZ(s->zs[k], s->S[k], r->S[k]);
+    for (int q = 0; q < (N + 1) * M; ++q) s->dvt[q] = DZ(s->vt[q], s->T[q], r->T[q]);
+#undef DZ
+    az = dual_frac(s, s->tau);
+    double zmax = 0;
+    for (int i = 0; i < N * nu; ++i) {
+        s->zl[i] += az * s->dzl[i];
+        s->zu[i] += az * s->dzu[i];
+        zmax = fmax(zmax, fmax(s->zl[i], s->zu[i]));
+    }
+    if (s->ns)
+        for (int k = 0; k <= N; ++k) {
+            s->zs[k] += az * s->dzs[k];
+            zmax = fmax(zmax, s->zs[k]);
+        }
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        s->vt[q] += az * s->dvt[q];
+        zmax = fmax(zmax, s->vt[q]);
+    }
+    if (zmax > o->bound_mult_reset_threshold) {
+        for (int i = 0; i < N * nu; ++i) s->zl[i] = s->zu[i] = 1.0;
+        for (int k = 0; k <= N; ++k) s->zs[k] = 1.0;
+        for (int q = 0; q < (N + 1) * M; ++q) s->vt[q] = 1.0;
+    }
+    free(zold);
+    memcpy(s->X, r->X, sizeof(double) * (N + 1) * nx);
+    memcpy(s->U, r->U, sizeof(double) * N * nu);
+    memcpy(s->S, r->S, sizeof(double) * (N + 1));
+    memcpy(s->T, r->T, sizeof(double) * (N + 1) * M);
+    memset(s->yi, 0, sizeof(double) * nx);
+    memset(s->yk, 0, sizeof(double) * N * nx);
+    memset(s->yt, 0, sizeof(double) * CMAX);
+    memset(s->yd, 0, sizeof(double) * (N + 1) * M);
+    (void)kappa_d;
+    return 0;
+}
+
+/* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
+ * seen, [4] = final mu, [5] = E_0 (scaled overall error), [6] = restoration phases, [7] = watchdog /
+ * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny) */
+int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                     const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
+                     int* iters_out, double* info) {
+    Sol sol, *s = &sol, rsol, *r = &rsol;
+    sol_setup(s, p, o, m, x0, xg);
     if (sol_alloc(s)) return NLOT_NUMERIC;
+    int r_alloc = 0;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     const double k1 = o->bound_push, k2 = o->bound_frac;
     const int nsave = (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX;
-    const int nres = XMAX + N * nx + CMAX + (N + 1) * M;
-    int n_soc = 0;
     double lin_resid = 0;
     double* qf_aff = (double*)malloc(sizeof(double) * 2 * nsave);
     double* qf_cen = qf_aff + nsave;
@@ -1621,8 +2329,17 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
     s->dw_last = 0;
     int status = NLOT_MAXITER, iter = 0;
     Errs e;
-    double* Xt = (double*)malloc(sizeof(double) * ((N + 1) * nx + N * nu + (N + 1) + (N + 1) * M));
-    double *Ut = Xt + (N + 1) * nx, *St = Ut + N * nu, *Tt = St + (N + 1);
+    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M;
+    double* tb = (double*)malloc(sizeof(double) * ntr);
+    Trial t = {tb, tb + (N + 1) * nx, tb + (N + 1) * nx + N * nu, tb + (N + 1) * nx + N * nu + N + 1, NULL, NULL};
+    /* watchdog (IPOPT StartWatchDog / StopWatchDog): saved iterate, direction and reference values */
+    const int nit = iter_len(s);
+    double* wd_it = (double*)malloc(sizeof(double) * (nit + nsave));
+    double* wd_dir = wd_it + nit;
+    int in_wd = 0, wd_short = 0, wd_trial = 0, in_soft = 0, soft_cnt = 0, tiny_last = 0;
+    int n_resto = 0, n_wd = 0, n_soft = 0, n_tiny = 0;
+    LsRef wd_ref = {0, 0, 0, 0, 1};
+    double wd_amax = 1, wd_az = 1, wd_amin = 0, wd_mu = 0, wd_tau = 0;
     for (;;) {
         eval_full(s);
         errors(s, &e);
@@ -1649,7 +2366,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             if (iter > 0) {
                 for (;;) {
                     double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
-                    if (Emu > kap * s->mu) break;
+                    if (Emu > kap * s->mu && !tiny_last) break;
                     double nm = fmin(0.2 * s->mu, pow(s->mu, 1.5));
                     nm = fmax(nm, mu_floor);
                     if (nm >= s->mu) break;
@@ -1657,6 +2374,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                     s->tau = fmax(0.99, 1.0 - s->mu);
                     s->nfilt = 0;
                     errors(s, &e); /* complmu depends on mu */
+                    tiny_last = 0;
                 }
             }
         } else { /* IPOPT AdaptiveMuUpdate::UpdateBarrierParameter */
@@ -1704,21 +2422,10 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         const double mu_it = s->mu;
         s->mu_dc = mu_it;
         if (use_qf) s->mu = 0.0; /* free mode: affine-scaling step first */
-        double dw = 0.0;
-        build(s, MODE_NEWTON, dw);
-        if (riccati(s, MODE_NEWTON)) {
-            dw = s->dw_last == 0.0 ? 1e-4 : fmax(1e-20, s->dw_last / 3.0);
-            for (;;) {
-                build(s, MODE_NEWTON, dw);
-                if (!riccati(s, MODE_NEWTON)) break;
-                dw *= (s->dw_last == 0.0) ? 100.0 : 8.0;
-                if (dw > 1e40) break;
-            }
-            if (dw > 1e40) {
-                status = NLOT_NUMERIC;
-                break;
-            }
-            s->dw_last = dw;
+        double dw;
+        if (newton_step(s, &dw)) {
+            status = NLOT_NUMERIC;
+            break;
         }
         lin_resid = fmax(lin_resid, linear_residual(s, MODE_NEWTON));
         recover(s, dw);
@@ -1743,157 +2450,184 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         } else {
             s->mu = mu_it;
         }
-        /* ---- step sizes: fraction to the boundary ---- */
-        double amax = 1.0, az = 1.0, tau = s->tau;
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < nu; ++i) {
-                int q = k * nu + i;
-                amax = frac_to_bound(s->U[q] - p->umin[i], s->dU[q], tau, amax);
-                amax = frac_to_bound(p->umax[i] - s->U[q], -s->dU[q], tau, amax);
-                az = frac_to_bound(s->zl[q], s->dzl[q], tau, az);
-                az = frac_to_bound(s->zu[q], s->dzu[q], tau, az);
-            }
-        if (s->ns)
-            for (int k = 0; k <= N; ++k) {
-                amax = frac_to_bound(s->S[k], s->dS[k], tau, amax);
-                az = frac_to_bound(s->zs[k], s->dzs[k], tau, az);
-            }
-        for (int q = 0; q < (N + 1) * M; ++q) {
-            amax = frac_to_bound(s->T[q], s->dT[q], tau, amax);
-            az = frac_to_bound(s->vt[q], s->dvt[q], tau, az);
-        }
-        /* ---- filter line search ---- */
+        /* ---- step sizes: fraction to the boundary; line-search reference values ---- */
+        const double tau = s->tau;
+        double amax = primal_frac(s, tau), az = dual_frac(s, tau);
         double theta, phi;
         merit(s, s->X, s->U, s->S, s->T, s->mu, &theta, &phi, NULL);
-        const double kappa_d = 1e-5, mu = s->mu;
-        double gd = 0; /* grad phi_mu . d */
-        for (int i = 0; i < (N + 1) * nx; ++i) gd += s->gX[i] * s->dX[i];
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < nu; ++i) {
-                int q = k * nu + i;
-                gd += (s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
-            }
-        if (s->ns)
-            for (int k = 0; k <= N; ++k) gd += (s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
-        for (int q = 0; q < (N + 1) * M; ++q) gd += (-mu / s->T[q] + kappa_d * mu) * s->dT[q];
-        const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3;
-        double amin = gt;
+        const double gd = barrier_gd(s);
+        double amin = 1e-5;
         if (gd < 0) {
-            amin = fmin(gt, gp * theta / (-gd));
-            if (theta <= s->theta_min) amin = fmin(amin, delta * pow(theta, sth) / pow(-gd, sph));
+            amin = fmin(1e-5, 1e-8 * theta / (-gd));
+            if (theta <= s->theta_min) amin = fmin(amin, pow(theta, 1.1) / pow(-gd, 2.3));
         }
         amin *= 0.05;
-        double alpha = amax;
-        int accepted = 0, armijo_ftype = 0, trials = 0;
-        double *rci_t = s->rci, *rcd_t = NULL, *rct_t = NULL, *rcq_t = NULL;
-        (void)rci_t;
-        double tri[XMAX], trt[CMAX];
-        double* trd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
-        double* trq = trd + N * nx;
-        rcd_t = trd;
-        rct_t = trt;
-        rcq_t = trq;
-        for (;;) {
-            ++trials;
-            for (int i = 0; i < (N + 1) * nx; ++i) Xt[i] = s->X[i] + alpha * s->dX[i];
-            for (int i = 0; i < N * nu; ++i) Ut[i] = s->U[i] + alpha * s->dU[i];
-            for (int k = 0; k <= N; ++k) St[k] = s->S[k] + alpha * s->dS[k];
-            for (int q = 0; q < (N + 1) * M; ++q) Tt[q] = s->T[q] + alpha * s->dT[q];
-            double tht, pht;
-            merit_r(s, Xt, Ut, St, Tt, mu, &tht, &pht, tri, rcd_t, rct_t, rcq_t);
-            if (ls_accept(s, theta, phi, gd, alpha, tht, pht, &armijo_ftype)) {
-                accepted = 1;
+        /* ---- line search (IPOPT BacktrackingLineSearch::FindAcceptableTrialPoint) ---- */
+        LsRef ref = {theta, phi, gd, 0.0, 0};
+        double alpha = amax, azz = az;
+        int accepted = 0, fa = 0, is_tiny = 0, augment = 1;
+        if (!in_soft && !in_wd && tiny_step(s, &e)) { /* tiny step: take the full step, no filter */
+            is_tiny = 1;
+            ++n_tiny;
+            trial_primal(s, amax, &t);
+            accepted = 1;
+            augment = 0;
+            if (tiny_last) { /* twice in a row: IPOPT STOP_AT_TINY_STEP */
+                accept_step(s, amax, az, &t);
+                ++iter;
+                status = NLOT_TINY_STEP;
                 break;
             }
-            /* ---- second-order correction on the first trial (IPOPT max_soc = 4, kappa_soc = 0.99) ---- */
-            if (trials == 1 && o->max_soc > 0 && tht >= theta) {
-                int soc_ok = 0;
-                double* save = (double*)malloc(sizeof(double) * nsave);
-                step_save(s, save, 0);
-                /* c_soc = alpha_max c(x) + c(x + alpha_max d) */
-                double *ci = s->rci, *cd = s->rcd, *ct = s->rct, *cq = s->rcq;
-                double* c0 = (double*)malloc(sizeof(double) * nres);
-                res_save(s, c0, 0);
-                for (int i = 0; i < nx; ++i) ci[i] = alpha * ci[i] + tri[i];
-                for (int i = 0; i < N * nx; ++i) cd[i] = alpha * cd[i] + trd[i];
-                for (int i = 0; i < s->nc; ++i) ct[i] = alpha * ct[i] + trt[i];
-                for (int i = 0; i < (N + 1) * M; ++i) cq[i] = alpha * cq[i] + trq[i];
-                double th_old = tht, a_test = alpha;
-                for (int pcount = 0; pcount < o->max_soc; ++pcount) {
-                    build(s, MODE_NEWTON, dw);
-                    if (riccati(s, MODE_NEWTON)) break; /* same matrix: cannot fail, but be safe */
-                    recover(s, dw);
-                    double asoc = primal_frac(s, tau);
-                    for (int i = 0; i < (N + 1) * nx; ++i) Xt[i] = s->X[i] + asoc * s->dX[i];
-                    for (int i = 0; i < N * nu; ++i) Ut[i] = s->U[i] + asoc * s->dU[i];
-                    for (int k = 0; k <= N; ++k) St[k] = s->S[k] + asoc * s->dS[k];
-                    for (int q = 0; q < (N + 1) * M; ++q) Tt[q] = s->T[q] + asoc * s->dT[q];
-                    double ths, phs;
-                    merit_r(s, Xt, Ut, St, Tt, mu, &ths, &phs, tri, rcd_t, rct_t, rcq_t);
-                    if (ls_accept(s, theta, phi, gd, a_test, ths, phs, &armijo_ftype)) {
-                        soc_ok = 1;
-                        alpha = asoc;
-                        az = dual_frac(s, tau);
-                        break;
+        } else if (in_soft) {
+            accepted = 0; /* soft restoration continues below */
+        } else {
+            if (!in_wd && o->watchdog_shortened_iter_trigger > 0 && wd_short >= o->watchdog_shortened_iter_trigger) {
+                /* StartWatchDog: remember the point, its direction and reference values */
+                in_wd = 1;
+                wd_trial = 0;
+                ++n_wd;
+                iter_io(s, wd_it, 0);
+                step_save(s, wd_dir, 0);
+                wd_ref = (LsRef){theta, phi, gd, amax, 1};
+                wd_amax = amax;
+                wd_az = az;
+                wd_amin = amin;
+                wd_mu = s->mu;
+                wd_tau = tau;
+            }
+            int skip_first = 0;
+            for (;;) {
+                const LsRef* rf = in_wd ? &wd_ref : &ref;
+                accepted = backtrack(s, rf, amax, az, amin, tau, skip_first, in_wd, dw, &t, &alpha, &azz, &fa);
+                if (in_wd) {
+                    if (accepted) {
+                        in_wd = 0;
+                    } else if (++wd_trial > o->watchdog_trial_iter_max) {
+                        /* StopWatchDog: back to the watchdog point and direction, backtrack from alpha_max/2 */
+                        in_wd = 0;
+                        wd_short = 0;
+                        iter_io(s, wd_it, 1);
+                        step_save(s, wd_dir, 1);
+                        s->mu = wd_mu;
+                        s->tau = wd_tau;
+                        amax = wd_amax;
+                        az = wd_az;
+                        amin = wd_amin;
+                        ref = (LsRef){wd_ref.theta, wd_ref.phi, wd_ref.gd, 0.0, 0};
+                        eval_full(s); /* residuals of the watchdog point (second-order corrections) */
+                        skip_first = 1;
+                        continue;
+                    } else { /* tentative step: accepted without the acceptance test */
+                        accepted = 1;
+                        alpha = amax;
+                        azz = az;
+                        trial_primal(s, amax, &t);
+                        fa = 0;
                     }
-                    if (ths > 0.99 * th_old) break;
-                    th_old = ths;
-                    for (int i = 0; i < nx; ++i) ci[i] = asoc * ci[i] + tri[i];
-                    for (int i = 0; i < N * nx; ++i) cd[i] = asoc * cd[i] + trd[i];
-                    for (int i = 0; i < s->nc; ++i) ct[i] = asoc * ct[i] + trt[i];
-                    for (int i = 0; i < (N + 1) * M; ++i) cq[i] = asoc * cq[i] + trq[i];
                 }
-                res_save(s, c0, 1); /* restore the current residuals */
-                free(c0);
-                if (!soc_ok) step_save(s, save, 1);
-                free(save);
-                if (soc_ok) {
+                break;
+            }
+            if (accepted) wd_short = (alpha < amax) ? wd_short + 1 : 0;
+            /* IPOPT filter reset heuristic: the filter is cleared when in filter_reset_trigger (5) successive
+             * iterations the last rejected trial was rejected by the filter (at most max_filter_resets = 5) */
+            if (accepted && s->n_filt_resets < 5) {
+                s->n_filt_rej = s->last_rej_filter ? s->n_filt_rej + 1 : 0;
+                if (s->n_filt_rej >= 5) {
+                    s->nfilt = 0;
+                    s->n_filt_resets++;
+                    s->n_filt_rej = 0;
+                }
+            }
+        }
+        if (!accepted && o->soft_resto_pderror_reduction_factor > 0 && o->resto) {
+            /* soft restoration phase (IPOPT TrySoftRestoStep): the damped full step if it is acceptable to
+             * the filter, or if it reduces the primal-dual error by the factor */
+            if (in_soft && ++soft_cnt > o->max_soft_resto_iters) {
+                accepted = 0;
+            } else {
+                const double a = fmin(amax, az);
+                trial_primal(s, a, &t);
+                double tht, pht;
+                trial_merit(s, &t, s->mu, &tht, &pht, NULL, NULL, NULL, NULL);
+                int ft = 0, sat = ls_accept(s, ref.theta, ref.phi, ref.gd, 0.0, tht, pht, &ft);
+                int ok = sat;
+                if (!ok) {
+                    const double mu_pd = (o->mu_strategy == 1 && s->free_mode) ? 0.0 : s->mu;
+                    const double mu_keep = s->mu;
+                    s->mu = mu_pd;
+                    Errs ec;
+                    errors(s, &ec);
+                    const double pd_c = pd_error(&ec);
+                    s->mu = mu_keep;
+                    double* snap = (double*)malloc(sizeof(double) * (nit + nsave));
+                    iter_io(s, snap, 0);
+                    step_save(s, snap + nit, 0);
+                    accept_step(s, a, a, &t);
+                    eval_full(s);
+                    s->mu = mu_pd;
+                    errors(s, &ec);
+                    s->mu = mu_keep;
+                    const double pd_t = pd_error(&ec);
+                    ok = isfinite(pd_t) && pd_t <= o->soft_resto_pderror_reduction_factor * pd_c;
+                    iter_io(s, snap, 1); /* the caller accepts the trial point itself */
+                    step_save(s, snap + nit, 1);
+                    eval_full(s);
+                    free(snap);
+                }
+                if (ok) {
                     accepted = 1;
-                    n_soc++;
+                    alpha = azz = a;
+                    augment = 0;
+                    ++n_soft;
+                    if (sat) {
+                        in_soft = 0;
+                        soft_cnt = 0;
+                    } else {
+                        in_soft = 1;
+                    }
+                } else {
+                    accepted = 0;
+                }
+            }
+        }
+        if (getenv("NLOT_VERBOSE"))
+            fprintf(stderr, "it %3d mu %.2e f %.6f th %.2e E0 %.2e dual %.2e dw %.1e amax %.2e a %.2e az %.2e nf %d%s%s%s\n",
+                    iter, s->mu, s->f, theta, E0, e.dual, dw, amax, alpha, azz, s->nfilt, in_wd ? " W" : "",
+                    in_soft ? " s" : "", is_tiny ? " T" : "");
+        if (!accepted) {
+            if (!o->resto) {
+                status = NLOT_LS_FAILED;
+                break;
+            }
+            /* ---- feasibility restoration phase ---- */
+            filter_add(s, theta, phi); /* the current point enters the filter first */
+            if (!r_alloc) {
+                sol_setup(r, p, o, m, x0, xg);
+                r->resto = 1;
+                if (sol_alloc(r)) {
+                    status = NLOT_NUMERIC;
                     break;
                 }
+                r_alloc = 1;
             }
-            alpha *= 0.5;
-            if (alpha < amin) break;
-        }
-        free(trd);
-        if (getenv("NLOT_VERBOSE"))
-            fprintf(stderr, "it %3d mu %.2e f %.6f th %.2e E0 %.2e dual %.2e dw %.1e amax %.2e a %.2e az %.2e tr %d nf %d soc %d\n", iter, mu,
-                    s->f, theta, E0, e.dual, dw, amax, alpha, az, trials, s->nfilt, n_soc);
-        if (!accepted) {
-            status = NLOT_LS_FAILED;
-            break;
-        }
-        if (!armijo_ftype) filter_add(s, theta, phi);
-        /* ---- accept trial point ---- */
-        memcpy(s->X, Xt, sizeof(double) * (N + 1) * nx);
-        memcpy(s->U, Ut, sizeof(double) * N * nu);
-        memcpy(s->S, St, sizeof(double) * (N + 1));
-        memcpy(s->T, Tt, sizeof(double) * (N + 1) * M);
-        for (int i = 0; i < nx; ++i) s->yi[i] += alpha * (s->yi_n[i] - s->yi[i]);
-        for (int i = 0; i < N * nx; ++i) s->yk[i] += alpha * (s->yk_n[i] - s->yk[i]);
-        for (int i = 0; i < s->nc; ++i) s->yt[i] += alpha * (s->yt_n[i] - s->yt[i]);
-        for (int i = 0; i < (N + 1) * M; ++i) s->yd[i] += alpha * (s->yd_n[i] - s->yd[i]);
-        const double ks = 1e10; /* kappa_Sigma bound-multiplier safeguard */
-#define ZUPD(z, dz, sl)                                                                          \
-    do {                                                                                         \
-        double zn = (z) + az * (dz), sv = (sl);                                                  \
-        zn = fmax(fmin(zn, ks * mu / sv), mu / (ks * sv));                                       \
-        (z) = zn;                                                                                \
-    } while (0)
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < nu; ++i) {
-                int q = k * nu + i;
-                ZUPD(s->zl[q], s->dzl[q], s->U[q] - p->umin[i]);
-                ZUPD(s->zu[q], s->dzu[q], p->umax[i] - s->U[q]);
+            ++n_resto;
+            int st = restoration(s, r, &iter, &lin_resid);
+            if (st) {
+                status = st;
+                break;
             }
-        if (s->ns)
-            for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k]);
-        for (int q = 0; q < (N + 1) * M; ++q) ZUPD(s->vt[q], s->dvt[q], s->T[q]);
-#undef ZUPD
+            in_soft = soft_cnt = 0;
+            in_wd = wd_short = 0;
+            tiny_last = 0;
+            continue;
+        }
+        if (augment && !fa) filter_add(s, ref.theta, ref.phi);
+        accept_step(s, alpha, azz, &t);
+        tiny_last = is_tiny;
         ++iter;
     }
-    free(Xt);
+    free(tb);
+    free(wd_it);
     free(qf_aff);
     memcpy(Xout, s->X, sizeof(double) * (N + 1) * nx);
     memcpy(Uout, s->U, sizeof(double) * N * nu);
@@ -1906,7 +2640,10 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         info[2] = e.cviol;
         info[3] = lin_resid;
         info[4] = s->mu;
+        info[6] = n_resto;
+        info[7] = 1e6 * n_wd + 1e4 * n_soft + 1e2 * (s->n_soc_tried > 99 ? 99 : s->n_soc_tried) + n_tiny;
     }
+    if (r_alloc) free(r->arena);
     free(s->arena);
     return status;
 }
@@ -1942,7 +2679,20 @@ void oracle_default_options(NlotSolverOptions* o) {
     o->constr_mult_init_max = 1e3;
     o->bound_push = 1e-2;
     o->bound_frac = 1e-2;
-    o->max_soc = 0; /* IPOPT default 4; 0 measured better here */
+    o->max_soc = 4; /* IPOPT defaults from here on */
+    o->resto = 1;
+    o->watchdog_shortened_iter_trigger = 10;
+    o->watchdog_trial_iter_max = 3;
+    o->max_soft_resto_iters = 10;
+    o->kappa_soc = 0.99;
+    o->tiny_step_tol = 10 * DBL_EPSILON;
+    o->tiny_step_y_tol = 1e-2;
+    o->soft_resto_pderror_reduction_factor = 0.9999;
+    o->required_infeasibility_reduction = 0.9;
+    o->resto_penalty_parameter = 1000.0;
+    o->resto_proximity_weight = 1.0;
+    o->bound_mult_reset_threshold = 1000.0;
+    o->resto_failure_feasibility_threshold = 0.0;
 }
 
 int oracle_sizeof_problem(void) { return (int)sizeof(NlotProblem); }

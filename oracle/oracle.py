@@ -140,8 +140,11 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None):
     Xi = None if X_init is None else np.ascontiguousarray(X_init, np.float64)
     st = lib().oracle_solve_one(C.byref(pc), C.byref(opt), C.byref(hm.desc) if hm else None, _dp(x0), _dp(xg),
                                 _dp(Xi), _dp(X), _dp(U), _dp(S), _dp(cost), it, _dp(info))
+    ev = int(info[7])
     return dict(status=st, X=X, U=U, S=S, cost=float(cost[0]), iters=int(it[0]), dual_inf=info[1],
-                constr_viol=info[2], lin_resid=info[3], mu=info[4], E0=info[5])
+                constr_viol=info[2], lin_resid=info[3], mu=info[4], E0=info[5], resto_phases=int(info[6]),
+                watchdogs=ev // 1000000, soft_resto_steps=(ev // 10000) % 100, soc_tried=(ev // 100) % 100,
+                tiny_steps=ev % 100)
 
 
 def solve_batch(problem, x0, xg, hm: HostMlp = None, opt=None, threads=0):

@@ -33,8 +33,8 @@ def run(out, B):
 
     x0, xg = sample_start_goal(METRIC_PROBLEM, B, seed=0, sdf=sdf)
     res = {}
-    for name, opt in (("adaptive", _abi.default_options()),
-                      ("monotone", _abi.default_options(mu_strategy=0, barrier_tol_factor=10.0))):
+    for name, opt in (("adaptive", _abi.gpu_options()),
+                      ("monotone", _abi.gpu_options(mu_strategy=0, barrier_tol_factor=10.0))):
         torch.cuda.synchronize()
         t = time.perf_counter()
         r = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)

@@ -8,7 +8,7 @@ from nlotrajectories_amd.solver import solve_batch
 b = BENCHMARKS["b2"]
 out = {}
 for k in [0, 1, 2, 3, 4, 6, 8, 12, 20]:
-    r = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=_abi.default_options(max_iter=k))
+    r = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=_abi.gpu_options(max_iter=k))
     out[f"X{k}"] = r["X"][0].cpu().numpy(); out[f"U{k}"] = r["U"][0].cpu().numpy(); out[f"S{k}"] = r["S"][0].cpu().numpy()
     out[f"st{k}"] = r["status"][0].item(); out[f"it{k}"] = r["iters"][0].item()
 os.makedirs("gpurun_out", exist_ok=True)

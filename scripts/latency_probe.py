@@ -23,7 +23,7 @@ def sdf(pts):
 
 for B in (1, 64):
     x0, xg = sample_start_goal(METRIC_PROBLEM, B, seed=3, sdf=sdf)
-    opt = _abi.default_options(max_iter=40)
+    opt = _abi.gpu_options(max_iter=40)
     solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)
     set_timing(True)
     torch.cuda.synchronize()

@@ -26,6 +26,6 @@ def sdf(pts):
 x0, xg = sample_start_goal(METRIC_PROBLEM, max(B, 1), seed=0, sdf=sdf)
 torch.cuda.synchronize()
 t = time.perf_counter()
-r = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=_abi.default_options(max_iter=iters))
+r = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=_abi.gpu_options(max_iter=iters))
 torch.cuda.synchronize()
 print(f"B={B} max_iter={iters} wall {time.perf_counter() - t:.3f} s", flush=True)

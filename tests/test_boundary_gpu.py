@@ -93,7 +93,7 @@ def test_l4casadi_wrapper_signature(artefact, golden):
     from nlotrajectories_amd.solver import solve_batch
 
     r = solve_batch(METRIC_PROBLEM, np.array([[0, 0, 0.785, 0, 0.0]]), np.array([[1, 1, 0.785, 0, 0.0]]), mlp=obs,
-                    options=__import__("nlotrajectories_amd._abi", fromlist=["x"]).default_options(max_iter=2))
+                    options=__import__("nlotrajectories_amd._abi", fromlist=["x"]).gpu_options(max_iter=2))
     assert r["iters"][0].item() == 2
     with pytest.raises(ValueError):
         L4CasADi(model, generate_jac_jac=True)

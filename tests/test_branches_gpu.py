@@ -59,7 +59,7 @@ def test_iterates_match_oracle(name):
 
     prob, x0, xg = _cases()[name]
     for k in (1, 3, 8):
-        opt = _abi.default_options(max_iter=k)
+        opt = _abi.gpu_options(max_iter=k)
         rg = solve_batch(prob, np.array([x0], float), np.array([xg], float), options=opt)
         rc = O.solve_one(prob, np.array(x0, float), np.array(xg, float), opt=opt)
         xp = np.array(x0, float)
@@ -89,7 +89,7 @@ def test_full_solves_match_oracle(name):
     X0[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
     XG[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
     rg = solve_batch(prob, X0, XG)
-    rc = O.solve_batch(prob, X0, XG, threads=8)
+    rc = O.solve_batch(prob, X0, XG, opt=__import__("nlotrajectories_amd._abi", fromlist=["x"]).gpu_options(), threads=8)
     sg = rg["status"].cpu().numpy()
     agree = (sg == rc["status"]).mean()
     both = (sg == 0) & (rc["status"] == 0)

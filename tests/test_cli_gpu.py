@@ -41,6 +41,9 @@ def test_learned_config_matches_oracle():
     f = os.path.join(CFG, "benchmark_3_unicycle_convex.yaml")
     X, U, status = run_benchmark(f, initializer="linear", weights="artefact", verbose=False)
     cfg = Config.load(f)
-    rc = O.solve_one(cfg.to_problem(), cfg.body.start_state, cfg.body.goal_state, O.HostMlp(MlpWeights.artefact()))
+    from nlotrajectories_amd import _abi
+
+    rc = O.solve_one(cfg.to_problem(), cfg.body.start_state, cfg.body.goal_state, O.HostMlp(MlpWeights.artefact()),
+                     opt=_abi.gpu_options())
     assert status == ("success" if rc["status"] == 0 else "failed")
     assert X.shape == (5, 41) and U.shape == (2, 40)

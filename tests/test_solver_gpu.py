@@ -33,7 +33,7 @@ def test_iterates_match_oracle_b2(strategy):
 
     b = BENCHMARKS["b2"]
     for k in (1, 2, 5, 10, 20):
-        opt = _abi.default_options(max_iter=k, **STRATEGIES[strategy])
+        opt = _abi.gpu_options(max_iter=k, **STRATEGIES[strategy])
         rg = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=opt)
         rc = O.solve_one(b["problem"], b["start"], b["goal"], opt=opt)
         assert rg["iters"][0].item() == rc["iters"] == k
@@ -56,7 +56,7 @@ def test_iterates_match_oracle_learned(artefact, strategy):
     mlp, hm = DeviceMlp(artefact), O.HostMlp(artefact)
     x0, xg = [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0]
     for k in (1, 3):
-        opt = _abi.default_options(max_iter=k, **STRATEGIES[strategy])
+        opt = _abi.gpu_options(max_iter=k, **STRATEGIES[strategy])
         rg = solve_batch(METRIC_PROBLEM, np.array([x0]), np.array([xg]), mlp=mlp, options=opt)
         rc = O.solve_one(METRIC_PROBLEM, x0, xg, hm, opt=opt)
         np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-4)
@@ -87,7 +87,7 @@ def test_batch_b2_analytic_matches_oracle(strategy):
     sdf = lambda P: np.sqrt(((np.asarray(P) - 0.5) ** 2).sum(1)) - 0.25
     x0, xg = sample_start_goal(p, 64, seed=1, sdf=sdf, lo=(0, 0), hi=(1, 1))
     tight = dict(tol=1e-8, constr_viol_tol=1e-8, compl_inf_tol=1e-8) if strategy == "adaptive" else {}
-    opt = _abi.default_options(**STRATEGIES[strategy], **tight)
+    opt = _abi.gpu_options(**STRATEGIES[strategy], **tight)
     rg = solve_batch(p, x0, xg, options=opt)
     rc = O.solve_batch(p, x0, xg, opt=opt, threads=8)
     agree, both, rel = _stats(rg, rc)
@@ -101,7 +101,13 @@ def test_batch_b2_analytic_matches_oracle(strategy):
 
 
 def test_batch_learned_sdf_matches_oracle(artefact):
+    """The metric workload (learned SDF, the reference's tol 1e-4, IPOPT defaults the GPU runs) on 256 seeded
+    instances.  Outcomes at tol 1e-4 are path-sensitive (ReLU kinks, discrete filter / mode decisions), so the
+    bar is the oracle's own reproducibility: the oracle run again with x0 perturbed by 1e-13 agrees with
+    itself on status and on 1e-4-relative final cost only to some rate, and the GPU must agree with the
+    oracle at least as well (2 % / 5 % slack for 256 samples), with a 90 % floor on status agreement."""
     O = _oracle()
+    from nlotrajectories_amd import _abi
     from nlotrajectories_amd.ops import DeviceMlp
     from nlotrajectories_amd.problem import METRIC_PROBLEM
     from nlotrajectories_amd.sampling import sample_start_goal
@@ -109,14 +115,83 @@ def test_batch_learned_sdf_matches_oracle(artefact):
 
     tm = artefact.torch_module()
     sdf = lambda P: tm(torch.tensor(np.asarray(P), dtype=torch.float32)).detach().numpy()[:, 0]
-    x0, xg = sample_start_goal(METRIC_PROBLEM, 32, seed=0, sdf=sdf)
-    rg = solve_batch(METRIC_PROBLEM, x0, xg, mlp=DeviceMlp(artefact))
-    rc = O.solve_batch(METRIC_PROBLEM, x0, xg, O.HostMlp(artefact), threads=8)
-    agree, both, rel = _stats(rg, rc)
-    print("mlp agree", agree, "both", both.sum(), "rel", np.sort(rel[both]))
-    assert agree >= 0.75
-    assert both.sum() >= 5
-    assert (rel[both] <= 1e-4).mean() >= 0.6
+    x0, xg = sample_start_goal(METRIC_PROBLEM, 256, seed=0, sdf=sdf)
+    opt = _abi.gpu_options()
+    rg = solve_batch(METRIC_PROBLEM, x0, xg, mlp=DeviceMlp(artefact), options=opt)
+    hm = O.HostMlp(artefact)
+    rc = O.solve_batch(METRIC_PROBLEM, x0, xg, hm, opt=opt)
+    xp = x0.copy()
+    xp[:, 0] += 1e-13
+    rp = O.solve_batch(METRIC_PROBLEM, xp, xg, hm, opt=opt)
+
+    def agreement(ra_status, ra_cost, rb_status, rb_cost):
+        st = (ra_status == rb_status).mean()
+        both = (ra_status == 0) & (rb_status == 0)
+        rel = np.abs(ra_cost - rb_cost) / np.abs(rb_cost)
+        return st, both.sum(), (rel[both] <= 1e-4).mean() if both.any() else 1.0, rel[both]
+
+    sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
+    st_g, n_g, c_g, rel_g = agreement(sg, cg, rc["status"], rc["cost"])
+    st_s, n_s, c_s, _ = agreement(rp["status"], rp["cost"], rc["status"], rc["cost"])
+    print(f"GPU vs oracle: status {st_g:.3f}, jointly solved {n_g}, cost<=1e-4 {c_g:.3f}, median rel "
+          f"{np.median(rel_g) if len(rel_g) else 0:.2e}; oracle vs perturbed oracle: status {st_s:.3f}, "
+          f"jointly solved {n_s}, cost<=1e-4 {c_s:.3f}; GPU status counts {np.bincount(sg, minlength=7).tolist()}, "
+          f"oracle {np.bincount(rc['status'], minlength=7).tolist()}")
+    assert st_g >= 0.9 and st_g >= st_s - 0.02
+    assert n_g >= 0.25 * len(x0)
+    assert c_g >= c_s - 0.05
+
+
+def test_safeguards_iterate_parity(artefact):
+    """Second-order corrections on the GPU: two seeded metric instances whose first 10 iterations try 1 and 2
+    corrections (oracle counts); GPU and oracle iterates after k iterations agree to 20x the oracle's own
+    response to a 1e-13 change of x0 (1e-6 floor)."""
+    O = _oracle()
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import METRIC_PROBLEM
+    from nlotrajectories_amd.solver import solve_batch
+
+    mlp, hm = DeviceMlp(artefact), O.HostMlp(artefact)
+    cases = [([1.005365686594, -0.295618399728, 2.030163010282, 0.0, 0.0],
+              [0.739845159389, 0.241155138369, 2.030163010282, 0.0, 0.0]),
+             ([0.867448714288, -0.018951007036, 2.54865910057, 0.0, 0.0],
+              [-0.040290170163, 0.592694980049, 2.54865910057, 0.0, 0.0])]
+    socs = 0
+    for x0, xg in cases:
+        x0, xg = np.array(x0), np.array(xg)
+        for k in (5, 10):
+            opt = _abi.gpu_options(max_iter=k)
+            rg = solve_batch(METRIC_PROBLEM, x0[None], xg[None], mlp=mlp, options=opt)
+            rc = O.solve_one(METRIC_PROBLEM, x0, xg, hm, opt=opt)
+            xp = x0.copy()
+            xp[0] += 1e-13
+            rp = O.solve_one(METRIC_PROBLEM, xp, xg, hm, opt=opt)
+            sens = max(float(np.abs(rp[n] - rc[n]).max()) for n in ("X", "U"))
+            d = max(float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U"))
+            print("k", k, "status", rc["status"], "gpu-oracle", d, "oracle sensitivity", sens, "SOC tried", rc["soc_tried"])
+            assert rg["status"][0].item() == rc["status"] and rg["iters"][0].item() == rc["iters"]
+            assert d <= max(1e-6, 20 * sens)
+        socs += rc["soc_tried"]
+    assert socs >= 2
+
+
+def test_tiny_step_rule_matches_oracle():
+    """IPOPT's tiny-step rule, made to fire with a large tiny_step_tol: full steps without a line search, and
+    STOP_AT_TINY_STEP after two in a row — same iterations and status on the GPU and in the oracle."""
+    O = _oracle()
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.problem import BENCHMARKS
+    from nlotrajectories_amd.solver import solve_batch
+
+    b = BENCHMARKS["b2"]
+    opt = _abi.gpu_options(tiny_step_tol=5e-3, tiny_step_y_tol=1e3)
+    rg = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=opt)
+    rc = O.solve_one(b["problem"], b["start"], b["goal"], opt=opt)
+    print("tiny: oracle", rc["status"], rc["iters"], rc["tiny_steps"], "gpu", rg["status"][0].item(), rg["iters"][0].item())
+    assert rc["tiny_steps"] >= 1
+    assert rg["status"][0].item() == rc["status"] and rg["iters"][0].item() == rc["iters"]
+    np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-6)
 
 
 def test_solution_satisfies_constraints():
