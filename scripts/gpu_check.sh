@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out/check}
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
     > "$OUT/gpu_tests.log" 2>&1
 echo "pytest exit $?" >> "$OUT/gpu_tests.log"
 tail -3 "$OUT/gpu_tests.log"
