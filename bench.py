@@ -118,8 +118,12 @@ def main():
     agg = {k: 0 for k in agg_keys}
     timing = {"on": False}
 
+    nstep = {"n": 0}
+
     def step():
         r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws)
+        nstep["n"] += 1
+        print(f"[bench] rank {rank} solve {nstep['n']} done", file=sys.stderr, flush=True)
         if timing["on"]:
             st = last_stats()
             for k in agg:
@@ -176,6 +180,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
+        print("[bench] CPU baseline (oracle) ...", file=sys.stderr, flush=True)
         cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
                            a.cpu_threads, opt)
 
