@@ -9,7 +9,10 @@ over RCCL at the end of every step (the only collective).
 
 value = solved instances of all ranks in the timed steps / max-over-ranks wall time of those steps.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B]
+With --workload stress: BASELINE.json configs[4], the same NLP at N = 256 knots with the 2-256x4-1 ReLU SDF
+MLP (seeded, MlpWeights.stress_sdf_mlp), 8192 instances per GPU; the roofline is then the MLP's (f32 MFMA).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --workload metric|stress]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 import argparse
@@ -29,7 +32,7 @@ from nlotrajectories_amd import _abi  # noqa: E402
 from nlotrajectories_amd.dist import gather_solutions, max_over_ranks, rank_world, sum_over_ranks  # noqa: E402
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
-from nlotrajectories_amd.problem import METRIC_PROBLEM  # noqa: E402
+from nlotrajectories_amd.problem import METRIC_PROBLEM, STRESS_PROBLEM  # noqa: E402
 from nlotrajectories_amd.sampling import sample_start_goal  # noqa: E402
 from nlotrajectories_amd.solver import last_stats, set_timing, solve_batch  # noqa: E402
 
@@ -40,6 +43,7 @@ SPLIT_PRODUCTS = 6  # fp32-equivalent product = 6 bf16 MFMA products (nlot_mlp.h
 # (fp32) FLOPs is the dense bf16 peak / 6
 PEAK_SPLIT_TFLOPS = PEAK_BF16_MFMA_TFLOPS / SPLIT_PRODUCTS
 PEAK_HBM_GBS = 8000.0
+PEAK_F32_MFMA_NOTE = "dense f32-input MFMA peak (v_mfma_f32_16x16x4_f32; exact fp32 products)"
 
 
 def parse():
@@ -47,10 +51,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step (SURVEY.md §8d config 3: 1024 / 16384 / 65536)")
+    ap.add_argument("--workload", choices=["metric", "stress"], default="metric",
+                    help="metric = BASELINE.json's headline config; stress = configs[4] (2-256x4-1 SDF MLP, N = 256)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="instances per GPU per step (metric default 65536, SURVEY.md §8d config 3; stress default "
+                         "8192 = 65536 over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=256, help="instances for the CPU baseline on all threads (0 = skip)")
-    ap.add_argument("--cpu-sample-1core", type=int, default=8, help="instances for the single-core CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="instances for the CPU baseline on all threads (0 = skip; default 256 metric / 32 stress)")
+    ap.add_argument("--cpu-sample-1core", type=int, default=None,
+                    help="instances for the single-core CPU baseline (default 8 metric / 2 stress)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
@@ -94,9 +104,17 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    prob = METRIC_PROBLEM
-    w = MlpWeights.artefact()
+    stress = a.workload == "stress"
+    if a.batch is None:
+        a.batch = 8192 if stress else 65536
+    if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
+        a.cpu_sample = 32 if stress else 256
+    if a.cpu_sample_1core is None:
+        a.cpu_sample_1core = 2 if stress else 8
+    prob = STRESS_PROBLEM if stress else METRIC_PROBLEM
+    w = MlpWeights.stress_sdf_mlp(seed=0) if stress else MlpWeights.artefact()
     mlp = DeviceMlp(w)
+    streaming = w.hidden == 256 or w.n_hidden > 2  # nlot_mlp.hip launch_mlp_strided dispatch
 
     def sdf_gpu(pts):
         v, _, _ = sdf_mlp_eval(mlp, torch.as_tensor(pts, dtype=torch.float32, device=dev), derivatives=False)
@@ -142,7 +160,7 @@ def main():
     r = results[-1]
     solved_total = sum_over_ranks(sum(int((x["status"] == 0).sum().item()) for x in results), dev)
     iters_solved = [x["iters"][x["status"] == 0].float().mean().item() for x in results if (x["status"] == 0).any()]
-    status_counts = torch.bincount(r["status"].long(), minlength=4).cpu().numpy().tolist()
+    status_counts = torch.bincount(r["status"].long(), minlength=len(_abi.STATUS_NAMES)).cpu().numpy().tolist()
 
     # rooflines.  Dominant kernel by device time: k_ric (the Newton solve, latency/occupancy-bound fp64 with
     # ~2.8 KB of stage data per knot): HBM roofline on its algorithmic bytes.  The two SDF-MLP launches:
@@ -160,8 +178,9 @@ def main():
         if per_solve is not None:
             ric_traffic = per_solve * ric_solves_per_launch
 
-    flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1
-    flop_fwd = w.flops_per_point_fwd      # 33,536
+    flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1, 789,504 for 2-256x4-1
+    flop_fwd = w.flops_per_point_fwd      # 33,536 / 394,752
+    mlp_peak = PEAK_F32_MFMA_TFLOPS if streaming else PEAK_SPLIT_TFLOPS
     n_l = max(agg["mlp_full_launches"], 1)
     avg_ms = agg["mlp_full_ms"] / n_l
     reused = agg["mlp_points_full_reused"]
@@ -186,8 +205,63 @@ def main():
 
     if rank == 0:
         B_all = a.batch * world
+        H, L = w.hidden, w.n_hidden
+        kname = (f"mlp_stream<{H},%s> (f32 MFMA 16x16x4, weights streamed through LDS half a layer at a time)"
+                 if streaming else f"mlp_bf16<{H},%s> (fp32-equivalent products as 6 split v_mfma_f32_32x32x16_bf16)")
+        ric = {
+            "kernel": "k_ric (lane-group Riccati Newton solve, fp64)",
+            "bound": "hbm",
+            "achieved": ric_achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": ric_achieved / PEAK_HBM_GBS,
+            "traffic": ric_traffic if not stress else None,
+            "bytes_per_solve": ric_bytes,
+            "solves_per_launch": ric_solves_per_launch,
+            "avg_launch_ms": ric_avg_ms,
+            "launches": agg["ric_launches"],
+            "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
+                    "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline",
+        }
+        mlp_full = {
+            "kernel": kname % "full" + ": SDF-MLP value + gradient + Hessian",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": mlp_peak,
+            "unit": "TFLOP/s",
+            "frac": achieved / mlp_peak,
+            "peak_note": PEAK_F32_MFMA_NOTE if streaming else
+                         "dense bf16 MFMA peak 2500 TFLOP/s / 6 split products per fp32-equivalent product; "
+                         "the f32-input MFMA peak would be 157.3",
+            "traffic": traffic if not stress else None,
+            "flop_per_point": flop_pt,
+            "forward_reused_frac": reused / max(agg["mlp_points_full"], 1),
+            "flop_counting": f"executed: {flop_pt:,} per point (2-{H}x{L + 1}-1 forward + reverse sweep), less the "
+                             f"{flop_fwd:,} forward where it was reused",
+            "points_per_launch": agg["mlp_points_full"] / n_l,
+            "avg_launch_ms": avg_ms,
+            "launches": agg["mlp_full_launches"],
+        }
+        mlp_value = {
+            "kernel": kname % "value" + ": line-search trial points, value only",
+            "bound": "mfma",
+            "achieved": v_achieved,
+            "peak": mlp_peak,
+            "unit": "TFLOP/s",
+            "frac": v_achieved / mlp_peak,
+            "flop_per_point": flop_fwd,
+            "points_per_launch": agg["mlp_points_value"] / n_v,
+            "avg_launch_ms": v_avg_ms,
+            "launches": agg["mlp_value_launches"],
+        }
+        # the dominant kernel by device time: k_ric on the metric workload, the SDF-MLP on the stress workload
+        if stress:
+            rooflines = {"roofline": mlp_full, "roofline_mlp_value": mlp_value, "roofline_ric": ric}
+        else:
+            rooflines = {"roofline": ric, "roofline_mlp_full": mlp_full, "roofline_mlp_value": mlp_value}
         line = {
-            "metric": "solved trajectories/sec (50-knot unicycle+learned-SDF)",
+            "metric": "solved trajectories/sec (50-knot unicycle+learned-SDF)" if not stress else
+                      "solved trajectories/sec (stress: 256-knot unicycle + 2-256x4-1 SDF MLP)",
             "value": solved_total / elapsed,
             "unit": "trajectories/s",
             "n_gpus": world,
@@ -199,9 +273,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f64 (interior-point solver) + f32 (SDF-MLP: fp32-equivalent split-bf16 MFMA products, as "
                      "the reference's fp32 libtorch graph)",
-            "data": "synthetic start/goal (seeded, SURVEY.md §8d); learned SDF = reference artefact weights",
+            "data": "synthetic start/goal (seeded, SURVEY.md §8d); learned SDF = " +
+                    ("seeded kaiming-uniform 2-256x4-1 ReLU net, output bias centred (MlpWeights.stress_sdf_mlp)"
+                     if stress else "reference artefact weights"),
             "config": {
-                "workload": "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
+                "workload": ("stress (BASELINE.json configs[4]): unicycle_2nd, rect 0.2x0.08, N=256, dt 0.1, rho=10, "
+                             "bounds +-1, SDF MLP 2-256x4-1 ReLU (3 HxH layers), linear init, IPOPT tol 1e-4")
+                            if stress else
+                            "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
                 "mu_strategy": a.mu_strategy,
                 "instances_per_gpu": a.batch,
@@ -210,58 +289,15 @@ def main():
                 "parallelism": f"instances sharded over {world} GPU(s); RCCL gather of solutions to rank 0",
                 "solved_per_step_rank0": int((r["status"] == 0).sum().item()),
                 "status_counts_rank0": status_counts,
-                "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / a.batch for i, c in enumerate(status_counts[:4])},
+                "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / a.batch for i, c in enumerate(status_counts)
+                                       if i in _abi.STATUS_NAMES},
                 "mean_iters_solved": float(np.mean(iters_solved)) if iters_solved else 0.0,
                 "lockstep_global_steps": agg["iterations"] // max(a.steps, 1),
                 "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
                 "ric_ms_per_step": agg["ric_ms"] / max(a.steps, 1),
                 "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) / max(a.steps, 1),
             },
-            "roofline": {
-                "kernel": "k_ric (lane-group Riccati Newton solve, fp64; dominant kernel by device time)",
-                "bound": "hbm",
-                "achieved": ric_achieved,
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": ric_achieved / PEAK_HBM_GBS,
-                "traffic": ric_traffic,
-                "bytes_per_solve": ric_bytes,
-                "solves_per_launch": ric_solves_per_launch,
-                "avg_launch_ms": ric_avg_ms,
-                "launches": agg["ric_launches"],
-                "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
-                        "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline",
-            },
-            "roofline_mlp_full": {
-                "kernel": "mlp_bf16<128,full> (SDF-MLP value+grad+Hessian; fp32-equivalent products as 6 split "
-                          "v_mfma_f32_32x32x16_bf16)",
-                "bound": "mfma",
-                "achieved": achieved,
-                "peak": PEAK_SPLIT_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / PEAK_SPLIT_TFLOPS,
-                "peak_note": "dense bf16 MFMA peak 2500 TFLOP/s / 6 split products per fp32-equivalent product; "
-                             "the f32-input MFMA peak would be 157.3",
-                "traffic": traffic,
-                "flop_per_point": flop_pt,
-                "forward_reused_frac": reused / max(agg["mlp_points_full"], 1),
-                "flop_counting": "executed: 67,072 per point, less the 33,536 forward where it was reused",
-                "points_per_launch": agg["mlp_points_full"] / n_l,
-                "avg_launch_ms": avg_ms,
-                "launches": agg["mlp_full_launches"],
-            },
-            "roofline_mlp_value": {
-                "kernel": "mlp_bf16<128,value> (line-search trial points, value only)",
-                "bound": "mfma",
-                "achieved": v_achieved,
-                "peak": PEAK_SPLIT_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": v_achieved / PEAK_SPLIT_TFLOPS,
-                "flop_per_point": flop_fwd,
-                "points_per_launch": agg["mlp_points_value"] / n_v,
-                "avg_launch_ms": v_avg_ms,
-                "launches": agg["mlp_value_launches"],
-            },
+            **rooflines,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

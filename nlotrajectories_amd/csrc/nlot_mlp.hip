@@ -22,6 +22,7 @@
 //     lam*d2f/dp2 = A diag(g .* (-scale cos z)) A^T (g = df/dh0), for a ReLU input layer it is 0.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -697,12 +698,268 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
     return NLOT_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Layer-streaming kernel for nets whose weights do not fit in LDS (the stress config 2-256x4-1: three
+// 256x256 HxH layers = 768 KB of fp32; any H in {64, 128, 256} with up to kMaxStreamLayers HxH layers).
+// f32-input MFMA v_mfma_f32_16x16x4_f32 (exact fp32 products): a wave owns 16 points (column = point),
+// 16-unit tiles in 4 registers per lane (row 4 (lane >> 4) + i), and that accumulator is the B operand of
+// the next layer's product with k = 16 T + 4 (lane >> 4) + i (k order permuted consistently on A).  Each
+// HxH layer passes through LDS half a layer at a time, stored k-major with a row stride of H/2 + 4 floats so
+// one ds_read_b32 of the A operand (16 consecutive outputs x 4 k of the lane groups) hits 64 distinct banks:
+//   forward  y = W h:     rows j0 .. j0 + H/2 of W, as sW[k][j - j0]
+//   reverse  g = W^T e:   columns i0 .. i0 + H/2, as sW[j][i - i0]
+// 4 waves (one per SIMD with the whole 512-register file; 64 points) share each staged half: the weights cross
+// L2 -> LDS 4 L x 132 KB per 64 points (H = 256, L layers, value + reverse sweep), against 0.53 MFLOP per
+// point and layer for the two sweeps.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxStreamLayers = 4;
+__host__ __device__ constexpr int stream_stride(int H) { return H / 2 + 4; }
+__host__ __device__ constexpr size_t stream_lds_floats(int H) { return (size_t)H * stream_stride(H) + (size_t)5 * H; }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int H, bool FULL>
+__global__ __launch_bounds__(256, 1) void mlp_stream(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+                                                     const int* __restrict__ cnt_dev, int P_per, int64_t ld,
+                                                     const float* __restrict__ lam, MlpOut out) {
+    constexpr int HH = H / 2, NT = H / 16, NTH = NT / 2, RS = stream_stride(H);
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sW = smem;                  // staged half layer [H][RS]
+    float* sA0 = sW + (size_t)H * RS;  // [H]
+    float* sA1 = sA0 + H;              // [H]
+    float* sb0 = sA1 + H;              // [H]
+    float* sw = sb0 + H;               // [H]
+    float* sbl = sw + H;               // [H]: bias of the layer being computed
+    const int L = w.n_hidden;
+    for (int idx = threadIdx.x; idx < H; idx += blockDim.x) {
+        sA0[idx] = w.A[idx];
+        sA1[idx] = w.A[H + idx];
+        sb0[idx] = w.b0[idx];
+        sw[idx] = w.w_out[idx];
+    }
+    const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
+    const int64_t npts = cnt * P_per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pn = lane & 15, lg = lane >> 4;  // point of the lane, lane group (k / row offset 4 lg)
+    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
+    const float scale = w.scale;
+    // rows [j0, j0 + HH) of layer l, k-major: sW[k][j - j0]; and its bias
+    auto stage_rows = [&](int l, int j0) {
+        const float* src = w.W + (size_t)l * H * H + (size_t)j0 * H;
+        for (int e = threadIdx.x; e < HH * H / 4; e += blockDim.x) {
+            const int j = (4 * e) / H, k = (4 * e) % H;
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)j * H + k);
+            sW[(k + 0) * RS + j] = v.x;
+            sW[(k + 1) * RS + j] = v.y;
+            sW[(k + 2) * RS + j] = v.z;
+            sW[(k + 3) * RS + j] = v.w;
+        }
+        for (int idx = threadIdx.x; idx < H; idx += blockDim.x) sbl[idx] = w.b[(size_t)l * H + idx];
+    };
+    // columns [i0, i0 + HH) of layer l: sW[j][i - i0]
+    auto stage_cols = [&](int l, int i0) {
+        const float* src = w.W + (size_t)l * H * H;
+        for (int e = threadIdx.x; e < H * HH / 4; e += blockDim.x) {
+            const int j = (4 * e) / HH, i = (4 * e) % HH;
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)j * H + i0 + i);
+            *reinterpret_cast<float4*>(sW + j * RS + i) = v;
+        }
+    };
+    constexpr int TP = 64;  // points per block tile (4 waves x 16, one per SIMD with the whole register file)
+    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += gridDim.x) {
+        const int64_t gi = tile * TP + wave * 16 + pn;
+        const bool valid = gi < npts;
+        const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
+        float px = 0.f, py = 0.f;
+        if (valid) {
+            px = pts[2 * pi];
+            py = pts[2 * pi + 1];
+        }
+        f32x4 acc[NT];
+        uint32_t mask[kMaxStreamLayers][NT / 8];  // ReLU bit (4 t + i) % 32 of word (4 t + i) / 32, layer l
+        // ---------------- forward: layer 0 from the input layer computed on the fly, then the others ----------
+#pragma unroll 1
+        for (int l = 0; l < L; ++l) {
+            f32x4 nacc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) nacc[t] = f32x4{};
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                __syncthreads();
+                stage_rows(l, hh * HH);
+                __syncthreads();
+#pragma unroll
+                for (int T = 0; T < NT; ++T)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int k = 16 * T + 4 * lg + i;
+                        float bv;
+                        if (l == 0) {
+                            const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
+                            if (fourier) {
+                                float sn, cs;
+                                sincos_fourier(z, &sn, &cs);
+                                bv = cs * scale;
+                            } else {
+                                bv = z > 0.f ? z : 0.f;
+                            }
+                        } else {
+                            bv = acc[T][i];
+                        }
+#pragma unroll
+                        for (int t = 0; t < NTH; ++t)
+                            nacc[hh * NTH + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sW[k * RS + 16 * t + pn], bv,
+                                                                                    nacc[hh * NTH + t], 0, 0, 0);
+                        asm volatile("" ::: "memory");  // bound the LDS loads the scheduler hoists (register file)
+                    }
+            }
+            // bias + ReLU (the bias of layer l was staged with its rows)
+#pragma unroll
+            for (int q = 0; q < NT / 8; ++q) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 8 * q + tt;
+                        const float v = nacc[t][i] + sbl[16 * t + 4 * lg + i];
+                        const bool on = v > 0.f;
+                        acc[t][i] = on ? v : 0.f;
+                        m |= (uint32_t)on << (4 * tt + i);
+                    }
+                mask[l][q] = m;
+            }
+        }
+        auto lsum = [](float v) {  // sum over the 4 lane groups (the 4 k / row offsets of a point)
+            v += __shfl_xor(v, 16);
+            return v + __shfl_xor(v, 32);
+        };
+        float fpart = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fpart = fmaf(sw[16 * t + 4 * lg + i], acc[t][i], fpart);
+        const float f = lsum(fpart) + w.b_out;
+        if constexpr (!FULL) {
+            if (valid && lg == 0) out.val[pi * out.sv] = f;
+            continue;
+        } else {
+            // ---------------- reverse sweep: e = lam w_out .* mask_top; g = W_l^T e; e = g .* mask_{l-1} ----
+            const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[t][i] = ((mask[L - 1][t >> 3] >> (4 * (t & 7) + i)) & 1) ? lm * sw[16 * t + 4 * lg + i] : 0.f;
+#pragma unroll 1
+            for (int l = L - 1; l >= 0; --l) {
+                f32x4 g[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) g[t] = f32x4{};
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    __syncthreads();
+                    stage_cols(l, hh * HH);
+                    __syncthreads();
+#pragma unroll
+                    for (int T = 0; T < NT; ++T)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int j = 16 * T + 4 * lg + i;
+                            const float bv = acc[T][i];
+#pragma unroll
+                            for (int t = 0; t < NTH; ++t)
+                                g[hh * NTH + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sW[j * RS + 16 * t + pn], bv,
+                                                                                     g[hh * NTH + t], 0, 0, 0);
+                            asm volatile("" ::: "memory");
+                        }
+                }
+                if (l > 0) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[t][i] = ((mask[l - 1][t >> 3] >> (4 * (t & 7) + i)) & 1) ? g[t][i] : 0.f;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) acc[t] = g[t];
+                }
+            }
+            // acc = lam df/dh0: contract with the input layer's derivatives (lane = (k, point))
+            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int k = 16 * t + 4 * lg + i;
+                    const float ax = sA0[k], ay = sA1[k];
+                    const float z = fmaf(py, ay, px * ax) + sb0[k];
+                    const float d = acc[t][i];
+                    float dz, c2;
+                    if (fourier) {
+                        float sn, cs;
+                        sincos_fourier(z, &sn, &cs);
+                        dz = d * (-scale * sn);
+                        c2 = d * (-scale * cs);
+                    } else {
+                        dz = z > 0.f ? d : 0.f;
+                        c2 = 0.f;
+                    }
+                    gx = fmaf(ax, dz, gx);
+                    gy = fmaf(ay, dz, gy);
+                    hxx = fmaf(ax * ax, c2, hxx);
+                    hxy = fmaf(ax * ay, c2, hxy);
+                    hyy = fmaf(ay * ay, c2, hyy);
+                }
+            gx = lsum(gx);
+            gy = lsum(gy);
+            hxx = lsum(hxx);
+            hxy = lsum(hxy);
+            hyy = lsum(hyy);
+            if (valid && lg == 0) {
+                out.val[pi * out.sv] = f;
+                if (out.gx) {
+                    out.gx[pi * out.sg] = gx;
+                    out.gy[pi * out.sg] = gy;
+                }
+                if (out.hxx) {
+                    out.hxx[pi * out.sh] = hxx;
+                    out.hxy[pi * out.sh] = hxy;
+                    if (out.hyx != out.hxy) out.hyx[pi * out.sh] = hxy;
+                    out.hyy[pi * out.sh] = hyy;
+                }
+            }
+        }
+    }
+}
+
+template <int H, bool FULL>
+static int launch_stream(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                         const float* lam, const MlpOut& out, hipStream_t stream) {
+    const size_t lds = sizeof(float) * stream_lds_floats(H);
+    static std::atomic<uint64_t> attr{0};
+    NLOT_HIP_CHECK(set_lds_attr_once(attr, (const void*)mlp_stream<H, FULL>, (int)lds));
+    const int64_t tiles = (n * P_per + 63) / 64;
+    const int64_t cap = device_cus();
+    const int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
+    hipLaunchKernelGGL((mlp_stream<H, FULL>), dim3(grid), dim3(256), lds, stream, w, pts, n, n_dev, P_per, ld, lam, out);
+    NLOT_HIP_CHECK(hipGetLastError());
+    return NLOT_OK;
+}
+
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                        const float* lam, const MlpOut& out, bool full, hipStream_t stream, const MlpReuse* reuse) {
     if (n <= 0) return NLOT_OK;
-    if (w.n_hidden < 1 || w.n_hidden > kMaxResidentLayers) {
-        set_error("MLP kernel: 1 or 2 hidden HxH layers are supported (DESIGN.md §7)");
+    if (w.n_hidden < 1 || w.n_hidden > kMaxStreamLayers) {
+        set_error("MLP kernel: 1 to 4 hidden HxH layers are supported (DESIGN.md §7)");
         return NLOT_ERR_INVALID;
+    }
+    // weights beyond LDS (H = 256, or more than 2 HxH layers): the layer-streaming kernel
+    if (w.H == 256 || w.n_hidden > kMaxResidentLayers) {
+        if (w.H == 256) return full ? launch_stream<256, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream)
+                                    : launch_stream<256, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+        if (w.H == 128) return full ? launch_stream<128, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream)
+                                    : launch_stream<128, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+        if (w.H == 64) return full ? launch_stream<64, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream)
+                                   : launch_stream<64, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
     }
 #define NLOT_MLP_CASE(HH, LL)                                                                      \
     if (w.H == HH && w.n_hidden == LL)                                                             \
@@ -714,7 +971,7 @@ int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* 
     NLOT_MLP_CASE(128, 2)
 #undef NLOT_MLP_CASE
     {
-        set_error("MLP kernel: hidden width must be 64 or 128 (DESIGN.md §7)");
+        set_error("MLP kernel: hidden width must be 64, 128 or 256 (DESIGN.md §7)");
         return NLOT_ERR_INVALID;
     }
 }
@@ -734,8 +991,9 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
         set_error("nlot_mlp_create: only ReLU hidden layers with a Fourier or Linear+ReLU input layer");
         return nullptr;
     }
-    if ((d->hidden != 64 && d->hidden != 128) || d->n_hidden < 1 || d->n_hidden > kMaxResidentLayers) {
-        set_error("nlot_mlp_create: hidden width 64/128 with 1-2 hidden layers supported (DESIGN.md §7)");
+    if ((d->hidden != 64 && d->hidden != 128 && d->hidden != 256) || d->n_hidden < 1 ||
+        d->n_hidden > kMaxStreamLayers) {
+        set_error("nlot_mlp_create: hidden width 64/128/256 with 1-4 hidden HxH layers supported (DESIGN.md §7)");
         return nullptr;
     }
     const int H = d->hidden, L = d->n_hidden;

@@ -233,3 +233,18 @@ class MlpWeights:
                     mod.weight.uniform_(-bound, bound, generator=gen)
                     mod.bias.zero_()
         return MlpWeights.from_module(m)
+
+    @staticmethod
+    def stress_sdf_mlp(seed=0, hidden=256, n_hidden=3) -> "MlpWeights":
+        """The stress configuration's SDF net: random_relu_mlp(256, 3, seed) with its output bias set to
+        minus the median of the net over a 64 x 64 grid of the sampling box [-0.3, 1.3]^2, so that about
+        half of the box is free space (a zero-bias ReLU net is positively homogeneous, and seed 0 is
+        negative on 98 % of the box)."""
+        w = MlpWeights.random_relu_mlp(hidden, n_hidden, seed)
+        m = w.torch_module().double()
+        g = torch.linspace(-0.3, 1.3, 64, dtype=torch.float64)
+        P = torch.stack(torch.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+        with torch.no_grad():
+            med = m(P)[:, 0].median().item()
+            m.output_layer.bias.fill_(-med)
+        return MlpWeights.from_module(m.float())

@@ -173,3 +173,7 @@ METRIC_PROBLEM = Problem(dynamics="unicycle_2nd", shape="rectangle", length=0.2,
 
 def heading(start_xy, goal_xy) -> float:
     return math.atan2(goal_xy[1] - start_xy[1], goal_xy[0] - start_xy[0])
+
+# The stress configuration (BASELINE.json configs[4]): the metric NLP at N = 256 knots (same dt,
+# a 25.6 s horizon) with the 2-256x4-1 ReLU SDF MLP (MlpWeights.random_relu_mlp(256, 3), seeded kaiming).
+STRESS_PROBLEM = METRIC_PROBLEM.with_(N=256)

@@ -28,7 +28,11 @@ def sample_start_goal(problem: Problem, B: int, seed: int = 0, sdf=None, lo=(-0.
     nx = problem.nx
     out0, outg = [], []
     lo, hi = np.asarray(lo, float), np.asarray(hi, float)
+    rounds = 0
     while sum(len(a) for a in out0) < B:
+        rounds += 1
+        if rounds > 64 and sum(len(a) for a in out0) < rounds:
+            raise RuntimeError("sample_start_goal: the scene leaves almost no free start/goal pairs in the box")
         n = max(4 * B, 1024)
         s = lo + (hi - lo) * rng.random((n, 2))
         g = lo + (hi - lo) * rng.random((n, 2))
