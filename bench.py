@@ -108,9 +108,9 @@ def main():
     if a.batch is None:
         a.batch = 8192 if stress else 65536
     if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
-        a.cpu_sample = 32 if stress else 256
+        a.cpu_sample = 16 if stress else 256
     if a.cpu_sample_1core is None:
-        a.cpu_sample_1core = 2 if stress else 8
+        a.cpu_sample_1core = 1 if stress else 8
     prob = STRESS_PROBLEM if stress else METRIC_PROBLEM
     w = MlpWeights.stress_sdf_mlp(seed=0) if stress else MlpWeights.artefact()
     mlp = DeviceMlp(w)
@@ -200,8 +200,14 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         print("[bench] CPU baseline (oracle) ...", file=sys.stderr, flush=True)
-        cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
-                           a.cpu_threads, opt)
+        if stress:  # per-iteration estimate (cpu_baseline docstring); iterations of ALL instances per solved one
+            tot_it = sum(int(x["iters"].sum().item()) for x in results)
+            n_solved = max(sum(int((x["status"] == 0).sum().item()) for x in results), 1)
+            cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
+                               a.cpu_threads, opt, iter_cap=10, gpu_iters_per_solved=tot_it / n_solved)
+        else:
+            cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
+                               a.cpu_threads, opt)
 
     if rank == 0:
         B_all = a.batch * world
@@ -305,9 +311,14 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt):
+def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu_iters_per_solved=None):
     """The oracle (C restatement, OpenMP over instances) on bounded samples of the same workload: the first
-    n_all instances of rank 0's batch on `threads` host threads, and the first n_one on one thread."""
+    n_all instances of rank 0's batch on `threads` host threads, and the first n_one on one thread, in chunks
+    of `threads` instances with a progress line after each.
+
+    iter_cap (the stress workload, where one oracle iteration costs ~1 s of fp32 MLP work on a core): the
+    sample runs at most iter_cap iterations per instance, and the value is an ESTIMATE = 1 / (measured
+    seconds per instance-iteration x the GPU run's iterations per solved instance), stated in `sample`."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
@@ -319,22 +330,46 @@ def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt):
         avail = os.cpu_count() or 1
     threads = max(1, min(threads, avail))
     hm = O.HostMlp(w)
+    run_opt = type(opt).from_buffer_copy(opt)
+    if iter_cap is not None:
+        run_opt.max_iter = iter_cap
 
     def run(n, th):
         t = time.perf_counter()
-        r = O.solve_batch(prob, x0[:n], xg[:n], hm, opt=opt, threads=th)
-        dt = time.perf_counter() - t
-        return int((r["status"] == 0).sum()), dt, np.bincount(r["status"], minlength=4).tolist()
+        st, its = [], []
+        for c0 in range(0, n, th):
+            r = O.solve_batch(prob, x0[c0:min(n, c0 + th)], xg[c0:min(n, c0 + th)], hm, opt=run_opt, threads=th)
+            st.append(r["status"])
+            its.append(r["iters"])
+            print(f"[bench] cpu baseline: {min(n, c0 + th)}/{n} instances on {th} thread(s), "
+                  f"{time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
+        st, its = np.concatenate(st), np.concatenate(its)
+        return int((st == 0).sum()), time.perf_counter() - t, np.bincount(st, minlength=7).tolist(), int(its.sum())
 
-    ns, dt, sc = run(n_all, threads)
-    out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
-           "sample": f"first {n_all} instances of rank 0's seeded batch: {ns} solved (status counts {sc}) in "
-                     f"{dt:.1f} s on {threads} OpenMP threads (host: os.cpu_count() = {os.cpu_count()}, "
-                     f"affinity = {avail} CPUs; the box's CPU share is 16)"}
+    host = (f"(host: os.cpu_count() = {os.cpu_count()}, affinity = {avail} CPUs; the box's CPU share is 16)")
+    ns, dt, sc, it = run(n_all, threads)
+    if iter_cap is None:
+        out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
+               "sample": f"first {n_all} instances of rank 0's seeded batch: {ns} solved (status counts {sc}) in "
+                         f"{dt:.1f} s on {threads} OpenMP threads {host}"}
+    else:
+        per_it = dt / max(it, 1)
+        out = {"value": 1.0 / (per_it * gpu_iters_per_solved), "unit": "trajectories/s", "cores": threads,
+               "kind": "port", "estimate": True,
+               "sample": f"first {n_all} instances of rank 0's seeded batch, at most {iter_cap} iterations each: "
+                         f"{it} instance-iterations in {dt:.1f} s on {threads} OpenMP threads {host} = "
+                         f"{per_it * 1e3:.1f} ms per instance-iteration; value = 1 / (that x the GPU run's "
+                         f"{gpu_iters_per_solved:.1f} iterations per solved instance)"}
     if n_one > 0:
-        ns1, dt1, _ = run(n_one, 1)
-        out["single_core"] = {"value": ns1 / dt1, "cores": 1,
-                              "sample": f"first {n_one} instances: {ns1} solved in {dt1:.1f} s on 1 thread"}
+        ns1, dt1, _, it1 = run(n_one, 1)
+        if iter_cap is None:
+            out["single_core"] = {"value": ns1 / dt1, "cores": 1,
+                                  "sample": f"first {n_one} instances: {ns1} solved in {dt1:.1f} s on 1 thread"}
+        else:
+            out["single_core"] = {"value": 1.0 / (dt1 / max(it1, 1) * gpu_iters_per_solved), "cores": 1,
+                                  "estimate": True,
+                                  "sample": f"first {n_one} instances, at most {iter_cap} iterations: {it1} "
+                                            f"instance-iterations in {dt1:.1f} s on 1 thread"}
     return out
 
 

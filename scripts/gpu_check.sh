@@ -23,6 +23,9 @@ if [ -n "$STRESS_BENCH" ]; then
   timeout -k 10 600 python -u bench.py --workload stress --steps 1 --warmup 1 > "$OUT/bench_stress.json" \
       2> "$OUT/bench_stress.err" || exit $?
   tail -c 1500 "$OUT/bench_stress.json"
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof_stress" -o run \
+      --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload stress --steps 1 --warmup 0 \
+      --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/prof_stress_bench.json" 2>&1) || exit $?
 fi
 if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" && \

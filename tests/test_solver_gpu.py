@@ -189,16 +189,20 @@ def test_safeguards_iterate_parity(artefact):
 
 def test_tiny_step_rule_matches_oracle():
     """IPOPT's tiny-step rule, made to fire with a large tiny_step_tol: full steps without a line search, and
-    STOP_AT_TINY_STEP after two in a row — same iterations and status on the GPU and in the oracle."""
+    STOP_AT_TINY_STEP after two in a row — same iterations and status on the GPU and in the oracle.  The
+    start/goal pair is one where the oracle's outcome is reproducible (a 1e-13 start perturbation moves the
+    iterate by 9e-13; the YAML's diagonal pair is chaotic: 94 vs 131 iterations under that perturbation)."""
     O = _oracle()
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.solver import solve_batch
 
     b = BENCHMARKS["b2"]
-    opt = _abi.gpu_options(tiny_step_tol=5e-3, tiny_step_y_tol=1e3)
-    rg = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=opt)
-    rc = O.solve_one(b["problem"], b["start"], b["goal"], opt=opt)
+    x0, xg = [0.0, 0.05, 0.0, 0.0, 0.0], [1.0, 0.1, 0.0, 0.0, 0.0]
+    opt = _abi.gpu_options(tiny_step_tol=0.1, tiny_step_y_tol=1e3)
+    rg = solve_batch(b["problem"], np.array([x0]), np.array([xg]), options=opt)
+    rc = O.solve_one(b["problem"], x0, xg, opt=opt)
+    assert rc["status"] == _abi.NLOT_TINY_STEP
     print("tiny: oracle", rc["status"], rc["iters"], rc["tiny_steps"], "gpu", rg["status"][0].item(), rg["iters"][0].item())
     assert rc["tiny_steps"] >= 1
     assert rg["status"][0].item() == rc["status"] and rg["iters"][0].item() == rc["iters"]
