@@ -703,67 +703,119 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
 // 256x256 HxH layers = 768 KB of fp32; any H in {64, 128, 256} with up to kMaxStreamLayers HxH layers).
 // f32-input MFMA v_mfma_f32_16x16x4_f32 (exact fp32 products): a wave owns 16 points (column = point),
 // 16-unit tiles in 4 registers per lane (row 4 (lane >> 4) + i), and that accumulator is the B operand of
-// the next layer's product with k = 16 T + 4 (lane >> 4) + i (k order permuted consistently on A).  Each
-// HxH layer passes through LDS half a layer at a time, stored k-major with a row stride of H/2 + 4 floats so
-// one ds_read_b32 of the A operand (16 consecutive outputs x 4 k of the lane groups) hits 64 distinct banks:
-//   forward  y = W h:     rows j0 .. j0 + H/2 of W, as sW[k][j - j0]
-//   reverse  g = W^T e:   columns i0 .. i0 + H/2, as sW[j][i - i0]
-// 4 waves (one per SIMD with the whole 512-register file; 64 points) share each staged half: the weights cross
-// L2 -> LDS 4 L x 132 KB per 64 points (H = 256, L layers, value + reverse sweep), against 0.53 MFLOP per
-// point and layer for the two sweeps.
+// the next layer's product with k = 16 T + 4 (lane >> 4) + i (k order permuted consistently on A).
+// Weights pass through LDS a quarter layer (a "unit") at a time, software-pipelined: the global loads of
+// unit u + 1 are issued into registers before the MFMAs of unit u, so their L2 latency hides under the
+// 8192 MFMA cycles per wave of a quarter (H = 256).  A unit is stored with a row stride of H/4 + 4 floats,
+// so every ds_read_b32 of an A operand (16 consecutive outputs x 4 k of the lane groups) hits 64 banks:
+//   forward  y = W h:     rows j0 .. j0 + H/4 of W, k-major: sW[k][j - j0]
+//   reverse  g = W^T e:   columns i0 .. i0 + H/4, as sW[j][i - i0]
+// 4 waves (one per SIMD with the whole 512-register file; 64 points per block tile) share each unit: the
+// weights cross L2 -> LDS 4 L x 4 B H^2 per 64 points for value + reverse sweep (3 MB at H = 256, L = 3).
 // ---------------------------------------------------------------------------------------------
 constexpr int kMaxStreamLayers = 4;
-__host__ __device__ constexpr int stream_stride(int H) { return H / 2 + 4; }
-__host__ __device__ constexpr size_t stream_lds_floats(int H) { return (size_t)H * stream_stride(H) + (size_t)5 * H; }
+__host__ __device__ constexpr int stream_stride(int H) { return H / 4 + 4; }
+__host__ __device__ constexpr size_t stream_lds_floats(int H) {
+    return (size_t)H * stream_stride(H) + (size_t)4 * H + (size_t)kMaxStreamLayers * H;
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int H, bool FULL>
 __global__ __launch_bounds__(256, 1) void mlp_stream(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
                                                      const int* __restrict__ cnt_dev, int P_per, int64_t ld,
                                                      const float* __restrict__ lam, MlpOut out) {
-    constexpr int HH = H / 2, NT = H / 16, NTH = NT / 2, RS = stream_stride(H);
+    constexpr int Q = H / 4, NQ = Q / 16, NT = H / 16, RS = stream_stride(H);
+    constexpr int PF = H * H / 4096;  // float4 of a unit per thread (Q x H floats over 256 threads)
+    static_assert(PF >= 1 && NQ >= 1, "H >= 64");
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* sW = smem;                  // staged half layer [H][RS]
+    float* sW = smem;                  // the staged unit [H][RS]
     float* sA0 = sW + (size_t)H * RS;  // [H]
     float* sA1 = sA0 + H;              // [H]
     float* sb0 = sA1 + H;              // [H]
     float* sw = sb0 + H;               // [H]
-    float* sbl = sw + H;               // [H]: bias of the layer being computed
+    float* sbl = sw + H;               // [kMaxStreamLayers][H]: HxH layer biases
     const int L = w.n_hidden;
-    for (int idx = threadIdx.x; idx < H; idx += blockDim.x) {
+    for (int idx = threadIdx.x; idx < H; idx += 256) {
         sA0[idx] = w.A[idx];
         sA1[idx] = w.A[H + idx];
         sb0[idx] = w.b0[idx];
         sw[idx] = w.w_out[idx];
     }
+    for (int idx = threadIdx.x; idx < L * H; idx += 256) sbl[idx] = w.b[idx];
+    __syncthreads();  // the input layer is read by every wave before the first staging barrier
     const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
     const int64_t npts = cnt * P_per;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pn = lane & 15, lg = lane >> 4;  // point of the lane, lane group (k / row offset 4 lg)
     const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
     const float scale = w.scale;
-    // rows [j0, j0 + HH) of layer l, k-major: sW[k][j - j0]; and its bias
-    auto stage_rows = [&](int l, int j0) {
-        const float* src = w.W + (size_t)l * H * H + (size_t)j0 * H;
-        for (int e = threadIdx.x; e < HH * H / 4; e += blockDim.x) {
-            const int j = (4 * e) / H, k = (4 * e) % H;
-            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)j * H + k);
-            sW[(k + 0) * RS + j] = v.x;
-            sW[(k + 1) * RS + j] = v.y;
-            sW[(k + 2) * RS + j] = v.z;
-            sW[(k + 3) * RS + j] = v.w;
+    // units of one block tile: forward (layer l, quarter q) = 4 l + q; FULL adds the reverse sweep,
+    // 4 L + 4 (L - 1 - l) + q
+    const int U = FULL ? 8 * L : 4 * L;
+    float4 pf[PF];
+    // Forward units: a wave covers 16 rows x 16 k per float4 pass (lane = jj + 16 kk: row 16 jb + jj, k = 16 kq +
+    // 4 kk .. + 3), so each transposed ds_write_b32 hits bank 16 kk + jj + const: 64 distinct banks.
+    // Reverse units: 16-byte row pieces, stored as they are.
+    // Per-thread parts of the unit addresses; the rest are compile-time offsets per r (a runtime-indexed
+    // address set would be hoisted out of the tile loop into registers)
+    constexpr int KQ = H / 16, QC = Q / 4;
+    const int jj = threadIdx.x & 15, kk = (threadIdx.x >> 4) & 3, w4 = threadIdx.x >> 6;
+    const int fwd_g = jj * H + 16 * w4 + 4 * kk, fwd_s = (16 * w4 + 4 * kk) * RS + jj;
+    const int rev_g = (threadIdx.x / QC) * H + 4 * (threadIdx.x % QC), rev_s = (threadIdx.x / QC) * RS + 4 * (threadIdx.x % QC);
+    auto fetch = [&](int u) {
+        const bool fwd = u < 4 * L;
+        const int l = fwd ? (u >> 2) : L - 1 - ((u - 4 * L) >> 2), q = u & 3;
+        const float* src = w.W + (size_t)l * H * H + (fwd ? q * Q * H + fwd_g : q * Q + rev_g);
+        if (fwd) {
+#pragma unroll
+            for (int r = 0; r < PF; ++r)
+                pf[r] = *reinterpret_cast<const float4*>(src + 16 * ((4 * r) / KQ) * H + 16 * ((4 * r) % KQ));
+        } else {
+#pragma unroll
+            for (int r = 0; r < PF; ++r) pf[r] = *reinterpret_cast<const float4*>(src + (256 * r / QC) * H);
         }
-        for (int idx = threadIdx.x; idx < H; idx += blockDim.x) sbl[idx] = w.b[(size_t)l * H + idx];
     };
-    // columns [i0, i0 + HH) of layer l: sW[j][i - i0]
-    auto stage_cols = [&](int l, int i0) {
-        const float* src = w.W + (size_t)l * H * H;
-        for (int e = threadIdx.x; e < H * HH / 4; e += blockDim.x) {
-            const int j = (4 * e) / HH, i = (4 * e) % HH;
-            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)j * H + i0 + i);
-            *reinterpret_cast<float4*>(sW + j * RS + i) = v;
+    auto commit = [&](int u) {
+        if (u < 4 * L) {
+#pragma unroll
+            for (int r = 0; r < PF; ++r) {
+                float* d = sW + fwd_s + 16 * ((4 * r) % KQ) * RS + 16 * ((4 * r) / KQ);
+                d[0] = pf[r].x;
+                d[RS] = pf[r].y;
+                d[2 * RS] = pf[r].z;
+                d[3 * RS] = pf[r].w;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < PF; ++r) *reinterpret_cast<float4*>(sW + rev_s + (256 * r / QC) * RS) = pf[r];
         }
     };
+    // acc_q[t] += W_unit(16 t + pn, k) B(k), k over all H (both sweeps read the unit as sW[k][16 t + pn]); the A
+    // operands of group (T, i) are loaded one group ahead of its MFMAs (one wave per SIMD: nothing else hides the
+    // LDS latency)
+    auto unit_mfma = [&](f32x4* accq, const f32x4* bsrc) {
+        float a_cur[NQ];
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) a_cur[t] = sW[(4 * lg) * RS + 16 * t + pn];
+#pragma unroll
+        for (int T = 0; T < NT; ++T)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float a_nxt[NQ];
+                if (4 * T + i + 1 < 4 * NT) {
+                    const int kn = 16 * ((4 * T + i + 1) >> 2) + 4 * lg + ((i + 1) & 3);
+#pragma unroll
+                    for (int t = 0; t < NQ; ++t) a_nxt[t] = sW[kn * RS + 16 * t + pn];
+                }
+                const float bv = bsrc[T][i];
+#pragma unroll
+                for (int t = 0; t < NQ; ++t) accq[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], bv, accq[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < NQ; ++t) a_cur[t] = a_nxt[t];
+                asm volatile("" ::: "memory");  // bound the LDS loads the scheduler hoists (register file)
+            }
+    };
+    fetch(0);
     constexpr int TP = 64;  // points per block tile (4 waves x 16, one per SIMD with the whole register file)
     for (int64_t tile = blockIdx.x; tile * TP < npts; tile += gridDim.x) {
         const int64_t gi = tile * TP + wave * 16 + pn;
@@ -775,58 +827,53 @@ __global__ __launch_bounds__(256, 1) void mlp_stream(MlpDev w, const float* __re
             py = pts[2 * pi + 1];
         }
         f32x4 acc[NT];
-        uint32_t mask[kMaxStreamLayers][NT / 8];  // ReLU bit (4 t + i) % 32 of word (4 t + i) / 32, layer l
-        // ---------------- forward: layer 0 from the input layer computed on the fly, then the others ----------
+        uint32_t mask[kMaxStreamLayers][NT / 8 > 0 ? NT / 8 : 1];  // ReLU bit 4 (t & 7) + i of word t >> 3
+        // input layer h0 (unit k = 16 T + 4 lg + i of the lane's point), computed once into the B registers
+#pragma unroll
+        for (int T = 0; T < NT; ++T)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = 16 * T + 4 * lg + i;
+                const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
+                if (fourier) {
+                    float sn, cs;
+                    sincos_fourier(z, &sn, &cs);
+                    acc[T][i] = cs * scale;
+                } else {
+                    acc[T][i] = z > 0.f ? z : 0.f;
+                }
+            }
+        // ---------------- forward through the HxH layers ----------------
 #pragma unroll 1
         for (int l = 0; l < L; ++l) {
             f32x4 nacc[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) nacc[t] = f32x4{};
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
+            for (int q = 0; q < 4; ++q) {
+                const int u = 4 * l + q;
                 __syncthreads();
-                stage_rows(l, hh * HH);
+                commit(u);
                 __syncthreads();
-#pragma unroll
-                for (int T = 0; T < NT; ++T)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int k = 16 * T + 4 * lg + i;
-                        float bv;
-                        if (l == 0) {
-                            const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
-                            if (fourier) {
-                                float sn, cs;
-                                sincos_fourier(z, &sn, &cs);
-                                bv = cs * scale;
-                            } else {
-                                bv = z > 0.f ? z : 0.f;
-                            }
-                        } else {
-                            bv = acc[T][i];
-                        }
-#pragma unroll
-                        for (int t = 0; t < NTH; ++t)
-                            nacc[hh * NTH + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sW[k * RS + 16 * t + pn], bv,
-                                                                                    nacc[hh * NTH + t], 0, 0, 0);
-                        asm volatile("" ::: "memory");  // bound the LDS loads the scheduler hoists (register file)
-                    }
+                fetch(u + 1 < U ? u + 1 : 0);
+                unit_mfma(nacc + q * NQ, acc);
             }
-            // bias + ReLU (the bias of layer l was staged with its rows)
+            const float* bl = sbl + l * H;
 #pragma unroll
-            for (int q = 0; q < NT / 8; ++q) {
+            for (int t = 0; t < NT; ++t) {
                 uint32_t m = 0;
 #pragma unroll
-                for (int tt = 0; tt < 8; ++tt)
+                for (int i = 0; i < 4; ++i) {
+                    const float v = nacc[t][i] + bl[16 * t + 4 * lg + i];
+                    const bool on = v > 0.f;
+                    acc[t][i] = on ? v : 0.f;
+                    m |= (uint32_t)on << (4 * (t & 7) + i);
+                }
+                if constexpr (FULL) {  // layer index is runtime: predicated writes keep the masks in registers
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int t = 8 * q + tt;
-                        const float v = nacc[t][i] + sbl[16 * t + 4 * lg + i];
-                        const bool on = v > 0.f;
-                        acc[t][i] = on ? v : 0.f;
-                        m |= (uint32_t)on << (4 * tt + i);
-                    }
-                mask[l][q] = m;
+                    for (int ll = 0; ll < kMaxStreamLayers; ++ll)
+                        if (ll == l) mask[ll][t >> 3] = (t & 7) == 0 ? m : (mask[ll][t >> 3] | m);
+                }
             }
         }
         auto lsum = [](float v) {  // sum over the 4 lane groups (the 4 k / row offsets of a point)
@@ -845,39 +892,36 @@ __global__ __launch_bounds__(256, 1) void mlp_stream(MlpDev w, const float* __re
         } else {
             // ---------------- reverse sweep: e = lam w_out .* mask_top; g = W_l^T e; e = g .* mask_{l-1} ----
             const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
+            auto mask_of = [&](int l, int word) {  // mask[l][word] for a runtime l, by selects
+                uint32_t m = mask[0][word];
+#pragma unroll
+                for (int ll = 1; ll < kMaxStreamLayers; ++ll) m = ll == l ? mask[ll][word] : m;
+                return m;
+            };
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    acc[t][i] = ((mask[L - 1][t >> 3] >> (4 * (t & 7) + i)) & 1) ? lm * sw[16 * t + 4 * lg + i] : 0.f;
+                    acc[t][i] = ((mask_of(L - 1, t >> 3) >> (4 * (t & 7) + i)) & 1) ? lm * sw[16 * t + 4 * lg + i] : 0.f;
 #pragma unroll 1
             for (int l = L - 1; l >= 0; --l) {
                 f32x4 g[NT];
 #pragma unroll
                 for (int t = 0; t < NT; ++t) g[t] = f32x4{};
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
+                for (int q = 0; q < 4; ++q) {
+                    const int u = 4 * L + 4 * (L - 1 - l) + q;
                     __syncthreads();
-                    stage_cols(l, hh * HH);
+                    commit(u);
                     __syncthreads();
-#pragma unroll
-                    for (int T = 0; T < NT; ++T)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int j = 16 * T + 4 * lg + i;
-                            const float bv = acc[T][i];
-#pragma unroll
-                            for (int t = 0; t < NTH; ++t)
-                                g[hh * NTH + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sW[j * RS + 16 * t + pn], bv,
-                                                                                     g[hh * NTH + t], 0, 0, 0);
-                            asm volatile("" ::: "memory");
-                        }
+                    fetch(u + 1 < U ? u + 1 : 0);
+                    unit_mfma(g + q * NQ, acc);
                 }
                 if (l > 0) {
 #pragma unroll
                     for (int t = 0; t < NT; ++t)
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) acc[t][i] = ((mask[l - 1][t >> 3] >> (4 * (t & 7) + i)) & 1) ? g[t][i] : 0.f;
+                        for (int i = 0; i < 4; ++i) acc[t][i] = ((mask_of(l - 1, t >> 3) >> (4 * (t & 7) + i)) & 1) ? g[t][i] : 0.f;
                 } else {
 #pragma unroll
                     for (int t = 0; t < NT; ++t) acc[t] = g[t];

@@ -2875,7 +2875,14 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     }
     g_stats.slots_in_lds = 0;  // stage slots live in the HBM workspace; k_ric stages them through LDS
     const int ric_blocks_per = RicG<DYN>::IPW;
-    int spec_threshold = 8192, spec_bulk = 1;  // measured best of {512, 2048, 8192} x {1, 2} (B = 65536)
+    // speculation while one value launch stays below ~56 GFLOP of forward work: 8192 instances of the metric
+    // (P = 204 corners x 33,536 FLOP; measured best of {512, 2048, 8192} x {1, 2} at B = 65536), 138 of the
+    // stress config (P = 1028 x 394,752 FLOP)
+    int spec_threshold = 8192, spec_bulk = 1;
+    if (use_mlp) {
+        const double H = mlp->dev.H, fwd = 2.0 * (2.0 * H + mlp->dev.n_hidden * H * H + H);
+        spec_threshold = (int)std::max(1.0, std::min(1e9, 5.6e10 / (fwd * (double)P)));
+    }
     if (const char* e = getenv("NLOT_SPEC_THRESHOLD")) spec_threshold = atoi(e);
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
     const int max_steps = (o.max_iter + 2) * 64;

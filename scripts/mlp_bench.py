@@ -9,8 +9,9 @@ import torch  # noqa: E402
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
 
+stress = len(sys.argv) > 2 and sys.argv[2] == "stress"  # python scripts/mlp_bench.py P [stress]
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 16384 * 204
-w = MlpWeights.artefact()
+w = MlpWeights.stress_sdf_mlp(0) if stress else MlpWeights.artefact()
 mlp = DeviceMlp(w)
 pts = (torch.rand(P, 2, device="cuda") * 1.6 - 0.3).contiguous()
 for full in (True, False):
