@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 5
+#define NLOT_ABI_VERSION 6
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -67,8 +67,11 @@ enum NlotShape {
 
 /* ---- analytic obstacles (core/sdf/casadi.py) ---------------------------------------------- */
 enum NlotObstacleType {
-    NLOT_OBS_CIRCLE = 0,  /* CircleObstacle.approximated_sdf casadi.py:33-41 */
-    NLOT_OBS_SQUARE = 1   /* SquareObstacle.approximated_sdf casadi.py:69-118 */
+    NLOT_OBS_CIRCLE = 0,    /* CircleObstacle.approximated_sdf casadi.py:33-41 */
+    NLOT_OBS_SQUARE = 1,    /* SquareObstacle.approximated_sdf casadi.py:69-118 */
+    NLOT_OBS_POLYGON = 2,   /* PolygonObstacle.approximated_sdf casadi.py:150-186 (EllipticRingObstacle
+                               casadi.py:193-248 is a polygon of its arc points); (cx, cy) = centroid */
+    NLOT_OBS_TRAPEZOID = 3  /* TrapezoidObstacle.approximated_sdf casadi.py:317-374 (4 vertices) */
 };
 
 enum NlotSdfKind {
@@ -76,14 +79,18 @@ enum NlotSdfKind {
     NLOT_SDF_MLP = 1       /* NNObstacle.approximated_sdf l4casadi.py:241-257 (learned)         */
 };
 
-#define NLOT_MAX_OBS 16
+#define NLOT_MAX_OBS 128   /* primitive obstacles (a discr_s of 30 arc points is 58 trapezoids) */
+#define NLOT_MAX_VERTS 512 /* polygon / trapezoid vertices of all obstacles */
 #define NLOT_MAX_BODY 8
 #define NLOT_MAX_NU 4
 
 typedef struct NlotObstacle {
     int32_t type;      /* NlotObstacleType */
-    int32_t pad_;
-    double cx, cy;     /* center */
+    int32_t group;     /* -1: a term of the scene's soft_min; g >= 0: consecutive obstacles of group g are first
+                          soft_min'ed together (a MultiObstacle inside the scene: ConvexEllipticRing casadi.py:393-445,
+                          ConvexSObstacle casadi.py:448-525), and that value is the scene's term */
+    int32_t v0, nv;    /* polygon / trapezoid: vertices verts[v0 .. v0 + nv) in the reference's point order */
+    double cx, cy;     /* circle / square: center; polygon: centroid (mean of the points, casadi.py:133) */
     double size;       /* circle: radius; square: side length */
     double margin;
 } NlotObstacle;
@@ -108,8 +115,9 @@ typedef struct NlotProblem {
     double softmin_alpha;    /* utils.py:18 alpha = 10 */
     double path_eps;         /* runner.py:81 epsilon = 1e-8 */
     int32_t n_obs;
-    int32_t pad_;
+    int32_t n_verts;
     NlotObstacle obs[NLOT_MAX_OBS];
+    double verts[NLOT_MAX_VERTS][2];
 } NlotProblem;
 
 /* IPOPT options (runner.py:113-125 + IPOPT defaults).  See DESIGN.md §4 for the restatement. */

@@ -14,15 +14,15 @@ STATE_DIM = {"point_1st": 4, "point_2nd": 4, "unicycle": 3, "unicycle_2nd": 5, "
              "ackermann_2nd": 7}
 CONTROL_DIM = {k: 2 for k in DYNAMICS}
 SHAPE_DOT, SHAPE_POLYGON = 0, 1
-OBS_CIRCLE, OBS_SQUARE = 0, 1
+OBS_CIRCLE, OBS_SQUARE, OBS_POLYGON, OBS_TRAPEZOID = 0, 1, 2, 3
 SDF_ANALYTIC, SDF_MLP = 0, 1
 MLP_IN_LINEAR_RELU, MLP_IN_FOURIER = 0, 1
-MAX_OBS, MAX_BODY, MAX_NU = 16, 8, 4
+MAX_OBS, MAX_VERTS, MAX_BODY, MAX_NU = 128, 512, 8, 4
 
 
 class NlotObstacle(C.Structure):
-    _fields_ = [("type", C.c_int32), ("pad_", C.c_int32), ("cx", C.c_double), ("cy", C.c_double),
-                ("size", C.c_double), ("margin", C.c_double)]
+    _fields_ = [("type", C.c_int32), ("group", C.c_int32), ("v0", C.c_int32), ("nv", C.c_int32),
+                ("cx", C.c_double), ("cy", C.c_double), ("size", C.c_double), ("margin", C.c_double)]
 
 
 class NlotProblem(C.Structure):
@@ -33,7 +33,8 @@ class NlotProblem(C.Structure):
         ("use_smooth", C.c_int32), ("slack_penalty", C.c_double), ("smooth_weight", C.c_double),
         ("enforce_heading", C.c_int32), ("sdf_kind", C.c_int32), ("umin", C.c_double * MAX_NU),
         ("umax", C.c_double * MAX_NU), ("softmin_alpha", C.c_double), ("path_eps", C.c_double),
-        ("n_obs", C.c_int32), ("pad_", C.c_int32), ("obs", NlotObstacle * MAX_OBS),
+        ("n_obs", C.c_int32), ("n_verts", C.c_int32), ("obs", NlotObstacle * MAX_OBS),
+        ("verts", (C.c_double * 2) * MAX_VERTS),
     ]
 
 

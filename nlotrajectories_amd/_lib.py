@@ -70,7 +70,7 @@ def lib():
     L.nlot_last_stats.argtypes = [C.POINTER(_abi.NlotSolveStats)]
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 5:
+    if L.nlot_abi_version() != 6:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

@@ -195,17 +195,80 @@ __device__ __forceinline__ HD sdf_square(double cx, double cy, double size, doub
     HD inside = smin(smax(d_x, d_y), z);
     return outside + inside;
 }
-// MultiObstacle.approximated_sdf (casadi.py:385-386): soft_min over obstacles, utils.py:18-33
+__device__ __forceinline__ HD hd_tanh(HD a) { double t = tanh(a.v), d = 1 - t * t; return hd_chain(a, t, d, -2 * t * d); }
+__device__ __forceinline__ HD hd_divc(HD a, double c) { return {a.v / c, a.gx / c, a.gy / c, a.hxx / c, a.hxy / c, a.hyy / c}; }
+// PolygonObstacle.approximated_sdf (casadi.py:150-186; EllipticRingObstacle is a polygon of its arc points):
+// soft_min of the edge-segment distances (hard clamp of the projection), signed by tanh(100 (x - cx)(y - cy))
+__device__ __forceinline__ HD sdf_polygon(const NlotProblem& p, const NlotObstacle& o, double x, double y) {
+    const double(*V)[2] = p.verts + o.v0;
+    const double a = p.softmin_alpha;
+    HD X = hd_var_x(x), Y = hd_var_y(y), sum = hd_const(0.0);
+    for (int e = 0; e < o.nv; ++e) {
+        const int e1 = e + 1 < o.nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], dx = V[e1][0] - x0, dy = V[e1][1] - y0;
+        const double seg = dx * dx + dy * dy + 1e-6;
+        HD traw = hd_divc(dx * (X + (-x0)) + dy * (Y + (-y0)), seg);
+        HD t = traw.v < 0.0 ? hd_const(0.0) : traw.v > 1.0 ? hd_const(1.0) : traw;
+        HD qx = X - (dx * t + x0), qy = Y - (dy * t + y0);
+        sum = sum + hd_exp((-a) * hd_sqrt(qx * qx + qy * qy));
+    }
+    HD md = (-1.0 / a) * hd_log(sum);
+    HD sign = hd_tanh(100.0 * ((X + (-o.cx)) * (Y + (-o.cy))));
+    return sign * md + (-o.margin);
+}
+// TrapezoidObstacle.approximated_sdf (casadi.py:317-374), soft helpers with soft_abs eps 1e-8 (casadi.py:288-312)
+__device__ __forceinline__ HD sdf_trapezoid(const NlotProblem& p, const NlotObstacle& o, double x, double y) {
+    const double(*V)[2] = p.verts + o.v0;
+    auto smax = [](HD a, HD b) { HD d = a - b; return 0.5 * (a + b + hd_sqrt(d * d + 1e-8)); };
+    auto smin = [](HD a, HD b) { HD d = a - b; return 0.5 * (a + b - hd_sqrt(d * d + 1e-8)); };
+    HD X = hd_var_x(x), Y = hd_var_y(y), zero = hd_const(0.0), one = hd_const(1.0), inner_max = zero, outside = zero;
+    for (int e = 0; e < o.nv; ++e) {
+        const int e1 = e + 1 < o.nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], ex = V[e1][0] - x0, ey = V[e1][1] - y0;
+        const double nl = sqrt(ey * ey + ex * ex + 1e-6), nx = ey / nl, ny = -ex / nl;
+        HD d = nx * (X + (-x0)) + ny * (Y + (-y0)) + (-o.margin);
+        inner_max = e == 0 ? d : smax(inner_max, d);
+    }
+    HD inside = smin(inner_max, zero);
+    for (int e = 0; e < o.nv; ++e) {
+        const int e1 = e + 1 < o.nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], ex = V[e1][0] - x0, ey = V[e1][1] - y0;
+        const double seg = ex * ex + ey * ey + 1e-6;
+        HD t = smin(one, smax(zero, hd_divc(ex * (X + (-x0)) + ey * (Y + (-y0)), seg)));
+        HD qx = X - (ex * t + x0), qy = Y - (ey * t + y0);
+        HD dist = hd_sqrt(qx * qx + qy * qy + 1e-6);
+        outside = e == 0 ? dist : smin(outside, dist);
+    }
+    return outside + inside + (-o.margin);
+}
+__device__ __forceinline__ HD sdf_prim(const NlotProblem& p, const NlotObstacle& o, double x, double y) {
+    switch (o.type) {
+        case NLOT_OBS_CIRCLE: return sdf_circle(o.cx, o.cy, o.size, o.margin, x, y);
+        case NLOT_OBS_SQUARE: return sdf_square(o.cx, o.cy, o.size, o.margin, x, y);
+        case NLOT_OBS_POLYGON: return sdf_polygon(p, o, x, y);
+        default: return sdf_trapezoid(p, o, x, y);
+    }
+}
+// MultiObstacle.approximated_sdf (casadi.py:385-386): soft_min over obstacles, utils.py:18-33; a group (a
+// MultiObstacle inside the scene: ConvexEllipticRing, ConvexSObstacle) is soft_min'ed first, one term
 __device__ __forceinline__ HD sdf_scene(const NlotProblem& p, double x, double y, bool derivs) {
+    const double a = p.softmin_alpha;
     HD sum = hd_const(0.0);
-    for (int i = 0; i < p.n_obs; ++i) {
-        const NlotObstacle& o = p.obs[i];
-        HD v = o.type == NLOT_OBS_CIRCLE ? sdf_circle(o.cx, o.cy, o.size, o.margin, x, y)
-                                         : sdf_square(o.cx, o.cy, o.size, o.margin, x, y);
-        sum = sum + hd_exp((-p.softmin_alpha) * v);
+    for (int i = 0; i < p.n_obs;) {
+        HD v;
+        const int g = p.obs[i].group;
+        if (g < 0) {
+            v = sdf_prim(p, p.obs[i], x, y);
+            ++i;
+        } else {
+            HD in = hd_const(0.0);
+            for (; i < p.n_obs && p.obs[i].group == g; ++i) in = in + hd_exp((-a) * sdf_prim(p, p.obs[i], x, y));
+            v = (-1.0 / a) * hd_log(in);
+        }
+        sum = sum + hd_exp((-a) * v);
     }
     (void)derivs;
-    return (-1.0 / p.softmin_alpha) * hd_log(sum);
+    return (-1.0 / a) * hd_log(sum);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -184,9 +184,9 @@ static size_t ws_doubles(const Dims& d, int64_t B) {
     return n;
 }
 
-constexpr size_t kHdr = 8192;  // device copies of NlotProblem, Dims, Ws (kernels read them through pointers:
+constexpr size_t kHdr = 32768;  // device copies of NlotProblem, Dims, Ws (kernels read them through pointers:
                                 // a by-value struct argument indexed at run time is copied to scratch)
-constexpr size_t kHdrProblem = 0, kHdrDims = 2048, kHdrWs = 4096;
+constexpr size_t kHdrProblem = 0, kHdrDims = 24576, kHdrWs = 28672;  // NlotProblem ~14.5 KB (vertex pool)
 
 static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
     size_t b = kHdr + align256(ws_doubles(d, B) * sizeof(double));
@@ -2801,7 +2801,20 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
     if (p->shape == NLOT_SHAPE_POLYGON && p->nx < 3) { set_error("polygon footprint needs a heading state"); return NLOT_ERR_INVALID; }
     if (p->sdf_kind == NLOT_SDF_MLP && !mlp) { set_error("learned SDF requires an NlotMlp"); return NLOT_ERR_INVALID; }
     if (p->sdf_kind == NLOT_SDF_ANALYTIC && (p->n_obs < 1 || p->n_obs > NLOT_MAX_OBS)) {
-        set_error("analytic SDF needs 1..16 obstacles"); return NLOT_ERR_INVALID;
+        set_error("analytic SDF needs 1..NLOT_MAX_OBS (128) obstacles"); return NLOT_ERR_INVALID;
+    }
+    if (p->sdf_kind == NLOT_SDF_ANALYTIC) {
+        if (p->n_verts < 0 || p->n_verts > NLOT_MAX_VERTS) { set_error("n_verts out of range"); return NLOT_ERR_INVALID; }
+        for (int i = 0; i < p->n_obs; ++i) {
+            const NlotObstacle& q = p->obs[i];
+            if (q.type < NLOT_OBS_CIRCLE || q.type > NLOT_OBS_TRAPEZOID) { set_error("unknown obstacle type"); return NLOT_ERR_INVALID; }
+            const bool poly = q.type == NLOT_OBS_POLYGON || q.type == NLOT_OBS_TRAPEZOID;
+            if (poly && (q.nv < (q.type == NLOT_OBS_TRAPEZOID ? 4 : 2) || (q.type == NLOT_OBS_TRAPEZOID && q.nv != 4) ||
+                         q.v0 < 0 || q.v0 + q.nv > p->n_verts)) {
+                set_error("polygon / trapezoid obstacle: vertex range outside verts[0, n_verts) (a trapezoid has 4)");
+                return NLOT_ERR_INVALID;
+            }
+        }
     }
     for (int i = 0; i < p->nu; ++i)
         if (!(p->umin[i] < p->umax[i])) { set_error("control bounds must satisfy min < max"); return NLOT_ERR_INVALID; }

@@ -15,9 +15,10 @@ import math
 from dataclasses import dataclass, field, replace
 from typing import List, Optional, Sequence, Tuple
 
-from . import _abi
+from . import _abi, obstacles as _obstacles
 
-Obstacle = dict  # {"type": "circle"|"square", "center": (x, y), "radius"|"size": r, "margin": m}
+Obstacle = dict  # the reference's YAML vocabulary (core/config.py:53-142): circle, square, polygon, trapezoid,
+#                  elliptical_ring, discr_s (+ convex_elliptic_ring); expanded by obstacles.expand
 
 
 def rectangle_body(length: float, width: float):
@@ -83,8 +84,7 @@ class Problem:
         if self.sdf == "analytic" and not self.obstacles:
             raise ValueError("analytic SDF needs at least one obstacle")
         obstacles = self.obstacles if self.sdf == "analytic" else []  # the learned SDF replaces the scene
-        if len(obstacles) > _abi.MAX_OBS:
-            raise ValueError(f"at most {_abi.MAX_OBS} obstacles")
+        prims, verts = _obstacles.expand(obstacles)
         p = _abi.NlotProblem()
         p.dynamics = _abi.DYNAMICS[self.dynamics]
         p.shape = _abi.SHAPE_DOT if self.shape == "dot" else _abi.SHAPE_POLYGON
@@ -106,20 +106,14 @@ class Problem:
             p.umin[i], p.umax[i] = float(lo), float(hi)
         p.softmin_alpha = float(self.softmin_alpha)
         p.path_eps = float(self.path_eps)
-        p.n_obs = len(obstacles)
-        for i, o in enumerate(obstacles):
-            t = o["type"]
-            if t == "circle":
-                p.obs[i].type = _abi.OBS_CIRCLE
-                p.obs[i].size = float(o["radius"])
-            elif t == "square":
-                p.obs[i].type = _abi.OBS_SQUARE
-                p.obs[i].size = float(o["size"])
-            else:
-                raise ValueError(f"obstacle type {t!r} is reached only through the learned SDF "
-                                 "(round-1 analytic kernels: circle, square)")
-            p.obs[i].cx, p.obs[i].cy = map(float, o["center"])
-            p.obs[i].margin = float(o.get("margin", 0.0))
+        p.n_obs = len(prims)
+        for i, o in enumerate(prims):
+            q = p.obs[i]
+            q.type, q.group, q.v0, q.nv = o["type"], o["group"], o["v0"], o["nv"]
+            q.cx, q.cy, q.size, q.margin = o["cx"], o["cy"], o["size"], o["margin"]
+        p.n_verts = len(verts)
+        for i, (x, y) in enumerate(verts):
+            p.verts[i][0], p.verts[i][1] = x, y
         return p
 
 

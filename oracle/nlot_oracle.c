@@ -121,6 +121,7 @@ static jet jsqrt(jet a) {
 static jet jrecip(jet a) { return junary(a, 1.0 / a.v, -1.0 / (a.v * a.v), 2.0 / (a.v * a.v * a.v)); }
 static jet jdiv(jet a, jet b) { return jmul(a, jrecip(b)); }
 static jet jsq(jet a) { return jmul(a, a); }
+
 /* phi(cx(z), cy(z)) given phi's value / gradient / Hessian in (cx, cy) */
 static jet jcompose2(double f, const double g[2], const double H[3] /*xx,xy,yy*/, jet cx, jet cy) {
     jet r = jconst(cx.n, f);
@@ -230,41 +231,132 @@ void oracle_mlp_eval(const NlotMlpDesc* m, const float* pts, long P, float* val,
 }
 
 /* ============================================================================================ */
-/* Analytic SDFs (core/sdf/casadi.py)                                                           */
+/* Analytic SDFs (core/sdf/casadi.py), in 2-D jets over the point (x, y): value, gradient, Hessian       */
 /* ============================================================================================ */
-static jet sdf_circle(const NlotObstacle* o, jet x, jet y) { /* casadi.py:33-41 */
-    jet dx = jaddc(x, -o->cx), dy = jaddc(y, -o->cy);
-    return jaddc(jsqrt(jadd(jsq(dx), jsq(dy))), -(o->size + o->margin));
+typedef struct {
+    double v, gx, gy, hxx, hxy, hyy;
+} j2;
+static j2 k2(double c) { j2 r = {c, 0, 0, 0, 0, 0}; return r; }
+static j2 add2(j2 a, j2 b) { j2 r = {a.v + b.v, a.gx + b.gx, a.gy + b.gy, a.hxx + b.hxx, a.hxy + b.hxy, a.hyy + b.hyy}; return r; }
+static j2 sub2(j2 a, j2 b) { j2 r = {a.v - b.v, a.gx - b.gx, a.gy - b.gy, a.hxx - b.hxx, a.hxy - b.hxy, a.hyy - b.hyy}; return r; }
+static j2 addc2(j2 a, double c) { a.v += c; return a; }
+static j2 sc2(double c, j2 a) { j2 r = {c * a.v, c * a.gx, c * a.gy, c * a.hxx, c * a.hxy, c * a.hyy}; return r; }
+static j2 divc2(j2 a, double c) { j2 r = {a.v / c, a.gx / c, a.gy / c, a.hxx / c, a.hxy / c, a.hyy / c}; return r; }
+static j2 mul2(j2 a, j2 b) {
+    j2 r = {a.v * b.v, a.gx * b.v + a.v * b.gx, a.gy * b.v + a.v * b.gy, a.hxx * b.v + a.v * b.hxx + 2 * a.gx * b.gx,
+            a.hxy * b.v + a.v * b.hxy + a.gx * b.gy + a.gy * b.gx, a.hyy * b.v + a.v * b.hyy + 2 * a.gy * b.gy};
+    return r;
 }
-static jet soft_abs6(jet v) { return jsqrt(jaddc(jsq(v), 1e-6)); }          /* casadi.py:81-85 */
-static jet smax6(jet a, jet b) {                                              /* casadi.py:95-99 */
-    return jscale(jadd(jadd(a, b), jsqrt(jaddc(jsq(jsub(a, b)), 1e-6))), 0.5);
+static j2 chain2(j2 a, double f0, double f1, double f2) {
+    j2 r = {f0, f1 * a.gx, f1 * a.gy, f1 * a.hxx + f2 * a.gx * a.gx, f1 * a.hxy + f2 * a.gx * a.gy,
+            f1 * a.hyy + f2 * a.gy * a.gy};
+    return r;
 }
-static jet smin6(jet a, jet b) {                                              /* casadi.py:101-105 */
-    return jscale(jsub(jadd(a, b), jsqrt(jaddc(jsq(jsub(a, b)), 1e-6))), 0.5);
+static j2 sqrt2(j2 a) { double q = sqrt(a.v); return chain2(a, q, 0.5 / q, -0.25 / (q * a.v)); }
+static j2 exp2_(j2 a) { double e = exp(a.v); return chain2(a, e, e, e); }
+static j2 log2_(j2 a) { return chain2(a, log(a.v), 1.0 / a.v, -1.0 / (a.v * a.v)); }
+static j2 tanh2(j2 a) { double t = tanh(a.v), d = 1 - t * t; return chain2(a, t, d, -2 * t * d); }
+
+static j2 sdf_circle(const NlotObstacle* o, j2 x, j2 y) { /* casadi.py:33-41 */
+    j2 dx = addc2(x, -o->cx), dy = addc2(y, -o->cy);
+    return addc2(sqrt2(add2(mul2(dx, dx), mul2(dy, dy))), -(o->size + o->margin));
 }
-static jet sdf_square(const NlotObstacle* o, jet x, jet y) { /* casadi.py:69-118 */
+/* SquareObstacle soft helpers casadi.py:81-105 (soft_abs eps 1e-6); TrapezoidObstacle's casadi.py:288-312 (1e-8) */
+static j2 sabs2(j2 v, double eps) { return sqrt2(addc2(mul2(v, v), eps)); }
+static j2 smax2(j2 a, j2 b, double eps) { return sc2(0.5, add2(add2(a, b), sabs2(sub2(a, b), eps))); }
+static j2 smin2(j2 a, j2 b, double eps) { return sc2(0.5, sub2(add2(a, b), sabs2(sub2(a, b), eps))); }
+static j2 sdf_square(const NlotObstacle* o, j2 x, j2 y) { /* casadi.py:69-118 */
     double half = o->size / 2 + o->margin;
-    jet dx = soft_abs6(jaddc(x, -o->cx)), dy = soft_abs6(jaddc(y, -o->cy));
-    jet d_x = jaddc(dx, -half), d_y = jaddc(dy, -half);
-    jet zero = jconst(x.n, 0.0);
-    jet dxo = smax6(d_x, zero), dyo = smax6(d_y, zero);
-    jet outside = jsqrt(jadd(jsq(dxo), jsq(dyo)));
-    jet inside = smin6(smax6(d_x, d_y), zero);
-    return jadd(outside, inside);
+    j2 dx = sabs2(addc2(x, -o->cx), 1e-6), dy = sabs2(addc2(y, -o->cy), 1e-6);
+    j2 d_x = addc2(dx, -half), d_y = addc2(dy, -half), zero = k2(0.0);
+    j2 dxo = smax2(d_x, zero, 1e-6), dyo = smax2(d_y, zero, 1e-6);
+    j2 outside = sqrt2(add2(mul2(dxo, dxo), mul2(dyo, dyo)));
+    j2 inside = smin2(smax2(d_x, d_y, 1e-6), zero, 1e-6);
+    return add2(outside, inside);
 }
-/* soft_min, core/utils.py:18-33 (no max-shift, exactly as written) */
+/* soft_min, core/utils.py:18-33 (no max-shift, exactly as written): sum of exp(-alpha v_i) in order, then
+   -1/alpha log */
+static j2 soft_min_fin(j2 sum, double alpha) { return sc2(-1.0 / alpha, log2_(sum)); }
+/* PolygonObstacle.approximated_sdf casadi.py:150-186: soft_min of the distances to the edge segments (hard
+   clamp of the projection parameter), signed by tanh(100 (x - cx)(y - cy)) about the centroid */
+static j2 sdf_polygon(const NlotProblem* p, const NlotObstacle* o, j2 x, j2 y) {
+    const double(*V)[2] = p->verts + o->v0;
+    const double a = p->softmin_alpha;
+    j2 sum = k2(0.0);
+    for (int e = 0; e < o->nv; ++e) {
+        const int e1 = e + 1 < o->nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], dx = V[e1][0] - x0, dy = V[e1][1] - y0;
+        const double seg = dx * dx + dy * dy + 1e-6;
+        j2 traw = divc2(add2(sc2(dx, addc2(x, -x0)), sc2(dy, addc2(y, -y0))), seg);
+        j2 t = traw.v < 0.0 ? k2(0.0) : traw.v > 1.0 ? k2(1.0) : traw;
+        j2 qx = sub2(x, addc2(sc2(dx, t), x0)), qy = sub2(y, addc2(sc2(dy, t), y0));
+        sum = add2(sum, exp2_(sc2(-a, sqrt2(add2(mul2(qx, qx), mul2(qy, qy))))));
+    }
+    j2 md = soft_min_fin(sum, a);
+    j2 sign = tanh2(sc2(100.0, mul2(addc2(x, -o->cx), addc2(y, -o->cy))));
+    return addc2(mul2(sign, md), -o->margin);
+}
+/* TrapezoidObstacle.approximated_sdf casadi.py:317-374 */
+static j2 sdf_trapezoid(const NlotProblem* p, const NlotObstacle* o, j2 x, j2 y) {
+    const double(*V)[2] = p->verts + o->v0;
+    const int nv = o->nv;
+    j2 zero = k2(0.0), one = k2(1.0), inner_max = zero, outside = zero;
+    for (int e = 0; e < nv; ++e) { /* half-plane distances, soft max folded left to right */
+        const int e1 = e + 1 < nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], ex = V[e1][0] - x0, ey = V[e1][1] - y0;
+        const double nl = sqrt(ey * ey + ex * ex + 1e-6), nx = ey / nl, ny = -ex / nl;
+        j2 d = addc2(add2(sc2(nx, addc2(x, -x0)), sc2(ny, addc2(y, -y0))), -o->margin);
+        inner_max = e == 0 ? d : smax2(inner_max, d, 1e-8);
+    }
+    j2 inside = smin2(inner_max, zero, 1e-8);
+    for (int e = 0; e < nv; ++e) { /* distances to the segments, smooth clamp, soft min folded */
+        const int e1 = e + 1 < nv ? e + 1 : 0;
+        const double x0 = V[e][0], y0 = V[e][1], ex = V[e1][0] - x0, ey = V[e1][1] - y0;
+        const double seg = ex * ex + ey * ey + 1e-6;
+        j2 t = smin2(one, smax2(zero, divc2(add2(sc2(ex, addc2(x, -x0)), sc2(ey, addc2(y, -y0))), seg), 1e-8), 1e-8);
+        j2 qx = sub2(x, addc2(sc2(ex, t), x0)), qy = sub2(y, addc2(sc2(ey, t), y0));
+        j2 dist = sqrt2(addc2(add2(mul2(qx, qx), mul2(qy, qy)), 1e-6));
+        outside = e == 0 ? dist : smin2(outside, dist, 1e-8);
+    }
+    return addc2(add2(outside, inside), -o->margin);
+}
+static j2 sdf_prim(const NlotProblem* p, const NlotObstacle* o, j2 x, j2 y) {
+    switch (o->type) {
+    case NLOT_OBS_CIRCLE: return sdf_circle(o, x, y);
+    case NLOT_OBS_SQUARE: return sdf_square(o, x, y);
+    case NLOT_OBS_POLYGON: return sdf_polygon(p, o, x, y);
+    default: return sdf_trapezoid(p, o, x, y);
+    }
+}
+/* MultiObstacle.approximated_sdf casadi.py:385-386 — soft_min even for one obstacle; a group (a MultiObstacle
+   in the scene: ConvexEllipticRing / ConvexSObstacle) is soft_min'ed first and enters as one term.  Evaluated
+   in (x, y) and composed with the corner's jet (as the GPU's 2-D hyper-duals). */
+static jet sdf_analytic(const NlotProblem* p, jet cx, jet cy) {
+    const double a = p->softmin_alpha;
+    j2 x = {cx.v, 1, 0, 0, 0, 0}, y = {cy.v, 0, 1, 0, 0, 0}, sum = k2(0.0);
+    for (int i = 0; i < p->n_obs;) {
+        j2 v;
+        if (p->obs[i].group < 0) {
+            v = sdf_prim(p, &p->obs[i], x, y);
+            ++i;
+        } else {
+            const int g = p->obs[i].group;
+            j2 in = k2(0.0);
+            for (; i < p->n_obs && p->obs[i].group == g; ++i) in = add2(in, exp2_(sc2(-a, sdf_prim(p, &p->obs[i], x, y))));
+            v = soft_min_fin(in, a);
+        }
+        sum = add2(sum, exp2_(sc2(-a, v)));
+    }
+    j2 s = soft_min_fin(sum, a);
+    double g[2] = {s.gx, s.gy}, H[3] = {s.hxx, s.hxy, s.hyy};
+    return jcompose2(s.v, g, H, cx, cy);
+}
+
+/* soft_min, core/utils.py:18-33, over jets of any dimension (the footprint's corner soft_min) */
 static jet soft_min_j(const jet* a, int n, double alpha) {
     jet s = jconst(a[0].n, 0.0);
     for (int i = 0; i < n; ++i) s = jadd(s, jexp(jscale(a[i], -alpha)));
     return jscale(jlog(s), -1.0 / alpha);
-}
-/* MultiObstacle.approximated_sdf casadi.py:385-386 — soft_min even for one obstacle */
-static jet sdf_analytic(const NlotProblem* p, jet x, jet y) {
-    jet v[NLOT_MAX_OBS];
-    for (int i = 0; i < p->n_obs; ++i)
-        v[i] = p->obs[i].type == NLOT_OBS_CIRCLE ? sdf_circle(&p->obs[i], x, y) : sdf_square(&p->obs[i], x, y);
-    return soft_min_j(v, p->n_obs, p->softmin_alpha);
 }
 
 /* SDF of the scene at world point (cx, cy) given as jets (any dimension). */

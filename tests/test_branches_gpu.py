@@ -44,8 +44,32 @@ def _cases():
                                     control_bounds=((-1, 1), (-2, 2)), obstacles=[_circle((0.5, 0.45), 0.12, 0.01)]),
                              [0, 0.4, 0, 0, 0, 0, 0], [1, 0.4, 0, 0, 0, 0, 0]),
         "unicycle2nd_N256": (b2["problem"].with_(N=256, dt=0.02), b2["start"], b2["goal"]),
+        # the remaining analytic obstacle types (casadi.py:127-525): benchmark_4's polygon and benchmark_6's
+        # elliptical rings (polygons of 30 arc points) from the reference's own YAML dumps, and a discr_s (a
+        # group of 18 trapezoids soft_min'ed inside the scene's soft_min) next to a trapezoid
+        **{name: _yaml_case(fn) for name, fn in (("b4_polygon", "benchmark_4_dot_nonconvex.yaml"),
+                                                  ("b6_elliptical_rings", "benchmark_6_ackermann_wave.yaml"))},
+        "discr_s_trapezoid": (Problem(dynamics="unicycle_2nd", length=0.1, width=0.05, N=50, slack_penalty=10,
+                                      control_bounds=((-1, 1), (-1, 1)), obstacles=[
+                                          {"type": "discr_s", "center": (0.3, 0.5), "semi_axes": (0.25, 0.2),
+                                           "width": 0.05, "angle": 3.14, "num_arc_points": 10, "margin": 0.01},
+                                          {"type": "trapezoid", "points": [(0.6, 0.05), (0.9, 0.05), (0.85, 0.25),
+                                                                           (0.65, 0.25)], "margin": 0.01}]),
+                              [0.0, 0.0, 0.6, 0.0, 0.0], [1.1, 0.9, 0.6, 0.0, 0.0]),
     }
     return c
+
+
+def _yaml_case(fn):
+    """A benchmark YAML (the reference's Config dump in tests/golden/nlp_golden.json) in casadi mode."""
+    import json
+    import os
+
+    from nlotrajectories_amd.config import Config
+
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nlp_golden.json")))
+    cfg = Config.model_validate(gold["configs"][fn])
+    return cfg.to_problem().with_(sdf="analytic"), list(cfg.body.start_state), list(cfg.body.goal_state)
 
 
 CASES = list(_cases().keys())
@@ -76,7 +100,7 @@ def test_iterates_match_oracle(name):
 
 
 @pytest.mark.parametrize("name", ["b1_dot_point2nd", "b5_ackermann2nd_squares", "b2_no_slack", "b2_smooth",
-                                  "b2_enforce_heading", "b6_settings_N100"])
+                                  "b2_enforce_heading", "b6_settings_N100", "b4_polygon", "discr_s_trapezoid"])
 def test_full_solves_match_oracle(name):
     import oracle as O
     from nlotrajectories_amd.solver import solve_batch

@@ -48,12 +48,13 @@ def test_soft_min():
 
 
 SCENES = ["benchmark_1_dot_circle.yaml", "benchmark_2_unicycle_circle.yaml", "benchmark_3_unicycle_convex.yaml",
-          "benchmark_5_ackermann_circle.yaml"]
+          "benchmark_4_dot_nonconvex.yaml", "benchmark_5_ackermann_circle.yaml", "benchmark_6_ackermann_wave.yaml"]
 
 
 @pytest.mark.parametrize("fn", SCENES)
 def test_scene_sdf_circle_square(fn):
-    """MultiObstacle.approximated_sdf of the circle/square scenes through the YAML -> Problem mapping."""
+    """MultiObstacle.approximated_sdf of the six benchmark scenes (circles, squares, benchmark_4's polygon,
+    benchmark_6's elliptical rings) through the YAML -> Problem mapping."""
     import oracle as O
     from nlotrajectories_amd.config import Config
 
@@ -77,3 +78,56 @@ def test_configs_parse_like_reference():
             assert ours["solver"][k] == ref["solver"][k], (fn, k)
         assert ours["model"] == ref["model"], fn
         assert ours["obstacles"] == ref["obstacles"], fn
+
+
+# the single obstacles of make_nlp_golden.py (casadi.py constructors with those arguments), as scene dicts
+SINGLE = {
+    "circle": {"type": "circle", "center": (0.5, 0.5), "radius": 0.2, "margin": 0.05},
+    "square": {"type": "square", "center": (0.8, 0.2), "size": 0.35, "margin": 0.01},
+    "polygon": {"type": "polygon", "points": [(0.1, 0.1), (0.6, 0.15), (0.7, 0.6), (0.2, 0.5)], "margin": 0.02},
+    "elliptical_ring": {"type": "elliptical_ring", "center": (0.25, 0.2), "semi_axes": (0.25, 0.2), "width": 0.05,
+                        "angle": 3.14, "margin": 0.01},
+    "elliptical_ring_neg": {"type": "elliptical_ring", "center": (0.7, 0.2), "semi_axes": (0.25, 0.2), "width": 0.05,
+                            "angle": -3.14, "margin": 0.01},
+    "trapezoid": {"type": "trapezoid", "points": [(0.2, 0.2), (0.8, 0.2), (0.6, 0.6), (0.4, 0.6)], "margin": 0.01},
+    "convex_elliptic_ring": {"type": "convex_elliptic_ring", "center": (0.5, 0.4), "semi_axes": (0.3, 0.25),
+                             "width": 0.06, "angle": 3.0, "num_arc_points": 8, "margin": 0.01, "rotation": 0.3},
+    "discr_s": {"type": "discr_s", "center": (0.3, 0.5), "semi_axes": (0.25, 0.2), "width": 0.05, "angle": 3.14,
+                "num_arc_points": 10, "margin": 0.01},
+}
+
+
+@pytest.mark.parametrize("name", list(SINGLE))
+def test_single_obstacle_sdf(name):
+    """approximated_sdf of each analytic obstacle type (the golden vectors record the obstacle alone; the
+    scene wraps it in a one-term soft_min, which is the identity: -1/a log(exp(-a v)) = v to rounding)."""
+    import oracle as O
+    from nlotrajectories_amd.problem import Problem
+
+    prob = Problem(shape="dot", dynamics="point_2nd", obstacles=[SINGLE[name]])
+    pts = np.asarray(GOLD["sdf"]["points"])
+    v = O.sdf_eval(prob, pts)[:, 0]
+    np.testing.assert_allclose(v, GOLD["sdf"][name], rtol=0, atol=1e-12, err_msg=name)
+
+
+@pytest.mark.parametrize("name", ["polygon", "trapezoid", "discr_s", "elliptical_ring"])
+def test_analytic_sdf_derivatives_match_finite_differences(name):
+    """The oracle's gradient / Hessian of the scene SDF (what the solver uses) against central differences."""
+    import oracle as O
+    from nlotrajectories_amd.problem import Problem
+
+    prob = Problem(shape="dot", dynamics="point_2nd", obstacles=[SINGLE[name]])
+    rng = np.random.default_rng(5)
+    P = rng.uniform(-0.3, 1.3, size=(40, 2))
+    h = 1e-6
+    out = O.sdf_eval(prob, P)
+    for a in range(2):
+        e = np.zeros(2)
+        e[a] = h
+        fp, fm = O.sdf_eval(prob, P + e), O.sdf_eval(prob, P - e)
+        g_fd = (fp[:, 0] - fm[:, 0]) / (2 * h)
+        np.testing.assert_allclose(out[:, 1 + a], g_fd, rtol=1e-5, atol=1e-6, err_msg=(name, a))
+        # Hessian row a from differences of the gradient (xx, xy, yy at columns 3, 4, 5)
+        H_fd = (fp[:, 1:3] - fm[:, 1:3]) / (2 * h)
+        cols = (3, 4) if a == 0 else (4, 5)
+        np.testing.assert_allclose(out[:, cols], H_fd, rtol=1e-4, atol=1e-4, err_msg=(name, a))
