@@ -53,7 +53,7 @@ enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4 };
 #define NLOT_WPE_ACC 3
 #endif
 #ifndef NLOT_WPE_RIC
-#define NLOT_WPE_RIC 1
+#define NLOT_WPE_RIC 2  // k_ric at 2 waves/SIMD: 12 % less k_ric time at the metric config than 1 (r02i A/B)
 #endif
 #ifndef NLOT_RIC_RING
 #define NLOT_RIC_RING 2
@@ -736,8 +736,13 @@ __device__ __forceinline__ void ric_sync_reads() {
 // Newton (or least-squares) solve of the instances whose stage matrices k_iter_a built (SC_RIC = 1),
 // with IPOPT's inertia correction: on a wrong inertia the group rebuilds its stages with the next
 // delta_w and factorises again.  Outputs: dX dU dS yi_n yk_n yt_n (and the second right-hand side).
+// waves per SIMD of k_ric: NLOT_WPE_RIC, except ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
 template <int DYN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RIC))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+struct RicWpe {
+    static constexpr int value = DYN == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
+};
+template <int DYN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
                                             int mode) {
     using R = RicG<DYN>;

@@ -16,8 +16,10 @@ b = BENCHMARKS["b2"]
 x0, xg, kw = b["start"], b["goal"], {}
 if tag == "tiny":
     x0, xg, kw = [0.0, 0.05, 0.0, 0.0, 0.0], [1.0, 0.1, 0.0, 0.0, 0.0], dict(tiny_step_tol=0.1, tiny_step_y_tol=1e3)
+elif tag == "tiny2":
+    x0, xg, kw = [0.0, 0.8, 0.0, 0.0, 0.0], [1.0, 0.9, 0.0, 0.0, 0.0], dict(tiny_step_tol=0.05, tiny_step_y_tol=1e3)
 out = {}
-for k in range(0, 23):
+for k in range(0, 14):
     r = solve_batch(b["problem"], np.array([x0]), np.array([xg]), options=_abi.gpu_options(max_iter=k, **kw))
     out[f"X{k}"] = r["X"][0].cpu().numpy(); out[f"U{k}"] = r["U"][0].cpu().numpy(); out[f"S{k}"] = r["S"][0].cpu().numpy()
     out[f"st{k}"] = r["status"][0].item(); out[f"it{k}"] = r["iters"][0].item()
