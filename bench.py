@@ -171,7 +171,7 @@ def main():
     ric_bytes = ric_bytes_per_solve(prob)
     ric_achieved = ric_solves_per_launch * ric_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     ric_traffic = None
-    tf = os.path.join(ROOT, "profiles", "r02", "kric_traffic.json")
+    tf = os.path.join(ROOT, "profiles", "r02", "kric_traffic.json")  # PMC, scripts/pmc_r02.sh
     if os.path.exists(tf):
         with open(tf) as f:
             per_solve = json.load(f).get("hbm_bytes_per_solve")
