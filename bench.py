@@ -187,12 +187,11 @@ def main():
     flop_launch = (agg["mlp_points_full"] * flop_pt - reused * flop_fwd) / n_l
     achieved = flop_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "mlp_full_traffic.json")
+    tf = os.path.join(ROOT, "profiles", "r02", "mlp_traffic_in_solve.json")  # PMC inside the solve, pmc_r02.sh
     if os.path.exists(tf):
         with open(tf) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch_per_point")
-            if traffic is not None:
-                traffic = traffic * agg["mlp_points_full"] / n_l
+            t = json.load(f)
+        traffic = (t["full_fetch_bytes_per_point_corrected"] + t["full_write_bytes_per_point"]) * agg["mlp_points_full"] / n_l
     n_v = max(agg["mlp_value_launches"], 1)
     v_avg_ms = agg["mlp_value_ms"] / n_v
     v_achieved = agg["mlp_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
