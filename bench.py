@@ -32,7 +32,7 @@ from nlotrajectories_amd import _abi  # noqa: E402
 from nlotrajectories_amd.dist import gather_solutions, max_over_ranks, rank_world, sum_over_ranks  # noqa: E402
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
-from nlotrajectories_amd.problem import METRIC_PROBLEM, STRESS_PROBLEM  # noqa: E402
+from nlotrajectories_amd.problem import B6_PROBLEM, BENCHMARKS, METRIC_PROBLEM, STRESS_PROBLEM  # noqa: E402
 from nlotrajectories_amd.sampling import sample_start_goal  # noqa: E402
 from nlotrajectories_amd.solver import last_stats, set_timing, solve_batch  # noqa: E402
 
@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["metric", "stress"], default="metric",
-                    help="metric = BASELINE.json's headline config; stress = configs[4] (2-256x4-1 SDF MLP, N = 256)")
+    ap.add_argument("--workload", choices=["metric", "stress", "b6"], default="metric",
+                    help="metric = BASELINE.json's headline config; stress = configs[4] (2-256x4-1 SDF MLP, N = 256); "
+                         "b6 = configs[3] (benchmark 6 Ackermann + ring corridor, N = 100, trained SDF)")
     ap.add_argument("--batch", type=int, default=None,
                     help="instances per GPU per step (metric default 65536, SURVEY.md §8d config 3; stress default "
                          "8192 = 65536 over 8 GPUs)")
@@ -104,15 +105,19 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    stress = a.workload == "stress"
+    stress, b6 = a.workload == "stress", a.workload == "b6"
     if a.batch is None:
-        a.batch = 8192 if stress else 65536
+        a.batch = 8192 if stress else 16384 if b6 else 65536
     if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
-        a.cpu_sample = 16 if stress else 256
+        a.cpu_sample = 16 if stress else 32 if b6 else 256
     if a.cpu_sample_1core is None:
-        a.cpu_sample_1core = 1 if stress else 8
-    prob = STRESS_PROBLEM if stress else METRIC_PROBLEM
-    w = MlpWeights.stress_sdf_mlp(seed=0) if stress else MlpWeights.artefact()
+        a.cpu_sample_1core = 1 if stress else 2 if b6 else 8
+    prob = STRESS_PROBLEM if stress else B6_PROBLEM if b6 else METRIC_PROBLEM
+    if b6:
+        wpath = os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")
+        w = MlpWeights.load(wpath)  # trained by scripts/train_sdf.py (NNObstacleTrainer restatement, seed 0)
+    else:
+        w = MlpWeights.stress_sdf_mlp(seed=0) if stress else MlpWeights.artefact()
     mlp = DeviceMlp(w)
     streaming = w.hidden == 256 or w.n_hidden > 2  # nlot_mlp.hip launch_mlp_strided dispatch
 
@@ -120,8 +125,14 @@ def main():
         v, _, _ = sdf_mlp_eval(mlp, torch.as_tensor(pts, dtype=torch.float32, device=dev), derivatives=False)
         return v.cpu().numpy()
 
-    # start/goal uniform in [-0.3, 1.3]^2, all corners sdf >= 0.02
-    x0, xg = sample_start_goal(prob, a.batch, seed=a.seed, sdf=sdf_gpu, rank=rank)
+    if b6:  # benchmark 6's start / goal, xy +- U[-0.05, 0.05]^2 (seeded per rank)
+        rng = np.random.default_rng(a.seed + 1000003 * rank)
+        x0 = np.repeat(np.array([BENCHMARKS["b6"]["start"]], float), a.batch, 0)
+        xg = np.repeat(np.array([BENCHMARKS["b6"]["goal"]], float), a.batch, 0)
+        x0[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
+        xg[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
+    else:  # start/goal uniform in [-0.3, 1.3]^2, all corners sdf >= 0.02
+        x0, xg = sample_start_goal(prob, a.batch, seed=a.seed, sdf=sdf_gpu, rank=rank)
     x0 = torch.tensor(x0, dtype=torch.float64, device=dev)
     xg = torch.tensor(xg, dtype=torch.float64, device=dev)
     opt = _abi.gpu_options() if a.mu_strategy == "adaptive" else \
@@ -265,8 +276,9 @@ def main():
         else:
             rooflines = {"roofline": ric, "roofline_mlp_full": mlp_full, "roofline_mlp_value": mlp_value}
         line = {
-            "metric": "solved trajectories/sec (50-knot unicycle+learned-SDF)" if not stress else
-                      "solved trajectories/sec (stress: 256-knot unicycle + 2-256x4-1 SDF MLP)",
+            "metric": "solved trajectories/sec (stress: 256-knot unicycle + 2-256x4-1 SDF MLP)" if stress else
+                      "solved trajectories/sec (b6: 101-knot Ackermann 2nd-order + ring-corridor learned SDF)" if b6
+                      else "solved trajectories/sec (50-knot unicycle+learned-SDF)",
             "value": solved_total / elapsed,
             "unit": "trajectories/s",
             "n_gpus": world,
@@ -280,11 +292,16 @@ def main():
                      "the reference's fp32 libtorch graph)",
             "data": "synthetic start/goal (seeded, SURVEY.md §8d); learned SDF = " +
                     ("seeded kaiming-uniform 2-256x4-1 ReLU net, output bias centred (MlpWeights.stress_sdf_mlp)"
-                     if stress else "reference artefact weights"),
+                     if stress else "2-128-128-1 ReLU net trained on benchmark 6's rings by the NNObstacleTrainer "
+                     "restatement (seed 0, nlotrajectories_amd/data/b6_mlp128_seed0.npz)" if b6
+                     else "reference artefact weights"),
             "config": {
                 "workload": ("stress (BASELINE.json configs[4]): unicycle_2nd, rect 0.2x0.08, N=256, dt 0.1, rho=10, "
                              "bounds +-1, SDF MLP 2-256x4-1 ReLU (3 HxH layers), linear init, IPOPT tol 1e-4")
                             if stress else
+                            ("b6 (BASELINE.json configs[3]): ackermann_2nd L=0.05, rect 0.08x0.05, N=100, dt 0.05, no "
+                             "slack (per-corner sdf >= 0), smooth w=0.5, bounds [+-1, +-2], learned SDF of 4 "
+                             "elliptical half rings, linear init, IPOPT tol 1e-4") if b6 else
                             "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
                 "mu_strategy": a.mu_strategy,

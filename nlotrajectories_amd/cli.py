@@ -7,8 +7,9 @@ metrics, append the results CSV) with nlot_solve_batch in place of CasADi/IPOPT.
 Differences from the reference, all loud:
   * initializer `rrt` (every shipped YAML) is not built yet: pass --initializer linear or
     default (default = CasADi's zero initial guess, run_benchmark.py:113-114 / DefualtInitializer);
-  * solver.mode l4casadi trains a network in the reference (NNObstacleTrainer); here the weights come
-    from --weights (an .npz written by MlpWeights.save, or the shipped artefact with --weights artefact);
+  * solver.mode l4casadi trains a network in the reference (NNObstacleTrainer); here `--weights train` does the
+    same (the seeded restatement in trainer.py, on the GPU), or the weights come from --weights (an .npz written
+    by MlpWeights.save, e.g. data/b6_mlp128_seed0.npz, or the shipped artefact with --weights artefact);
   * solver.type sqpmethod is not provided (the reference's default benchmarks all use ipopt);
   * plots are not produced; the CSV row always carries all 20 header columns (the reference writes 17
     values under a 20-column header).
@@ -71,9 +72,15 @@ def run_benchmark(config_path, initializer="yaml", weights=None, results_dir="re
     mlp = None
     if prob.sdf == "mlp":
         if weights is None:
-            raise ValueError("solver.mode l4casadi: pass --weights <file.npz> or --weights artefact "
-                             "(the reference trains the network at this point, NNObstacleTrainer)")
-        w = MlpWeights.artefact() if weights == "artefact" else MlpWeights.load(weights)
+            raise ValueError("solver.mode l4casadi: pass --weights train (train the config's network, as the "
+                             "reference does), --weights <file.npz> or --weights artefact")
+        if weights == "train":  # run_benchmark.py:84-95
+            from .trainer import train_for_config
+
+            model, _ = train_for_config(cfg, verbose=verbose)
+            w = MlpWeights.from_module(model)
+        else:
+            w = MlpWeights.artefact() if weights == "artefact" else MlpWeights.load(weights)
         mlp = DeviceMlp(w)
     x0 = np.asarray(cfg.body.start_state, float)[None]
     xg = np.asarray(cfg.body.goal_state, float)[None]
@@ -149,7 +156,7 @@ def main(argv=None):
     ap.add_argument("--config", type=str, required=True, help="Path to benchmark YAML config")
     ap.add_argument("--initializer", choices=["yaml", "linear", "default"], default="yaml",
                     help="override the YAML initializer (rrt is not built yet)")
-    ap.add_argument("--weights", type=str, default=None, help="learned-SDF weights (.npz) or 'artefact'")
+    ap.add_argument("--weights", type=str, default=None, help="learned-SDF weights: 'train' (NNObstacleTrainer), an .npz, or 'artefact'")
     ap.add_argument("--results", type=str, default="results")
     a = ap.parse_args(argv)
     run_benchmark(Path(a.config), initializer=a.initializer, weights=a.weights, results_dir=a.results)

@@ -156,6 +156,24 @@ BENCHMARKS = {
                                obstacles=[_circle((0.5, 0.5), 0.2, 0.01), _square((1.2, 0.37), 0.1, 0.01),
                                           _square((1.1, 0.7), 0.2, 0.01), _square((0.2, 0.9), 0.1, 0.01)]),
                start=[0, 0, 0, 0.0, 0.0, 0.0, 0.0], goal=[1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0]),
+    # benchmark_4_dot_nonconvex.yaml (mode l4casadi; the analytic scene is its training target / casadi mode)
+    "b4": dict(problem=Problem(dynamics="unicycle_2nd", shape="rectangle", length=0.1, width=0.1, N=80, dt=0.05,
+                               use_slack=True, slack_penalty=60, use_smooth=False, smooth_weight=0.5,
+                               enforce_heading=False, control_bounds=((-2, 2), (-3, 3)),
+                               obstacles=[{"type": "polygon", "margin": 0.01, "points": [
+                                   (0.5, -0.06), (0.654, 0.336), (1.05, 0.336), (0.7, 0.5), (0.86, 0.86), (0.5, 0.68),
+                                   (0.14, 0.86), (0.3, 0.5), (-0.05, 0.336), (0.346, 0.336)]}]),
+               start=[0.7, 0.2, -0.1, 0.0, 0.0], goal=[0.5, 0.85, 0.785, 0.0, 0.0]),
+    # benchmark_6_ackermann_wave.yaml (mode l4casadi): four elliptical half rings
+    "b6": dict(problem=Problem(dynamics="ackermann_2nd", shape="rectangle", length=0.08, width=0.05, wheelbase=0.05,
+                               N=80, dt=0.05, use_slack=False, slack_penalty=10, use_smooth=True, smooth_weight=0.5,
+                               enforce_heading=False, control_bounds=((-1, 1), (-2, 2)),
+                               obstacles=[{"type": "elliptical_ring", "center": c, "semi_axes": (0.25, 0.2),
+                                           "width": 0.05, "angle": a, "margin": 0.01, "rotation": 0.0,
+                                           "num_arc_points": 15}
+                                          for c, a in (((0.25, 0.2), 3.14), ((0.7, 0.2), -3.14), ((0.25, 0.6), 3.14),
+                                                       ((0.7, 0.6), -3.14))]),
+               start=[0.0, 0.4, 0.785, 0.0, 0.0, 0.0, 0.0], goal=[1.0, 0.4, 0.785, 0.0, 0.0, 0.0, 0.0]),
 }
 
 # The metric configuration (BASELINE.json metric): benchmark_3's body,
@@ -171,3 +189,7 @@ def heading(start_xy, goal_xy) -> float:
 # The stress configuration (BASELINE.json configs[4]): the metric NLP at N = 256 knots (same dt,
 # a 25.6 s horizon) with the 2-256x4-1 ReLU SDF MLP (MlpWeights.random_relu_mlp(256, 3), seeded kaiming).
 STRESS_PROBLEM = METRIC_PROBLEM.with_(N=256)
+
+# BASELINE.json configs[3]: benchmark 6 at the north_star's N = 100 knots with the learned
+# SDF trained on its ring scene (scripts/train_sdf.py -> nlotrajectories_amd/data/b6_mlp128_seed0.npz)
+B6_PROBLEM = BENCHMARKS["b6"]["problem"].with_(N=100, sdf="mlp")
