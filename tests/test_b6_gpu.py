@@ -1,0 +1,68 @@
+"""BASELINE.json configs[3] on the GPU: benchmark 6 (ackermann_2nd, no slack = per-corner constraints, smooth
+w = 0.5) at N = 100 with the learned SDF trained on its ring corridor (data/b6_mlp128_seed0.npz).  Iterates vs
+the oracle (fp32 MLP on both sides: 1e-4, or 20x the oracle's own response to a 1e-13 start perturbation), and
+a seeded batch whose GPU-solved instances satisfy their constraints."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nlotrajectories_amd", "data")
+
+
+def _setup():
+    import oracle as O
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import B6_PROBLEM, BENCHMARKS
+
+    w = MlpWeights.load(os.path.join(DATA, "b6_mlp128_seed0.npz"))
+    return O, B6_PROBLEM, BENCHMARKS["b6"], DeviceMlp(w), O.HostMlp(w)
+
+
+def test_b6_iterates_match_oracle():
+    O, prob, b, mlp, hm = _setup()
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.solver import solve_batch
+
+    x0, xg = np.array(b["start"], float), np.array(b["goal"], float)
+    x0[1] += 0.02  # off the corridor's centre line by a little
+    for k in (1, 3, 8):
+        opt = _abi.gpu_options(max_iter=k)
+        rg = solve_batch(prob, x0[None], xg[None], mlp=mlp, options=opt)
+        rc = O.solve_one(prob, x0, xg, hm, opt=opt)
+        xp = x0.copy()
+        xp[0] += 1e-13
+        rp = O.solve_one(prob, xp, xg, hm, opt=opt)
+        sens = max(float(np.abs(rp[n] - rc[n]).max()) for n in ("X", "U"))
+        d = {n: float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U")}
+        print("b6 k", k, "status", rc["status"], rg["status"][0].item(), d, "oracle sensitivity", sens, flush=True)
+        assert rg["status"][0].item() == rc["status"]
+        for n, v in d.items():
+            assert v <= max(1e-4, 20 * sens), (k, n, v)
+
+
+def test_b6_batch_solutions_are_feasible():
+    O, prob, b, mlp, hm = _setup()
+    from nlotrajectories_amd.solver import solve_batch
+
+    rng = np.random.default_rng(4)
+    B = 64
+    X0 = np.repeat(np.array([b["start"]], float), B, 0)
+    XG = np.repeat(np.array([b["goal"]], float), B, 0)
+    X0[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
+    XG[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
+    r = solve_batch(prob, X0, XG, mlp=mlp)
+    st = r["status"].cpu().numpy()
+    print("b6 batch statuses", np.bincount(st, minlength=7).tolist(), flush=True)
+    X, U = r["X"].cpu().numpy(), r["U"].cpu().numpy()
+    for i in np.where(st == 0)[0]:
+        assert np.abs(X[i, 0] - X0[i]).max() < 1e-4
+        assert np.abs(X[i, -1, [0, 1, 3, 4, 5, 6]] - XG[i, [0, 1, 3, 4, 5, 6]]).max() < 1e-4
+        F = X[i, :-1] + prob.dt * np.stack([O.dynamics(prob, X[i, k], U[i, k]) for k in range(prob.N)])
+        assert np.abs(X[i, 1:] - F).max() < 1e-4
+        # per-corner learned SDF >= 0 (no slack), to the constraint tolerance
+        c = np.concatenate([O.corners(prob, X[i, k]) for k in range(prob.N + 1)])
+        v, _, _ = O.mlp_eval(hm, c, want=False)
+        assert v.min() > -1e-4
