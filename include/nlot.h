@@ -246,6 +246,32 @@ void nlot_last_stats(NlotSolveStats* out);
 typedef double casadi_real_t;
 typedef long long int casadi_int_t;
 int32_t nlot_casadi_bind(const NlotMlp* mlp);
+
+/* ---- RRT initializer (core/trajectory_initialization.py:58-239, RRTInitializer) ----------------- */
+typedef struct NlotRrtOptions {
+    double bounds[2][2];       /* [[xmin, ymin], [xmax, ymax]] sampling box (YAML rrt_bounds) */
+    double step_size;          /* extension step (0.05) */
+    double margin;             /* safety distance added to the footprint inflation (0.01) */
+    double goal_sample_rate;   /* probability of sampling the goal (0.05) */
+    uint64_t seed;             /* counter-based RNG seed (the reference draws from Python's global `random`) */
+    int32_t max_iter;          /* tree extensions tried (1000) */
+    int32_t pad_;
+} NlotRrtOptions;
+
+/* Bytes of device workspace nlot_rrt_init needs for B instances (tree, path and spline buffers). */
+size_t nlot_rrt_workspace_size(const NlotRrtOptions* opt, int64_t B);
+
+/* Batched RRTInitializer.get_initial_guess: per instance, an RRT in the xy plane from x0[b][0:2] to xg[b][0:2]
+ * against the scene's EXACT SDF (MultiObstacle.sdf, casadi.py:381-383; the footprint by point inflation,
+ * trajectory_initialization.py:108-113), the path with intermediate points at turns > 60 degrees, greedy
+ * shortcuts and a not-a-knot cubic spline resampled to N + 1 points; other states 0 (:233-236).
+ *   x0, xg   [B][nx] fp64 device      X_init [B][N+1][nx] fp64 device (out)
+ *   ok       [B] int32 device (out): 1, or 0 where the reference raises "RRT failed to find a path within max_iter"
+ *            (X_init of that instance is then the straight line)
+ * Requires prob->sdf_kind-independent obstacles: the analytic scene in prob->obs (the training target in l4casadi
+ * mode). Asynchronous on `stream`. */
+int32_t nlot_rrt_init(const NlotProblem* prob, const NlotRrtOptions* opt, const double* x0, const double* xg,
+                      double* X_init, int32_t* ok, int64_t B, void* workspace, size_t workspace_bytes, void* stream);
 casadi_int_t nn_sdf_n_in(void);
 casadi_int_t nn_sdf_n_out(void);
 const casadi_int_t* nn_sdf_sparsity_in(casadi_int_t i);

@@ -23,7 +23,7 @@ EXPORTED = [
     "nlot_last_stats", "nlot_casadi_bind", "nn_sdf_n_in", "nn_sdf_n_out", "nn_sdf_sparsity_in",
     "nn_sdf_sparsity_out", "nn_sdf", "jac_nn_sdf_n_in", "jac_nn_sdf_n_out", "jac_nn_sdf",
     "adj1_nn_sdf_n_in", "adj1_nn_sdf_n_out", "adj1_nn_sdf", "jac_adj1_nn_sdf_n_in",
-    "jac_adj1_nn_sdf_n_out", "jac_adj1_nn_sdf",
+    "jac_adj1_nn_sdf_n_out", "jac_adj1_nn_sdf", "nlot_rrt_workspace_size", "nlot_rrt_init",
 ]
 
 
@@ -68,6 +68,11 @@ def lib():
     L.nlot_solve_batch.restype = C.c_int32
     L.nlot_set_timing.argtypes = [C.c_int32]
     L.nlot_last_stats.argtypes = [C.POINTER(_abi.NlotSolveStats)]
+    L.nlot_rrt_workspace_size.argtypes = [C.POINTER(_abi.NlotRrtOptions), C.c_int64]
+    L.nlot_rrt_workspace_size.restype = C.c_size_t
+    L.nlot_rrt_init.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotRrtOptions), vp, vp, vp, vp, C.c_int64,
+                                vp, C.c_size_t, vp]
+    L.nlot_rrt_init.restype = C.c_int32
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
     if L.nlot_abi_version() != 6:
