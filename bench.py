@@ -32,6 +32,7 @@ from nlotrajectories_amd import _abi  # noqa: E402
 from nlotrajectories_amd.dist import gather_solutions, max_over_ranks, rank_world, sum_over_ranks  # noqa: E402
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
+from nlotrajectories_amd.rrt import rrt_initial_guess  # noqa: E402
 from nlotrajectories_amd.problem import B6_PROBLEM, BENCHMARKS, METRIC_PROBLEM, STRESS_PROBLEM  # noqa: E402
 from nlotrajectories_amd.sampling import sample_start_goal  # noqa: E402
 from nlotrajectories_amd.solver import last_stats, set_timing, solve_batch  # noqa: E402
@@ -150,7 +151,11 @@ def main():
     nstep = {"n": 0}
 
     def step():
-        r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws)
+        X_init = None
+        if b6:  # benchmark 6's own initializer: RRT against the exact ring scene (YAML rrt settings), timed
+            X_init, _ = rrt_initial_guess(prob, x0, xg, bounds=[[0.0, 0.0], [1.3, 1.3]], step_size=0.02,
+                                          max_iter=5000, margin=0.01, seed=a.seed + 7919 * rank)
+        r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws, X_init=X_init)
         nstep["n"] += 1
         print(f"[bench] rank {rank} solve {nstep['n']} done", file=sys.stderr, flush=True)
         if timing["on"]:
@@ -301,7 +306,8 @@ def main():
                             if stress else
                             ("b6 (BASELINE.json configs[3]): ackermann_2nd L=0.05, rect 0.08x0.05, N=100, dt 0.05, no "
                              "slack (per-corner sdf >= 0), smooth w=0.5, bounds [+-1, +-2], learned SDF of 4 "
-                             "elliptical half rings, linear init, IPOPT tol 1e-4") if b6 else
+                             "elliptical half rings, RRT init (the YAML's: bounds [0, 1.3]^2, step 0.02, max_iter 5000, "
+                             "margin 0.01; inside the timed step), IPOPT tol 1e-4") if b6 else
                             "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
                 "mu_strategy": a.mu_strategy,

@@ -5,8 +5,9 @@ metrics, append the results CSV) with nlot_solve_batch in place of CasADi/IPOPT.
     python -m nlotrajectories_amd.cli --config benchmark_2_unicycle_circle.yaml --initializer linear
 
 Differences from the reference, all loud:
-  * initializer `rrt` (every shipped YAML) is not built yet: pass --initializer linear or
-    default (default = CasADi's zero initial guess, run_benchmark.py:113-114 / DefualtInitializer);
+  * initializer `rrt` (every shipped YAML) runs the batched GPU RRT (rrt.py) with a seeded counter-based
+    random stream (the reference draws from Python's unseeded `random`); --initializer linear|default override
+    it (default = CasADi's zero initial guess, run_benchmark.py:113-114 / DefualtInitializer);
   * solver.mode l4casadi trains a network in the reference (NNObstacleTrainer); here `--weights train` does the
     same (the seeded restatement in trainer.py, on the GPU), or the weights come from --weights (an .npz written
     by MlpWeights.save, e.g. data/b6_mlp128_seed0.npz, or the shipped artefact with --weights artefact);
@@ -65,9 +66,6 @@ def run_benchmark(config_path, initializer="yaml", weights=None, results_dir="re
     if cfg.solver.type != "ipopt":
         raise NotImplementedError("solver.type sqpmethod is not provided (only the IPOPT restatement)")
     init = cfg.solver.initializer.choice.mode if initializer == "yaml" else initializer
-    if init == "rrt":
-        raise NotImplementedError("the rrt initializer is not built yet (DESIGN.md §9); "
-                                  "rerun with --initializer linear or --initializer default")
     prob = cfg.to_problem()
     mlp = None
     if prob.sdf == "mlp":
@@ -87,6 +85,14 @@ def run_benchmark(config_path, initializer="yaml", weights=None, results_dir="re
     if x0.shape[1] != prob.nx or xg.shape[1] != prob.nx:
         raise ValueError(f"start/goal states must have {prob.nx} entries for {prob.dynamics}")
     X_init = np.zeros((1, prob.N + 1, prob.nx)) if init == "default" else None  # CasADi default guess
+    if init == "rrt":  # RRTInitializer (run_benchmark.py:118-131) on the GPU, against the exact scene
+        from .rrt import rrt_initial_guess
+
+        ic = cfg.solver.initializer.choice
+        X_init, ok = rrt_initial_guess(prob, x0, xg, bounds=ic.rrt_bounds, step_size=ic.step_size,
+                                       max_iter=ic.max_iter, margin=ic.margin)
+        if not bool(ok[0]):
+            raise RuntimeError("RRT failed to find a path within max_iter.")
     opt = options or _abi.gpu_options()
     torch.cuda.synchronize()
     t0 = time.time()
@@ -154,8 +160,8 @@ def _f(prob, X, U):
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="run-benchmark")
     ap.add_argument("--config", type=str, required=True, help="Path to benchmark YAML config")
-    ap.add_argument("--initializer", choices=["yaml", "linear", "default"], default="yaml",
-                    help="override the YAML initializer (rrt is not built yet)")
+    ap.add_argument("--initializer", choices=["yaml", "linear", "default", "rrt"], default="yaml",
+                    help="override the YAML initializer (yaml = the config's own, rrt for every shipped one)")
     ap.add_argument("--weights", type=str, default=None, help="learned-SDF weights: 'train' (NNObstacleTrainer), an .npz, or 'artefact'")
     ap.add_argument("--results", type=str, default="results")
     a = ap.parse_args(argv)

@@ -1,6 +1,6 @@
 """YAML surface: the schema (config.py) validates the shipped scenario files and maps them onto the same
 NLP as the restated BENCHMARKS; the reference's malformed configs/*.yaml are rejected;
-the CLI fails loudly on what is not built (rrt, sqpmethod, learned SDF without weights)."""
+the CLI fails loudly on what is not built (sqpmethod, learned SDF without weights)."""
 import glob
 import os
 
@@ -48,11 +48,7 @@ def test_cli_refuses_what_is_not_built(tmp_path):
     from nlotrajectories_amd.cli import run_benchmark
 
     base = yaml.safe_load(open(os.path.join(CFG, "benchmark_2_unicycle_circle.yaml")))
-    base["solver"]["initializer"] = [{"mode": "rrt", "rrt_bounds": [[0, 0], [1, 1]]}]
-    f = tmp_path / "rrt.yaml"
-    f.write_text(yaml.safe_dump(base))
-    with pytest.raises(NotImplementedError, match="rrt"):
-        run_benchmark(f)
+    f = tmp_path / "sqp.yaml"
     base["solver"]["type"] = "sqpmethod"
     f.write_text(yaml.safe_dump(base))
     with pytest.raises(NotImplementedError, match="sqpmethod"):
