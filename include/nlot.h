@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 6
+#define NLOT_ABI_VERSION 7
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -72,6 +72,11 @@ enum NlotObstacleType {
     NLOT_OBS_POLYGON = 2,   /* PolygonObstacle.approximated_sdf casadi.py:150-186 (EllipticRingObstacle
                                casadi.py:193-248 is a polygon of its arc points); (cx, cy) = centroid */
     NLOT_OBS_TRAPEZOID = 3  /* TrapezoidObstacle.approximated_sdf casadi.py:317-374 (4 vertices) */
+};
+
+enum NlotIntegrator {
+    NLOT_INTEG_EULER = 0, /* x_{k+1} = x_k + dt f(x_k, u_k), runner.py:62-63 */
+    NLOT_INTEG_RK4 = 1    /* x_{k+1} = x_k + dt (k1 + 2 k2 + 2 k3 + k4) / 6 (opt-in, non-parity) */
 };
 
 enum NlotSdfKind {
@@ -118,6 +123,9 @@ typedef struct NlotProblem {
     int32_t n_verts;
     NlotObstacle obs[NLOT_MAX_OBS];
     double verts[NLOT_MAX_VERTS][2];
+    int32_t integrator;      /* NLOT_INTEG_EULER (the reference's defects, runner.py:62-63; default) or NLOT_INTEG_RK4
+                                (opt-in classical RK4 step as the defect map; not the reference's NLP) */
+    int32_t pad2_;
 } NlotProblem;
 
 /* IPOPT options (runner.py:113-125 + IPOPT defaults).  See DESIGN.md §4 for the restatement. */

@@ -15,6 +15,7 @@ STATE_DIM = {"point_1st": 4, "point_2nd": 4, "unicycle": 3, "unicycle_2nd": 5, "
 CONTROL_DIM = {k: 2 for k in DYNAMICS}
 SHAPE_DOT, SHAPE_POLYGON = 0, 1
 OBS_CIRCLE, OBS_SQUARE, OBS_POLYGON, OBS_TRAPEZOID = 0, 1, 2, 3
+INTEG_EULER, INTEG_RK4 = 0, 1
 SDF_ANALYTIC, SDF_MLP = 0, 1
 MLP_IN_LINEAR_RELU, MLP_IN_FOURIER = 0, 1
 MAX_OBS, MAX_VERTS, MAX_BODY, MAX_NU = 128, 512, 8, 4
@@ -34,7 +35,7 @@ class NlotProblem(C.Structure):
         ("enforce_heading", C.c_int32), ("sdf_kind", C.c_int32), ("umin", C.c_double * MAX_NU),
         ("umax", C.c_double * MAX_NU), ("softmin_alpha", C.c_double), ("path_eps", C.c_double),
         ("n_obs", C.c_int32), ("n_verts", C.c_int32), ("obs", NlotObstacle * MAX_OBS),
-        ("verts", (C.c_double * 2) * MAX_VERTS),
+        ("verts", (C.c_double * 2) * MAX_VERTS), ("integrator", C.c_int32), ("pad2_", C.c_int32),
     ]
 
 

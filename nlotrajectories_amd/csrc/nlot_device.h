@@ -17,7 +17,7 @@ template <int DYN> struct Dyn;
 
 template <> struct Dyn<NLOT_POINT_1ST> {  // dynamics.py:33-41  f = (u0, u1, 0, 0)
     static constexpr int NX = 4, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o, double = 0) {
         o[0] = u[0]; o[1] = u[1]; o[2] = 0; o[3] = 0; (void)x;
     }
     __device__ __forceinline__ static void jac(const double* x, const double* u, double dt, double, double (*A)[NX], double (*B)[NU]) {
@@ -29,7 +29,7 @@ template <> struct Dyn<NLOT_POINT_1ST> {  // dynamics.py:33-41  f = (u0, u1, 0, 
 
 template <> struct Dyn<NLOT_POINT_2ND> {  // dynamics.py:44-56  f = (vx, vy, ax, ay)
     static constexpr int NX = 4, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o, double = 0) {
         o[0] = x[2]; o[1] = x[3]; o[2] = u[0]; o[3] = u[1];
     }
     __device__ __forceinline__ static void jac(const double*, const double*, double dt, double, double (*A)[NX], double (*B)[NU]) {
@@ -41,7 +41,7 @@ template <> struct Dyn<NLOT_POINT_2ND> {  // dynamics.py:44-56  f = (vx, vy, ax,
 
 template <> struct Dyn<NLOT_UNICYCLE> {  // dynamics.py:59-73  f = (v c, v s, w), u = (v, w)
     static constexpr int NX = 3, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o, double = 0) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = u[0] * c; o[1] = u[0] * s; o[2] = u[1];
     }
@@ -61,7 +61,7 @@ template <> struct Dyn<NLOT_UNICYCLE> {  // dynamics.py:59-73  f = (v c, v s, w)
 
 template <> struct Dyn<NLOT_UNICYCLE_2ND> {  // dynamics.py:76-96  f = (v c, v s, w, a, alpha)
     static constexpr int NX = 5, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double, double* o, double = 0) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = x[3] * c; o[1] = x[3] * s; o[2] = x[4]; o[3] = u[0]; o[4] = u[1];
     }
@@ -83,7 +83,7 @@ template <> struct Dyn<NLOT_UNICYCLE_2ND> {  // dynamics.py:76-96  f = (v c, v s
 
 template <> struct Dyn<NLOT_ACKERMANN> {  // dynamics.py:99-118  f = (v c, v s, v tan(psi)/L, psidot)
     static constexpr int NX = 4, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o, double = 0) {
         double s, c; sincos(x[2], &s, &c);
         o[0] = u[0] * c; o[1] = u[0] * s; o[2] = u[0] * tan(x[3]) / L; o[3] = u[1];
     }
@@ -108,7 +108,7 @@ template <> struct Dyn<NLOT_ACKERMANN> {  // dynamics.py:99-118  f = (v c, v s, 
 
 template <> struct Dyn<NLOT_ACKERMANN_2ND> {  // dynamics.py:121-148, output order reproduced as written
     static constexpr int NX = 7, NU = 2;
-    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o) {
+    __device__ __forceinline__ static void f(const double* x, const double* u, double L, double* o, double = 0) {
         double s, c; sincos(x[2], &s, &c);
         double tp = tan(x[3]), q = 1 + x[3] * x[3];
         o[0] = x[4] * c; o[1] = x[4] * s; o[2] = x[4] * tp / L; o[3] = x[6];
@@ -147,6 +147,155 @@ template <> struct Dyn<NLOT_ACKERMANN_2ND> {  // dynamics.py:121-148, output ord
         H[4][6] += dt * g46; H[6][4] += dt * g46;
     }
 };
+
+// ---------------------------------------------------------------------------------------------
+// RK4 defects (opt-in, NlotProblem.integrator = NLOT_INTEG_RK4; not the reference's discretisation, which is
+// Euler, runner.py:62-63).  Dyn<D + NLOT_RK4_BIAS> keeps the Euler-shaped interface of Dyn<D>: its f is the
+// effective rate f_eff = (k1 + 2 k2 + 2 k3 + k4) / 6, so F = x + dt f_eff is the classical RK4 step, and its
+// jac / hess differentiate f_eff exactly with second-order forward jets over z = (x, u) (the oracle does the
+// same with its jets, in the same operation order).
+// ---------------------------------------------------------------------------------------------
+constexpr int NLOT_RK4_BIAS = 8;
+
+template <int N>
+struct Jt {  // value, gradient, lower-triangular Hessian over N variables
+    double v, g[N], h[N * (N + 1) / 2];
+};
+template <int N> __device__ inline Jt<N> jt_const(double c) {
+    Jt<N> r;
+    r.v = c;
+    for (int i = 0; i < N; ++i) r.g[i] = 0;
+    for (int i = 0; i < N * (N + 1) / 2; ++i) r.h[i] = 0;
+    return r;
+}
+template <int N> __device__ inline Jt<N> jt_var(double c, int i) { Jt<N> r = jt_const<N>(c); r.g[i] = 1; return r; }
+template <int N> __device__ inline Jt<N> operator+(const Jt<N>& a, const Jt<N>& b) {
+    Jt<N> r;
+    r.v = a.v + b.v;
+    for (int i = 0; i < N; ++i) r.g[i] = a.g[i] + b.g[i];
+    for (int i = 0; i < N * (N + 1) / 2; ++i) r.h[i] = a.h[i] + b.h[i];
+    return r;
+}
+template <int N> __device__ inline Jt<N> operator*(const Jt<N>& a, double c) {
+    Jt<N> r;
+    r.v = a.v * c;
+    for (int i = 0; i < N; ++i) r.g[i] = a.g[i] * c;
+    for (int i = 0; i < N * (N + 1) / 2; ++i) r.h[i] = a.h[i] * c;
+    return r;
+}
+template <int N> __device__ inline Jt<N> jt_addc(Jt<N> a, double c) { a.v += c; return a; }
+template <int N> __device__ inline Jt<N> operator*(const Jt<N>& a, const Jt<N>& b) {
+    Jt<N> r;
+    r.v = a.v * b.v;
+    for (int i = 0; i < N; ++i) r.g[i] = a.g[i] * b.v + a.v * b.g[i];
+    for (int i = 0, q = 0; i < N; ++i)
+        for (int j = 0; j <= i; ++j, ++q) r.h[q] = a.h[q] * b.v + a.v * b.h[q] + a.g[i] * b.g[j] + a.g[j] * b.g[i];
+    return r;
+}
+template <int N> __device__ inline Jt<N> jt_unary(const Jt<N>& a, double f0, double f1, double f2) {
+    Jt<N> r;
+    r.v = f0;
+    for (int i = 0; i < N; ++i) r.g[i] = f1 * a.g[i];
+    for (int i = 0, q = 0; i < N; ++i)
+        for (int j = 0; j <= i; ++j, ++q) r.h[q] = f1 * a.h[q] + f2 * a.g[i] * a.g[j];
+    return r;
+}
+// scalar helpers with one spelling for double and jets (the oracle's jet operations, nlot_oracle.c)
+__device__ inline double tsin(double a) { return sin(a); }
+__device__ inline double tcos(double a) { return cos(a); }
+__device__ inline double ttan(double a) { return tan(a); }
+__device__ inline double trecip(double a) { return 1.0 / a; }
+__device__ inline double taddc(double a, double c) { return a + c; }
+__device__ inline double tconst(double c, double) { return c; }
+template <int N> __device__ inline Jt<N> tsin(const Jt<N>& a) { return jt_unary(a, sin(a.v), cos(a.v), -sin(a.v)); }
+template <int N> __device__ inline Jt<N> tcos(const Jt<N>& a) { return jt_unary(a, cos(a.v), -sin(a.v), -cos(a.v)); }
+template <int N> __device__ inline Jt<N> ttan(const Jt<N>& a) {
+    const double t = tan(a.v), s2 = 1.0 + t * t;
+    return jt_unary(a, t, s2, 2.0 * t * s2);
+}
+template <int N> __device__ inline Jt<N> trecip(const Jt<N>& a) {
+    return jt_unary(a, 1.0 / a.v, -1.0 / (a.v * a.v), 2.0 / (a.v * a.v * a.v));
+}
+template <int N> __device__ inline Jt<N> taddc(const Jt<N>& a, double c) { return jt_addc(a, c); }
+template <int N> __device__ inline Jt<N> tconst(double c, const Jt<N>&) { return jt_const<N>(c); }
+
+// f(x, u) of model D for a double or jet scalar, in the oracle's operation order (dyn_f, nlot_oracle.c)
+template <int D, class T>
+__device__ inline void fgen(const T* x, const T* u, double L, T* f) {
+    if constexpr (D == NLOT_POINT_1ST) {
+        f[0] = u[0]; f[1] = u[1]; f[2] = tconst(0.0, x[0]); f[3] = tconst(0.0, x[0]);
+    } else if constexpr (D == NLOT_POINT_2ND) {
+        f[0] = x[2]; f[1] = x[3]; f[2] = u[0]; f[3] = u[1];
+    } else if constexpr (D == NLOT_UNICYCLE) {
+        f[0] = u[0] * tcos(x[2]); f[1] = u[0] * tsin(x[2]); f[2] = u[1];
+    } else if constexpr (D == NLOT_UNICYCLE_2ND) {
+        f[0] = x[3] * tcos(x[2]); f[1] = x[3] * tsin(x[2]); f[2] = x[4]; f[3] = u[0]; f[4] = u[1];
+    } else if constexpr (D == NLOT_ACKERMANN) {
+        f[0] = u[0] * tcos(x[2]); f[1] = u[0] * tsin(x[2]); f[2] = (u[0] * ttan(x[3])) * (1.0 / L); f[3] = u[1];
+    } else {  // ackermann_2nd, vector order as written (domega in the v slot)
+        f[0] = x[4] * tcos(x[2]); f[1] = x[4] * tsin(x[2]); f[2] = (x[4] * ttan(x[3])) * (1.0 / L); f[3] = x[6];
+        f[4] = ((x[6] * trecip(taddc(x[3] * x[3], 1.0))) * x[4] + ttan(x[3]) * u[0]) * (1.0 / L);
+        f[5] = u[0]; f[6] = u[1];
+    }
+}
+// f_eff = (k1 + 2 k2 + 2 k3 + k4) / 6 with stage points x + k (dt / 2), x + k (dt / 2), x + k dt
+template <int D, int NX, class T>
+__device__ inline void rk4_feff(const T* x, const T* u, double dt, double L, T* fe) {
+    T k[NX], xs[NX];
+    fgen<D>(x, u, L, k);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { fe[i] = k[i]; xs[i] = x[i] + k[i] * (0.5 * dt); }
+    fgen<D>(xs, u, L, k);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { fe[i] = fe[i] + k[i] * 2.0; xs[i] = x[i] + k[i] * (0.5 * dt); }
+    fgen<D>(xs, u, L, k);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { fe[i] = fe[i] + k[i] * 2.0; xs[i] = x[i] + k[i] * dt; }
+    fgen<D>(xs, u, L, k);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) fe[i] = (fe[i] + k[i]) * (1.0 / 6.0);
+}
+template <int D, int NX, int NU>
+__device__ __noinline__ void rk4_jets(const double* x, const double* u, double dt, double L, Jt<NX + NU>* fe) {
+    constexpr int N = NX + NU;
+    Jt<N> xj[NX], uj[NU];
+    for (int i = 0; i < NX; ++i) xj[i] = jt_var<N>(x[i], i);
+    for (int i = 0; i < NU; ++i) uj[i] = jt_var<N>(u[i], NX + i);
+    rk4_feff<D, NX>(xj, uj, dt, L, fe);
+}
+
+template <int D>
+struct DynRk4 {
+    static constexpr int NX = Dyn<D>::NX, NU = Dyn<D>::NU, N = NX + NU;
+    __device__ static void f(const double* x, const double* u, double L, double* o, double dt) {
+        rk4_feff<D, NX>(x, u, dt, L, o);
+    }
+    __device__ static void jac(const double* x, const double* u, double dt, double L, double (*A)[NX], double (*B)[NU]) {
+        Jt<N> fe[NX];
+        rk4_jets<D, NX, NU>(x, u, dt, L, fe);
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) A[i][j] = (i == j ? 1.0 : 0.0) + dt * fe[i].g[j];
+            for (int j = 0; j < NU; ++j) B[i][j] = dt * fe[i].g[NX + j];
+        }
+    }
+    __device__ static void hess(const double* x, const double* u, const double* l, double dt, double L, double (*H)[N]) {
+        Jt<N> fe[NX];
+        rk4_jets<D, NX, NU>(x, u, dt, L, fe);
+        for (int a = 0; a < N; ++a)
+            for (int b = 0; b < N; ++b) {
+                const int q = a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a;
+                double s = 0;
+                for (int i = 0; i < NX; ++i) s += l[i] * fe[i].h[q];
+                H[a][b] += dt * s;
+            }
+    }
+};
+template <> struct Dyn<NLOT_POINT_1ST + NLOT_RK4_BIAS> : DynRk4<NLOT_POINT_1ST> {};
+template <> struct Dyn<NLOT_POINT_2ND + NLOT_RK4_BIAS> : DynRk4<NLOT_POINT_2ND> {};
+template <> struct Dyn<NLOT_UNICYCLE + NLOT_RK4_BIAS> : DynRk4<NLOT_UNICYCLE> {};
+template <> struct Dyn<NLOT_UNICYCLE_2ND + NLOT_RK4_BIAS> : DynRk4<NLOT_UNICYCLE_2ND> {};
+template <> struct Dyn<NLOT_ACKERMANN + NLOT_RK4_BIAS> : DynRk4<NLOT_ACKERMANN> {};
+template <> struct Dyn<NLOT_ACKERMANN_2ND + NLOT_RK4_BIAS> : DynRk4<NLOT_ACKERMANN_2ND> {};
 
 // ---------------------------------------------------------------------------------------------
 // 2-D hyper-dual number (value, gradient, Hessian in (x, y)) for the analytic SDFs

@@ -739,7 +739,7 @@ __device__ __forceinline__ void ric_sync_reads() {
 // waves per SIMD of k_ric: NLOT_WPE_RIC, except ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
 template <int DYN>
 struct RicWpe {
-    static constexpr int value = DYN == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
+    static constexpr int value = DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
 };
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
@@ -1675,7 +1675,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
 #pragma unroll
         for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
-        Dyn<DYN>::f(x, u, p.wheelbase, f);
+        Dyn<DYN>::f(x, u, p.wheelbase, f, p.dt);
 #pragma unroll
         for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
     }
@@ -2490,7 +2490,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     double u[NU], f[NX];
 #pragma unroll
                     for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
-                    Dyn<DYN>::f(xk, u, p.wheelbase, f);
+                    Dyn<DYN>::f(xk, u, p.wheelbase, f, p.dt);
 #pragma unroll
                     for (int i = 0; i < NX; ++i) {
                         const double c = AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]);
@@ -2800,6 +2800,9 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
         return NLOT_ERR_INVALID;
     }
     if (p->N < 2 || p->N > 4096 || p->dt <= 0) { set_error("N must be in [2, 4096], dt > 0"); return NLOT_ERR_INVALID; }
+    if (p->integrator != NLOT_INTEG_EULER && p->integrator != NLOT_INTEG_RK4) {
+        set_error("integrator must be NLOT_INTEG_EULER or NLOT_INTEG_RK4"); return NLOT_ERR_INVALID;
+    }
     if (p->shape == NLOT_SHAPE_POLYGON && (p->n_body < 1 || p->n_body > MMAX)) {
         set_error("polygon footprint: 1..4 corners"); return NLOT_ERR_INVALID;
     }
@@ -3013,14 +3016,23 @@ extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOption
         return NLOT_ERR_WORKSPACE;
     }
     hipStream_t st = (hipStream_t)stream;
-    switch (p->dynamics) {
-    case NLOT_POINT_1ST: return run<NLOT_POINT_1ST>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
-    case NLOT_POINT_2ND: return run<NLOT_POINT_2ND>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
-    case NLOT_UNICYCLE: return run<NLOT_UNICYCLE>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
-    case NLOT_UNICYCLE_2ND: return run<NLOT_UNICYCLE_2ND>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
-    case NLOT_ACKERMANN: return run<NLOT_ACKERMANN>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
-    case NLOT_ACKERMANN_2ND: return run<NLOT_ACKERMANN_2ND>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
+    // the dynamics model and the integrator select the instantiation (Euler: DYN; RK4: DYN + NLOT_RK4_BIAS)
+#define NLOT_RUN(D) return run<D>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st)
+    switch (p->dynamics + (p->integrator == NLOT_INTEG_RK4 ? NLOT_RK4_BIAS : 0)) {
+    case NLOT_POINT_1ST: NLOT_RUN(NLOT_POINT_1ST);
+    case NLOT_POINT_2ND: NLOT_RUN(NLOT_POINT_2ND);
+    case NLOT_UNICYCLE: NLOT_RUN(NLOT_UNICYCLE);
+    case NLOT_UNICYCLE_2ND: NLOT_RUN(NLOT_UNICYCLE_2ND);
+    case NLOT_ACKERMANN: NLOT_RUN(NLOT_ACKERMANN);
+    case NLOT_ACKERMANN_2ND: NLOT_RUN(NLOT_ACKERMANN_2ND);
+    case NLOT_POINT_1ST + NLOT_RK4_BIAS: NLOT_RUN(NLOT_POINT_1ST + NLOT_RK4_BIAS);
+    case NLOT_POINT_2ND + NLOT_RK4_BIAS: NLOT_RUN(NLOT_POINT_2ND + NLOT_RK4_BIAS);
+    case NLOT_UNICYCLE + NLOT_RK4_BIAS: NLOT_RUN(NLOT_UNICYCLE + NLOT_RK4_BIAS);
+    case NLOT_UNICYCLE_2ND + NLOT_RK4_BIAS: NLOT_RUN(NLOT_UNICYCLE_2ND + NLOT_RK4_BIAS);
+    case NLOT_ACKERMANN + NLOT_RK4_BIAS: NLOT_RUN(NLOT_ACKERMANN + NLOT_RK4_BIAS);
+    case NLOT_ACKERMANN_2ND + NLOT_RK4_BIAS: NLOT_RUN(NLOT_ACKERMANN_2ND + NLOT_RK4_BIAS);
     }
+#undef NLOT_RUN
     set_error("unknown dynamics");
     return NLOT_ERR_INVALID;
 }

@@ -51,6 +51,7 @@ class Problem:
     sdf: str = "analytic"               # analytic | mlp
     softmin_alpha: float = 10.0         # utils.py:18
     path_eps: float = 1e-8              # runner.py:81
+    integrator: str = "euler"           # euler (runner.py:62-63) | rk4 (opt-in, not the reference's NLP)
 
     @property
     def nx(self) -> int:
@@ -106,6 +107,9 @@ class Problem:
             p.umin[i], p.umax[i] = float(lo), float(hi)
         p.softmin_alpha = float(self.softmin_alpha)
         p.path_eps = float(self.path_eps)
+        if self.integrator not in ("euler", "rk4"):
+            raise ValueError(f"integrator must be 'euler' or 'rk4', not {self.integrator!r}")
+        p.integrator = _abi.INTEG_RK4 if self.integrator == "rk4" else _abi.INTEG_EULER
         p.n_obs = len(prims)
         for i, o in enumerate(prims):
             q = p.obs[i]

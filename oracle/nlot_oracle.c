@@ -444,6 +444,13 @@ static void dyn_f(const NlotProblem* p, const jet* x, const jet* u, jet* f) {
     }
 }
 
+/* The defect map F(x, u) = x + dt f (Euler) or the RK4 step, with A = dF/dx [nx][nx], B = dF/du [nx][nu] */
+static void dyn_eval(const NlotProblem* p, const double* x, const double* u, const double* lam, double* F,
+                     double* A, double* B, double* Hl);
+void oracle_dyn_map(const NlotProblem* p, const double* x, const double* u, double* F, double* A, double* B) {
+    dyn_eval(p, x, u, NULL, F, A, B, NULL);
+}
+
 void oracle_dynamics(const NlotProblem* p, const double* x, const double* u, double* f) {
     int n = p->nx + p->nu;
     jet xj[8], uj[4], fj[8];
@@ -453,14 +460,35 @@ void oracle_dynamics(const NlotProblem* p, const double* x, const double* u, dou
     for (int i = 0; i < p->nx; ++i) f[i] = fj[i].v;
 }
 
-/* F = x + dt f(x,u) (runner.py:62-63): value, A = dF/dx, B = dF/du, Hl = sum_i lam_i d2F_i/dz2 */
+/* The opt-in RK4 defect map (NLOT_INTEG_RK4, not the reference's NLP): the effective rate
+   f_eff = (k1 + 2 k2 + 2 k3 + k4) / 6 with stage points x + k dt/2, x + k dt/2, x + k dt, so that
+   F = x + dt f_eff; the GPU's DynRk4 (nlot_device.h) uses the same operation order. */
+static void dyn_feff(const NlotProblem* p, const jet* x, const jet* u, jet* fe) {
+    if (p->integrator != NLOT_INTEG_RK4) {
+        dyn_f(p, x, u, fe);
+        return;
+    }
+    const int nx = p->nx;
+    const double dt = p->dt;
+    jet k[8], xs[8];
+    dyn_f(p, x, u, k);
+    for (int i = 0; i < nx; ++i) { fe[i] = k[i]; xs[i] = jadd(x[i], jscale(k[i], 0.5 * dt)); }
+    dyn_f(p, xs, u, k);
+    for (int i = 0; i < nx; ++i) { fe[i] = jadd(fe[i], jscale(k[i], 2.0)); xs[i] = jadd(x[i], jscale(k[i], 0.5 * dt)); }
+    dyn_f(p, xs, u, k);
+    for (int i = 0; i < nx; ++i) { fe[i] = jadd(fe[i], jscale(k[i], 2.0)); xs[i] = jadd(x[i], jscale(k[i], dt)); }
+    dyn_f(p, xs, u, k);
+    for (int i = 0; i < nx; ++i) fe[i] = jscale(jadd(fe[i], k[i]), 1.0 / 6.0);
+}
+
+/* F = x + dt f(x,u) (runner.py:62-63; f_eff under RK4): value, A = dF/dx, B = dF/du, Hl = sum_i lam_i d2F_i/dz2 */
 static void dyn_eval(const NlotProblem* p, const double* x, const double* u, const double* lam, double* F,
                      double* A, double* B, double* Hl) {
     int nx = p->nx, nu = p->nu, n = nx + nu;
     jet xj[8], uj[4], fj[8];
     for (int i = 0; i < nx; ++i) xj[i] = jvar(n, x[i], i);
     for (int i = 0; i < nu; ++i) uj[i] = jvar(n, u[i], nx + i);
-    dyn_f(p, xj, uj, fj);
+    dyn_feff(p, xj, uj, fj);
     for (int i = 0; i < nx; ++i) {
         F[i] = x[i] + p->dt * fj[i].v;
         if (A)

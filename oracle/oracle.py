@@ -99,6 +99,16 @@ def soft_min(vals, alpha=10.0):
     return lib().oracle_soft_min(_dp(v), len(v), alpha)
 
 
+def dyn_map(problem, x, u):
+    """(F, A, B) of the defect map x_{k+1} = F(x_k, u_k): Euler or, with problem.integrator 'rk4', RK4."""
+    pc = problem.to_c()
+    nx, nu = problem.nx, problem.nu
+    F, A, B = np.zeros(nx), np.zeros((nx, nx)), np.zeros((nx, nu))
+    lib().oracle_dyn_map(C.byref(pc), _dp(np.ascontiguousarray(x, np.float64)), _dp(np.ascontiguousarray(u, np.float64)),
+                         _dp(F), _dp(A), _dp(B))
+    return F, A, B
+
+
 def dynamics(problem, x, u):
     pc = problem.to_c()
     x = np.ascontiguousarray(x, np.float64)

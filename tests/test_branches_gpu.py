@@ -49,6 +49,9 @@ def _cases():
         # group of 18 trapezoids soft_min'ed inside the scene's soft_min) next to a trapezoid
         **{name: _yaml_case(fn) for name, fn in (("b4_polygon", "benchmark_4_dot_nonconvex.yaml"),
                                                   ("b6_elliptical_rings", "benchmark_6_ackermann_wave.yaml"))},
+        # the opt-in RK4 defects (X1; not the reference's Euler NLP): the DYN + NLOT_RK4_BIAS instantiations
+        "b2_rk4": (b2["problem"].with_(integrator="rk4"), b2["start"], b2["goal"]),
+        "b5_ackermann2nd_rk4": (b5["problem"].with_(integrator="rk4"), b5["start"], b5["goal"]),
         "discr_s_trapezoid": (Problem(dynamics="unicycle_2nd", length=0.1, width=0.05, N=50, slack_penalty=10,
                                       control_bounds=((-1, 1), (-1, 1)), obstacles=[
                                           {"type": "discr_s", "center": (0.3, 0.5), "semi_axes": (0.25, 0.2),

@@ -131,3 +131,36 @@ def test_analytic_sdf_derivatives_match_finite_differences(name):
         H_fd = (fp[:, 1:3] - fm[:, 1:3]) / (2 * h)
         cols = (3, 4) if a == 0 else (4, 5)
         np.testing.assert_allclose(out[:, cols], H_fd, rtol=1e-4, atol=1e-4, err_msg=(name, a))
+
+
+@pytest.mark.parametrize("dyn", ["point_1st", "point_2nd", "unicycle", "unicycle_2nd", "ackermann", "ackermann_2nd"])
+def test_rk4_defect_map(dyn):
+    """The opt-in RK4 defect map (integrator='rk4'; not the reference's Euler NLP) equals the classical RK4 step
+    of the reference's own f (golden-pinned above), and its A, B match central differences."""
+    import oracle as O
+    from nlotrajectories_amd.problem import Problem
+
+    kw = dict(dynamics=dyn, shape="dot", dt=0.1, obstacles=[{"type": "circle", "center": (0, 0), "radius": 0.1}])
+    if "ackermann" in dyn:
+        kw["wheelbase"] = 0.1
+    p = Problem(**kw).with_(integrator="rk4")
+    rng = np.random.default_rng(2)
+    x, u = rng.uniform(-0.8, 0.8, p.nx), rng.uniform(-1, 1, p.nu)
+    f = lambda z: np.asarray(O.dynamics(p, z, u))  # noqa: E731
+    k1 = f(x)
+    k2 = f(x + 0.5 * p.dt * k1)
+    k3 = f(x + 0.5 * p.dt * k2)
+    k4 = f(x + p.dt * k3)
+    F, A, B = O.dyn_map(p, x, u)
+    np.testing.assert_allclose(F, x + p.dt * (k1 + 2 * k2 + 2 * k3 + k4) / 6, rtol=0, atol=1e-14)
+    h = 1e-6
+    for j in range(p.nx):
+        e = np.zeros(p.nx)
+        e[j] = h
+        np.testing.assert_allclose(A[:, j], (O.dyn_map(p, x + e, u)[0] - O.dyn_map(p, x - e, u)[0]) / (2 * h), atol=1e-7)
+    for j in range(p.nu):
+        e = np.zeros(p.nu)
+        e[j] = h
+        np.testing.assert_allclose(B[:, j], (O.dyn_map(p, x, u + e)[0] - O.dyn_map(p, x, u - e)[0]) / (2 * h), atol=1e-7)
+    Fe, _, _ = O.dyn_map(p.with_(integrator="euler"), x, u)
+    np.testing.assert_allclose(Fe, x + p.dt * k1, atol=1e-15)
