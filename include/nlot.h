@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 7
+#define NLOT_ABI_VERSION 8
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -161,20 +161,29 @@ typedef struct NlotSolverOptions {
 
 /* Learned SDF: an l4casadi-wrappable torch model, flattened.
  *   FourierMLP (core/nn_architectures.py:30-72):  h0 = scale * cos(p @ A + b0)         (in_kind 1)
- *   l4c.naive.MultiLayerPerceptron:              h0 = relu(p @ A + b0)                 (in_kind 0)
- *   then n_hidden x  h_{l+1} = relu(W_l h_l + b_l);   f = w_out . h + b_out.
+ *   l4c.naive.MultiLayerPerceptron:              h0 = act(p @ A + b0)                  (in_kind 0)
+ *   SIREN (core/nn_architectures.py:8-26,75-100): in_kind 0 with act = NLOT_ACT_SINE, fourier_scale = omega_0
+ *   then n_hidden x  h_{l+1} = act(W_l h_l + b_l);   f = w_out . h + b_out.
+ * ReLU nets run on the MFMA kernels (n_hidden 1-4); the smooth activations on the hyper-dual kernel
+ * (value, gradient and Hessian propagated forward through every layer; n_hidden 0-4), DESIGN.md §7.
  * All weights fp32 (the reference's l4casadi path evaluates the TorchScript graph in fp32,
  * gen/nn_sdf.cpp casts the CasADi doubles to float).  Host OR device pointers depending on the
  * consumer (nlot_mlp_create copies host arrays to the device). */
 #define NLOT_MLP_IN_LINEAR_RELU 0
 #define NLOT_MLP_IN_FOURIER 1
+/* activations (core/nn_architectures.py:47-52 names; l4casadi naive: ReLU/Tanh/Sigmoid/LeakyReLU) */
+#define NLOT_ACT_RELU 0
+#define NLOT_ACT_TANH 1
+#define NLOT_ACT_SIGMOID 2
+#define NLOT_ACT_LEAKY_RELU 3 /* negative slope 0.01 (F.leaky_relu / nn.LeakyReLU default) */
+#define NLOT_ACT_SINE 4       /* sin(omega_0 z), SineLayer nn_architectures.py:8-26; omega_0 in fourier_scale */
 
 typedef struct NlotMlpDesc {
     int32_t in_kind;       /* NLOT_MLP_IN_* */
     int32_t hidden;        /* H (multiple of 32, <= 256) */
     int32_t n_hidden;      /* hidden HxH layers (>= 0) */
-    int32_t act;           /* 0 = ReLU (the only activation in round 1) */
-    float fourier_scale;   /* FourierFeatureLayer.scale */
+    int32_t act;           /* NLOT_ACT_* of the hidden layers (and of the input layer when in_kind 0) */
+    float fourier_scale;   /* FourierFeatureLayer.scale (in_kind 1); omega_0 when act = NLOT_ACT_SINE */
     float b_out;
     const float* A;        /* [2][H]  (in, out) */
     const float* b0;       /* [H] */

@@ -18,6 +18,8 @@ OBS_CIRCLE, OBS_SQUARE, OBS_POLYGON, OBS_TRAPEZOID = 0, 1, 2, 3
 INTEG_EULER, INTEG_RK4 = 0, 1
 SDF_ANALYTIC, SDF_MLP = 0, 1
 MLP_IN_LINEAR_RELU, MLP_IN_FOURIER = 0, 1
+# hidden activations (include/nlot.h NLOT_ACT_*)
+ACT_RELU, ACT_TANH, ACT_SIGMOID, ACT_LEAKY_RELU, ACT_SINE = 0, 1, 2, 3, 4
 MAX_OBS, MAX_VERTS, MAX_BODY, MAX_NU = 128, 512, 8, 4
 
 

@@ -46,7 +46,8 @@ struct MlpDev {
     int in_kind;     // NLOT_MLP_IN_*
     int H;           // hidden width
     int n_hidden;    // HxH layers
-    float scale;     // fourier scale
+    int act;         // NLOT_ACT_* (ReLU: the MFMA kernels; smooth activations: mlp_smooth)
+    float scale;     // fourier scale; omega_0 for NLOT_ACT_SINE
     float b_out;
     const float* A;     // [2][H]
     const float* b0;    // [H]
@@ -54,6 +55,7 @@ struct MlpDev {
     const float* b;     // [n_hidden][H]
     const float* w_out; // [H]
     const void* Wp;     // [3][H][H] bf16 planes (hi, mid, lo) of layer 0, for the split-bf16 value kernel
+    const float* Wt;    // [n_hidden][H][H] (in, out): transposed HxH layers for mlp_smooth (smooth nets only)
 };
 
 // Output addressing of the MLP kernel: element q of point i goes to ptr_q[i * stride_q].

@@ -989,9 +989,197 @@ static int launch_stream(const MlpDev& w, const float* pts, int64_t n, const int
     return NLOT_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Smooth activations (tanh, sigmoid, leaky ReLU, SIREN's sine; core/nn_architectures.py:8-100 and
+// l4casadi's naive MLP): the Hessian has a term from every layer, so value, gradient and Hessian are
+// carried FORWARD through the net as hyper-duals in fp32 — per hidden unit the 6 components
+// (a, a_x, a_y, a_xx, a_xy, a_yy) of a point, with z = W a + b linear in all of them and, per unit,
+//   a = s(z), a_x = s'(z) z_x, a_xx = s''(z) z_x^2 + s'(z) z_xx, a_xy = s''(z) z_x z_y + s'(z) z_xy, ...
+// A block of 256 threads owns a tile of kSmoothPB points: thread t computes hidden unit t % H for the
+// points of group t / H; the layer's activations of the tile sit in LDS as [k][point][component] (one
+// broadcast float4 stream per k), the weights come transposed ([in][out]: a coalesced row per k) from L2.
+// These nets are not on the metric path (the reference's YAMLs use ReLU); the bound is the fp32 VALU at
+// 6 H^2 FMA per point and layer.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSmoothPB = 8;
+
+// s(z), s'(z), s''(z) of the activation
+__device__ __forceinline__ void act3(int act, float omega, float z, float& s, float& d1, float& d2) {
+    if (act == NLOT_ACT_TANH) {
+        s = tanhf(z);
+        d1 = 1.f - s * s;
+        d2 = -2.f * s * d1;
+    } else if (act == NLOT_ACT_SIGMOID) {
+        s = 1.f / (1.f + expf(-z));
+        d1 = s * (1.f - s);
+        d2 = d1 * (1.f - 2.f * s);
+    } else if (act == NLOT_ACT_LEAKY_RELU) {
+        s = z > 0.f ? z : 0.01f * z;
+        d1 = z > 0.f ? 1.f : 0.01f;
+        d2 = 0.f;
+    } else if (act == NLOT_ACT_SINE) {
+        const float u = omega * z;  // torch: sin(omega_0 * linear(x)), the product rounded first
+        s = sinf(u);
+        const float c = cosf(u);
+        d1 = omega * c;
+        d2 = -omega * omega * s;
+    } else {  // ReLU
+        s = z > 0.f ? z : 0.f;
+        d1 = z > 0.f ? 1.f : 0.f;
+        d2 = 0.f;
+    }
+}
+
+template <int H, bool FULL>
+__global__ __launch_bounds__(256) void mlp_smooth(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+                                                  const int* __restrict__ cnt_dev, int P_per, int64_t ld,
+                                                  const float* __restrict__ lam, MlpOut out) {
+    constexpr int NC = FULL ? 6 : 1;            // hyper-dual components carried
+    constexpr int NG = 256 / H;                 // point groups of a block
+    constexpr int PPT = kSmoothPB / NG;         // points per thread
+    constexpr int ROW = kSmoothPB * NC;         // floats per k in LDS
+    static_assert(NG >= 1 && PPT >= 1 && (PPT * NC) % 2 == 0, "mlp_smooth shape");
+    __shared__ __attribute__((aligned(16))) float act_s[H * ROW];
+    __shared__ float pxy[kSmoothPB][2];
+    __shared__ float lam_s[kSmoothPB];
+    __shared__ int64_t pidx[kSmoothPB];
+    const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
+    const int64_t npts = cnt * P_per;
+    const int t = threadIdx.x, i = t % H, grp = t / H, p0 = grp * PPT;
+    const int act = w.act, L = w.n_hidden;
+    const float omega = w.scale;
+    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
+    for (int64_t tile = blockIdx.x; tile * kSmoothPB < npts; tile += gridDim.x) {
+        if (t < kSmoothPB) {
+            const int64_t gi = tile * kSmoothPB + t;
+            const bool valid = gi < npts;
+            const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : -1;
+            pidx[t] = pi;
+            pxy[t][0] = valid ? pts[2 * pi] : 0.f;
+            pxy[t][1] = valid ? pts[2 * pi + 1] : 0.f;
+            lam_s[t] = (valid && lam) ? lam[pi] : 1.f;
+        }
+        __syncthreads();
+        // input layer: z = p A + b0 (as torch: p @ A then + b0), dz/dp = (A0, A1), d2z = 0
+        const float a0 = w.A[i], a1 = w.A[H + i], bb = w.b0[i];
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+            const int p = p0 + q;
+            const float z = fmaf(pxy[p][1], a1, pxy[p][0] * a0) + bb;
+            float s, d1, d2;
+            if (fourier) {  // scale * cos(z) (nn_architectures.py:38)
+                const float sn = sinf(z), cs = cosf(z);
+                s = cs * w.scale;
+                d1 = -w.scale * sn;
+                d2 = -w.scale * cs;
+            } else {
+                act3(act, omega, z, s, d1, d2);
+            }
+            float* dst = act_s + i * ROW + p * NC;
+            dst[0] = s;
+            if constexpr (FULL) {
+                dst[1] = d1 * a0;
+                dst[2] = d1 * a1;
+                dst[3] = d2 * a0 * a0;
+                dst[4] = d2 * a0 * a1;
+                dst[5] = d2 * a1 * a1;
+            }
+        }
+        __syncthreads();
+        // hidden layers
+#pragma unroll 1
+        for (int l = 0; l < L; ++l) {
+            const float* Wt = w.Wt + (size_t)l * H * H + i;
+            float acc[PPT * NC];
+#pragma unroll
+            for (int e = 0; e < PPT * NC; ++e) acc[e] = 0.f;
+            const float* src = act_s + p0 * NC;
+#pragma unroll 4
+            for (int k = 0; k < H; ++k) {
+                const float wk = Wt[(size_t)k * H];
+                const float2* ak = reinterpret_cast<const float2*>(src + k * ROW);
+#pragma unroll
+                for (int e2 = 0; e2 < PPT * NC / 2; ++e2) {
+                    const float2 v = ak[e2];
+                    acc[2 * e2] = fmaf(wk, v.x, acc[2 * e2]);
+                    acc[2 * e2 + 1] = fmaf(wk, v.y, acc[2 * e2 + 1]);
+                }
+            }
+            const float bl = w.b[(size_t)l * H + i];
+            __syncthreads();  // every thread has read the layer's input
+#pragma unroll
+            for (int q = 0; q < PPT; ++q) {
+                const float* z = acc + q * NC;
+                float s, d1, d2;
+                act3(act, omega, z[0] + bl, s, d1, d2);
+                float* dst = act_s + i * ROW + (p0 + q) * NC;
+                dst[0] = s;
+                if constexpr (FULL) {
+                    dst[1] = d1 * z[1];
+                    dst[2] = d1 * z[2];
+                    dst[3] = fmaf(d2 * z[1], z[1], d1 * z[3]);
+                    dst[4] = fmaf(d2 * z[1], z[2], d1 * z[4]);
+                    dst[5] = fmaf(d2 * z[2], z[2], d1 * z[5]);
+                }
+            }
+            __syncthreads();
+        }
+        // output layer: thread (point, component) contracts w_out over the hidden units
+        if (t < ROW) {
+            const int p = t / NC, c = t % NC;
+            float s = 0.f;
+            for (int k = 0; k < H; ++k) s = fmaf(w.w_out[k], act_s[k * ROW + t], s);
+            const int64_t pi = pidx[p];
+            if (pi >= 0) {
+                const float lm = lam_s[p];
+                if (c == 0) out.val[pi * out.sv] = s + w.b_out;
+                if constexpr (FULL) {
+                    if (c == 1 && out.gx) out.gx[pi * out.sg] = lm * s;
+                    if (c == 2 && out.gy) out.gy[pi * out.sg] = lm * s;
+                    if (out.hxx) {
+                        if (c == 3) out.hxx[pi * out.sh] = lm * s;
+                        if (c == 4) {
+                            out.hxy[pi * out.sh] = lm * s;
+                            if (out.hyx != out.hxy) out.hyx[pi * out.sh] = lm * s;
+                        }
+                        if (c == 5) out.hyy[pi * out.sh] = lm * s;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the tile's LDS is reused by the next one
+    }
+}
+
+template <int H, bool FULL>
+static int launch_smooth(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                         const float* lam, const MlpOut& out, hipStream_t stream) {
+    const int64_t tiles = (n * P_per + kSmoothPB - 1) / kSmoothPB;
+    const int64_t cap = (int64_t)device_cus() * 8;
+    const int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
+    hipLaunchKernelGGL((mlp_smooth<H, FULL>), dim3(grid), dim3(256), 0, stream, w, pts, n, n_dev, P_per, ld, lam, out);
+    NLOT_HIP_CHECK(hipGetLastError());
+    return NLOT_OK;
+}
+
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                        const float* lam, const MlpOut& out, bool full, hipStream_t stream, const MlpReuse* reuse) {
     if (n <= 0) return NLOT_OK;
+    if (w.act != NLOT_ACT_RELU) {  // smooth activations: forward hyper-duals (the ReLU masks / reuse do not apply)
+        if (w.n_hidden < 0 || w.n_hidden > kMaxStreamLayers) {
+            set_error("MLP kernel: 0 to 4 hidden HxH layers are supported for smooth activations");
+            return NLOT_ERR_INVALID;
+        }
+#define NLOT_SMOOTH_CASE(HH)                                                                     \
+    if (w.H == HH) return full ? launch_smooth<HH, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream) \
+                               : launch_smooth<HH, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+        NLOT_SMOOTH_CASE(64)
+        NLOT_SMOOTH_CASE(128)
+        NLOT_SMOOTH_CASE(256)
+#undef NLOT_SMOOTH_CASE
+        set_error("MLP kernel: hidden width must be 64, 128 or 256 (DESIGN.md §7)");
+        return NLOT_ERR_INVALID;
+    }
     if (w.n_hidden < 1 || w.n_hidden > kMaxStreamLayers) {
         set_error("MLP kernel: 1 to 4 hidden HxH layers are supported (DESIGN.md §7)");
         return NLOT_ERR_INVALID;
@@ -1031,19 +1219,23 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
         set_error("nlot_mlp_create: null descriptor or weight pointer");
         return nullptr;
     }
-    if (d->act != 0 || (d->in_kind != NLOT_MLP_IN_FOURIER && d->in_kind != NLOT_MLP_IN_LINEAR_RELU)) {
-        set_error("nlot_mlp_create: only ReLU hidden layers with a Fourier or Linear+ReLU input layer");
+    if (d->act < NLOT_ACT_RELU || d->act > NLOT_ACT_SINE ||
+        (d->in_kind != NLOT_MLP_IN_FOURIER && d->in_kind != NLOT_MLP_IN_LINEAR_RELU)) {
+        set_error("nlot_mlp_create: activation must be NLOT_ACT_* and the input layer Fourier or Linear+act");
         return nullptr;
     }
-    if ((d->hidden != 64 && d->hidden != 128 && d->hidden != 256) || d->n_hidden < 1 ||
+    const bool smooth = d->act != NLOT_ACT_RELU;
+    if ((d->hidden != 64 && d->hidden != 128 && d->hidden != 256) || d->n_hidden < (smooth ? 0 : 1) ||
         d->n_hidden > kMaxStreamLayers) {
-        set_error("nlot_mlp_create: hidden width 64/128/256 with 1-4 hidden HxH layers supported (DESIGN.md §7)");
+        set_error("nlot_mlp_create: hidden width 64/128/256 with 1-4 hidden HxH layers supported (0-4 for smooth "
+                  "activations; DESIGN.md §7)");
         return nullptr;
     }
     const int H = d->hidden, L = d->n_hidden;
     const size_t nA = 2 * H, nb0 = H, nW = (size_t)L * H * H, nb = (size_t)L * H, nw = H;
     const size_t nWp = (size_t)3 * H * H / 2;  // bf16 planes of layer 0, in float units
-    const size_t total = nA + nb0 + nW + nb + nw + nWp;
+    const size_t nWt = smooth ? nW : 0;        // transposed HxH layers (mlp_smooth)
+    const size_t total = nA + nb0 + nW + nb + nw + nWp + nWt + 4;
     float* blk = nullptr;
     if (hipMalloc(&blk, total * sizeof(float)) != hipSuccess) {
         set_error("nlot_mlp_create: hipMalloc failed");
@@ -1052,7 +1244,7 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     float* p = blk;
     auto put = [&](const float* src, size_t cnt) -> float* {
         float* dst = p;
-        hipMemcpy(dst, src, cnt * sizeof(float), hipMemcpyHostToDevice);
+        if (cnt) hipMemcpy(dst, src, cnt * sizeof(float), hipMemcpyHostToDevice);
         p += cnt;
         return dst;
     };
@@ -1063,6 +1255,7 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     m->dev.in_kind = d->in_kind;
     m->dev.H = H;
     m->dev.n_hidden = L;
+    m->dev.act = d->act;
     m->dev.scale = d->fourier_scale;
     m->dev.b_out = d->b_out;
     m->dev.A = put(d->A, nA);
@@ -1070,7 +1263,8 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     m->dev.W = put(d->W, nW);
     m->dev.b = put(d->b, nb);
     m->dev.w_out = put(d->w_out, nw);
-    {  // layer-0 weights split into three bf16 planes, round-to-nearest-even at each step (host, exact)
+    m->dev.Wp = nullptr;
+    if (L > 0) {  // layer-0 weights split into three bf16 planes, round-to-nearest-even at each step (host, exact)
         std::vector<uint16_t> planes((size_t)3 * H * H);
         auto bf16_rne = [](float x) -> uint16_t {
             uint32_t u;
@@ -1094,6 +1288,14 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
             planes[(size_t)2 * H * H + i] = lo;
         }
         m->dev.Wp = put(reinterpret_cast<const float*>(planes.data()), nWp);
+    }
+    m->dev.Wt = nullptr;
+    if (smooth && L > 0) {  // [l][in][out] for mlp_smooth's coalesced rows
+        std::vector<float> wt(nW);
+        for (int l = 0; l < L; ++l)
+            for (int o = 0; o < H; ++o)
+                for (int k = 0; k < H; ++k) wt[(size_t)l * H * H + (size_t)k * H + o] = d->W[(size_t)l * H * H + (size_t)o * H + k];
+        m->dev.Wt = put(wt.data(), nWt);
     }
     if (hipDeviceSynchronize() != hipSuccess) {
         set_error("nlot_mlp_create: copy failed");

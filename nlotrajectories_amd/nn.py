@@ -110,7 +110,7 @@ class SineLayer(nn.Module):
 
 
 class SIREN(nn.Module):
-    """core/nn_architectures.py:75-100 (kernel support: DESIGN.md §7, next)."""
+    """core/nn_architectures.py:75-100 (the SDF kernels take it as in_kind LINEAR + NLOT_ACT_SINE)."""
 
     def __init__(self, input_dim, hidden_dim, output_dim, num_layers=3, omega_0=30):
         super().__init__()
@@ -125,6 +125,13 @@ class SIREN(nn.Module):
         return self.output_layer(x)
 
 
+# activation codes <-> the reference's names (FourierMLP: nn_architectures.py:47-52; naive MLP: l4casadi)
+_FOURIER_ACT_NAMES = {_abi.ACT_RELU: "ReLU", _abi.ACT_TANH: "tanh", _abi.ACT_SIGMOID: "sigmoid",
+                      _abi.ACT_LEAKY_RELU: "leaky_relu"}
+_NAIVE_ACT_NAMES = {_abi.ACT_RELU: "ReLU", _abi.ACT_TANH: "Tanh", _abi.ACT_SIGMOID: "Sigmoid",
+                    _abi.ACT_LEAKY_RELU: "LeakyReLU"}
+
+
 @dataclass
 class MlpWeights:
     """Flat fp32 weights: h0 = phi(p @ A + b0); n_hidden x relu(W h + b); f = w_out . h + b_out."""
@@ -132,9 +139,10 @@ class MlpWeights:
     in_kind: int
     hidden: int
     n_hidden: int
-    fourier_scale: float
+    fourier_scale: float  # FourierFeatureLayer.scale; omega_0 for SIREN (act = ACT_SINE)
     b_out: float
     arrays: Dict[str, np.ndarray]
+    act: int = _abi.ACT_RELU  # hidden activation (and the input layer's, in_kind LINEAR)
 
     @property
     def flops_per_point_fwd(self) -> int:
@@ -151,14 +159,21 @@ class MlpWeights:
     def torch_module(self) -> nn.Module:
         """Equivalent torch module (fp32), for reference evaluation in tests / the numpy path."""
         H = self.hidden
-        if self.in_kind == _abi.MLP_IN_FOURIER:
-            m = FourierMLP(2, H, 1, num_layers=self.n_hidden + 2, scale=self.fourier_scale)
+        if self.act == _abi.ACT_SINE and self.in_kind != _abi.MLP_IN_FOURIER:
+            m = SIREN(2, H, 1, num_layers=self.n_hidden + 2, omega_0=self.fourier_scale)
+            sd = {"layers.0.linear.weight": self.arrays["A"].T, "layers.0.linear.bias": self.arrays["b0"]}
+            for l in range(self.n_hidden):
+                sd[f"layers.{l + 1}.linear.weight"] = self.arrays["W"][l]
+                sd[f"layers.{l + 1}.linear.bias"] = self.arrays["b"][l]
+        elif self.in_kind == _abi.MLP_IN_FOURIER:
+            m = FourierMLP(2, H, 1, num_layers=self.n_hidden + 2, scale=self.fourier_scale,
+                           activation_function=_FOURIER_ACT_NAMES[self.act])
             sd = {"fourier.weights": self.arrays["A"], "fourier.bias": self.arrays["b0"]}
             for l in range(self.n_hidden):
                 sd[f"layers.{l}.weight"] = self.arrays["W"][l]
                 sd[f"layers.{l}.bias"] = self.arrays["b"][l]
         else:
-            m = MultiLayerPerceptron(2, H, 1, self.n_hidden + 1, "ReLU")
+            m = MultiLayerPerceptron(2, H, 1, self.n_hidden + 1, _NAIVE_ACT_NAMES[self.act])
             sd = {"input_layer.weight": self.arrays["A"].T, "input_layer.bias": self.arrays["b0"]}
             for l in range(self.n_hidden):
                 sd[f"hidden_layers.{l}.weight"] = self.arrays["W"][l]
@@ -170,11 +185,24 @@ class MlpWeights:
 
     @staticmethod
     def from_module(model: nn.Module) -> "MlpWeights":
-        """Flatten a FourierMLP / MultiLayerPerceptron (ReLU) into kernel form."""
+        """Flatten a FourierMLP / MultiLayerPerceptron / SIREN into kernel form."""
         g = lambda t: t.detach().cpu().float().numpy().copy()
+        if isinstance(model, SIREN):
+            first, rest = model.layers[0], list(model.layers[1:])
+            H = first.linear.weight.shape[0]
+            if first.linear.bias is None or any(l.linear.bias is None for l in rest):
+                raise ValueError("SIREN layers without bias are not supported")
+            omegas = {float(l.omega_0) for l in model.layers}
+            if len(omegas) != 1:
+                raise ValueError("SIREN layers must share omega_0")
+            arrays = dict(A=g(first.linear.weight).T.copy(), b0=g(first.linear.bias),
+                          W=np.stack([g(l.linear.weight) for l in rest]) if rest else np.zeros((0, H, H), np.float32),
+                          b=np.stack([g(l.linear.bias) for l in rest]) if rest else np.zeros((0, H), np.float32),
+                          w_out=g(model.output_layer.weight)[0])
+            return MlpWeights(_abi.MLP_IN_LINEAR_RELU, H, len(rest), omegas.pop(),
+                              float(g(model.output_layer.bias)[0]), arrays, _abi.ACT_SINE)
         if isinstance(model, FourierMLP) or hasattr(model, "fourier"):
-            if getattr(model, "activation_name", "ReLU") != "ReLU":
-                raise ValueError("round-1 kernels support ReLU hidden layers")
+            act = {v: k for k, v in _FOURIER_ACT_NAMES.items()}[getattr(model, "activation_name", "ReLU")]
             H = model.fourier.weights.shape[1]
             Ws = [g(l.weight) for l in model.layers]
             bs = [g(l.bias) for l in model.layers]
@@ -183,10 +211,12 @@ class MlpWeights:
                           b=np.stack(bs) if bs else np.zeros((0, H), np.float32),
                           w_out=g(model.output_layer.weight)[0])
             return MlpWeights(_abi.MLP_IN_FOURIER, H, len(Ws), float(model.fourier.scale),
-                              float(g(model.output_layer.bias)[0]), arrays)
+                              float(g(model.output_layer.bias)[0]), arrays, act)
         if hasattr(model, "input_layer") and hasattr(model, "hidden_layers"):
-            if getattr(model, "activation", "ReLU") != "ReLU":
-                raise ValueError("the SDF kernels support ReLU hidden layers (DESIGN.md §7)")
+            name = getattr(model, "activation", "ReLU")
+            if name not in _NAIVE_ACT_NAMES.values() or name is None:
+                raise ValueError(f"unsupported activation {name!r} for the SDF kernels (DESIGN.md §7)")
+            act = {v: k for k, v in _NAIVE_ACT_NAMES.items()}[name]
             H = model.input_layer.weight.shape[0]
             Ws = [g(l.weight) for l in model.hidden_layers]
             bs = [g(l.bias) for l in model.hidden_layers]
@@ -194,20 +224,21 @@ class MlpWeights:
                           W=np.stack(Ws) if Ws else np.zeros((0, H, H), np.float32),
                           b=np.stack(bs) if bs else np.zeros((0, H), np.float32),
                           w_out=g(model.output_layer.weight)[0])
-            return MlpWeights(_abi.MLP_IN_LINEAR_RELU, H, len(Ws), 1.0, float(g(model.output_layer.bias)[0]), arrays)
+            return MlpWeights(_abi.MLP_IN_LINEAR_RELU, H, len(Ws), 1.0, float(g(model.output_layer.bias)[0]), arrays,
+                              act)
         raise TypeError(f"unsupported model type {type(model).__name__} (DESIGN.md §7)")
 
     def save(self, path) -> None:
         """Plain npz (no pickle): the arrays plus the scalar fields."""
         np.savez(path, in_kind=self.in_kind, hidden=self.hidden, n_hidden=self.n_hidden,
-                 fourier_scale=self.fourier_scale, b_out=self.b_out, **self.arrays)
+                 fourier_scale=self.fourier_scale, b_out=self.b_out, act=self.act, **self.arrays)
 
     @staticmethod
     def load(path) -> "MlpWeights":
         z = np.load(path, allow_pickle=False)
         arrays = {k: z[k].astype(np.float32) for k in ("A", "b0", "W", "b", "w_out")}
         return MlpWeights(int(z["in_kind"]), int(z["hidden"]), int(z["n_hidden"]), float(z["fourier_scale"]),
-                          float(z["b_out"]), arrays)
+                          float(z["b_out"]), arrays, int(z["act"]) if "act" in z.files else _abi.ACT_RELU)
 
     @staticmethod
     def artefact() -> "MlpWeights":

@@ -19,7 +19,7 @@ class DeviceMlp:
         self.weights = weights
         self._arrs = {k: np.ascontiguousarray(v, np.float32) for k, v in weights.arrays.items()}
         fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
-        d = _abi.NlotMlpDesc(in_kind=weights.in_kind, hidden=weights.hidden, n_hidden=weights.n_hidden, act=0,
+        d = _abi.NlotMlpDesc(in_kind=weights.in_kind, hidden=weights.hidden, n_hidden=weights.n_hidden, act=weights.act,
                              fourier_scale=weights.fourier_scale, b_out=weights.b_out)
         d.A, d.b0, d.W, d.b, d.w_out = (fp(self._arrs[k]) for k in ("A", "b0", "W", "b", "w_out"))
         h = lib().nlot_mlp_create(C.byref(d))

@@ -140,9 +140,79 @@ static jet jcompose2(double f, const double g[2], const double H[3] /*xx,xy,yy*/
 /* ============================================================================================ */
 /* out: [0]=f [1..2]=lam*grad [3..5]=lam*hess (xx,xy,yy).  lam scales the adjoint seed
  * (adj1 / jac_adj1, gen/nn_sdf.cpp:79-104); lam = 1 gives jac_nn_sdf.  want = 0: value only. */
+/* s, s', s'' of a smooth hidden activation (core/nn_architectures.py:47-52; SineLayer :8-26 with omega_0) */
+static void oracle_act3(int act, float omega, float z, float* s, float* d1, float* d2) {
+    switch (act) {
+        case NLOT_ACT_TANH: *s = tanhf(z); *d1 = 1.f - *s * *s; *d2 = -2.f * *s * *d1; break;
+        case NLOT_ACT_SIGMOID: *s = 1.f / (1.f + expf(-z)); *d1 = *s * (1.f - *s); *d2 = *d1 * (1.f - 2.f * *s); break;
+        case NLOT_ACT_LEAKY_RELU: *s = z > 0.f ? z : 0.01f * z; *d1 = z > 0.f ? 1.f : 0.01f; *d2 = 0.f; break;
+        case NLOT_ACT_SINE: {
+            const float u = omega * z;
+            *s = sinf(u); *d1 = omega * cosf(u); *d2 = -omega * omega * *s;
+            break;
+        }
+        default: *s = z > 0.f ? z : 0.f; *d1 = z > 0.f ? 1.f : 0.f; *d2 = 0.f;
+    }
+}
+
+/* Smooth nets: value, gradient and Hessian carried forward through every layer (the Hessian has a term
+ * from each activation), 6 components per hidden unit: a, a_x, a_y, a_xx, a_xy, a_yy. */
+static void oracle_mlp_point_smooth(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
+    enum { HM = 256 };
+    const int H = m->hidden;
+    float a[6][HM], z[6][HM];
+    for (int k = 0; k < H; ++k) {
+        const float ax = m->A[k], ay = m->A[H + k];
+        const float zz = fmaf(py, ay, px * ax) + m->b0[k];
+        float s, d1, d2;
+        if (m->in_kind == NLOT_MLP_IN_FOURIER) {
+            s = cosf(zz) * m->fourier_scale;
+            d1 = -m->fourier_scale * sinf(zz);
+            d2 = -m->fourier_scale * cosf(zz);
+        } else {
+            oracle_act3(m->act, m->fourier_scale, zz, &s, &d1, &d2);
+        }
+        a[0][k] = s;
+        a[1][k] = d1 * ax;
+        a[2][k] = d1 * ay;
+        a[3][k] = d2 * ax * ax;
+        a[4][k] = d2 * ax * ay;
+        a[5][k] = d2 * ay * ay;
+    }
+    for (int l = 0; l < m->n_hidden; ++l) {
+        const float* W = m->W + (size_t)l * H * H;
+        const float* b = m->b + (size_t)l * H;
+        for (int j = 0; j < H; ++j)
+            for (int c = 0; c < 6; ++c) {
+                float t = 0.f;
+                for (int k = 0; k < H; ++k) t = fmaf(W[(size_t)j * H + k], a[c][k], t);
+                z[c][j] = t;
+            }
+        for (int j = 0; j < H; ++j) {
+            float s, d1, d2;
+            oracle_act3(m->act, m->fourier_scale, z[0][j] + b[j], &s, &d1, &d2);
+            a[0][j] = s;
+            a[1][j] = d1 * z[1][j];
+            a[2][j] = d1 * z[2][j];
+            a[3][j] = d2 * z[1][j] * z[1][j] + d1 * z[3][j];
+            a[4][j] = d2 * z[1][j] * z[2][j] + d1 * z[4][j];
+            a[5][j] = d2 * z[2][j] * z[2][j] + d1 * z[5][j];
+        }
+    }
+    float o[6] = {0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < 6; ++c)
+        for (int j = 0; j < H; ++j) o[c] = fmaf(m->w_out[j], a[c][j], o[c]);
+    out[0] = o[0] + m->b_out;
+    for (int c = 1; c < 6; ++c) out[c] = want ? lam * o[c] : 0.f;
+}
+
 void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
     enum { HM = 256, LM = 8 };
     const int H = m->hidden;
+    if (m->act != NLOT_ACT_RELU) {
+        oracle_mlp_point_smooth(m, px, py, lam, want, out);
+        return;
+    }
     float z0[HM], h[HM], hn[HM];
     unsigned char mask[LM + 1][HM];
     for (int k = 0; k < H; ++k) {

@@ -67,7 +67,7 @@ class HostMlp:
     def __init__(self, w):
         self.w = {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in w.arrays.items()}
         d = _abi.NlotMlpDesc()
-        d.in_kind, d.hidden, d.n_hidden, d.act = w.in_kind, w.hidden, w.n_hidden, 0
+        d.in_kind, d.hidden, d.n_hidden, d.act = w.in_kind, w.hidden, w.n_hidden, getattr(w, "act", 0)
         d.fourier_scale, d.b_out = w.fourier_scale, w.b_out
         d.A, d.b0 = _fp(self.w["A"]), _fp(self.w["b0"])
         d.W, d.b = _fp(self.w["W"]), _fp(self.w["b"])
