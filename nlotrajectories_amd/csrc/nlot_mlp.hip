@@ -1335,10 +1335,6 @@ extern "C" int32_t nlot_sdf_mlp_eval(const NlotMlp* mlp, const float* pts, int64
         o.hyy = hess + 3;
         o.sh = 4;
     }
-    const bool full = grad || hess;
-    if (full && !grad) {  // kernel writes grad and hess together: route grad to a scratch-free path
-        set_error("nlot_sdf_mlp_eval: hess requires grad (jac_adj1 is evaluated with adj1)");
-        return NLOT_ERR_INVALID;
-    }
+    const bool full = grad || hess;  // every kernel skips a null grad or hess plane (jac_adj1 alone is allowed)
     return launch_mlp_strided(mlp->dev, pts, P, nullptr, 1, 0, lam, o, full, (hipStream_t)stream);
 }

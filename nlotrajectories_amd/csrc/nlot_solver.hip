@@ -744,7 +744,7 @@ struct RicWpe {
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
-                                            int mode) {
+                                            const int* __restrict__ nact, int mode) {
     using R = RicG<DYN>;
     using SV = Solver<DYN>;
     constexpr int NX = R::NX, NU = R::NU, NV = R::NV, NZ = R::NZ, NC = R::NC, NCOL = R::NCOL, NQE = R::NQE;
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     __shared__ __attribute__((aligned(16))) double ring[RING][NDMA][R::IPW][DW];  // DMA'd stage inputs
     const int grp = threadIdx.x / G, l = threadIdx.x % G, gb = grp * G;
     const int si = blockIdx.x * R::IPW + grp;
-    if (si >= n_active) return;
+    if (si >= n_active || si >= *nact) return;
     const int b = active[si];
     if ((int)SC(SC_RIC) != 1) return;
     typename R::Sh& sh = shg[grp];
@@ -1564,6 +1564,7 @@ template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
                                                const double* __restrict__ xg, int init_pass, int* cnt) {
+    if ((int)blockIdx.x >= cnt[2]) return;  // grid sized by a stale (larger) host count: steps run ahead of the host
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -1983,6 +1984,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* cnt, float* tp) {
+    if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -2451,6 +2453,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                                                const int* __restrict__ active, int* __restrict__ next,
                                                const double* __restrict__ x0, const double* __restrict__ xg, int* cnt,
                                                int* cnt_next, float* tp_next, const float* tval, int nspec_next) {
+    if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
@@ -2755,7 +2758,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             }
         }
     }
-    if (ph != PH_DONE && lane == 0) next[atomicAdd(&cnt[2], 1)] = b;
+    if (ph != PH_DONE && lane == 0) next[atomicAdd(&cnt_next[2], 1)] = b;  // the next step's active count
 }
 
 __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
@@ -2861,21 +2864,27 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     g_stats = NlotSolveStats{};
     hipLaunchKernelGGL(k_init_state, dim3(Bi), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit);
     NLOT_HIP_CHECK(hipGetLastError());
+    // Steps run ahead of the host: every kernel reads its step's active count on the device (cnt[2] of the
+    // step's counter set, written by the previous step's k_accept), and grids are sized by the host's last
+    // known count, an upper bound (the active set only shrinks).  The host waits once per KPIPE steps: it
+    // then learns the counts (the D2H copies of each step's counters land in a pinned ring) and whether any
+    // instance is still active; the at most KPIPE - 1 steps launched past the end exit at once.
+    constexpr int KPIPE = 8;
     // host-side resources released on every return path (NLOT_HIP_CHECK returns early)
     struct Res {
         int* hcnt = nullptr;
-        hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        hipEvent_t ev[KPIPE][8] = {};
         ~Res() {
-            for (auto& e : ev)
-                if (e) hipEventDestroy(e);
+            for (auto& r : ev)
+                for (auto& e : r)
+                    if (e) hipEventDestroy(e);
             if (hcnt) hipHostFree(hcnt);
         }
     } res;
-    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, 8 * sizeof(int), hipHostMallocDefault));
-    int* const hcnt = res.hcnt;
-    hipEvent_t* const ev = res.ev;
+    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, KPIPE * 16 * sizeof(int), hipHostMallocDefault));
     if (g_timing)
-        for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&ev[i]));
+        for (int k = 0; k < KPIPE; ++k)
+            for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
     MlpOut mo{}, mo_t[2] = {};
     MlpReuse reuse[2] = {};
     if (use_mlp) {
@@ -2906,12 +2915,19 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     }
     if (const char* e = getenv("NLOT_SPEC_THRESHOLD")) spec_threshold = atoi(e);
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
+    int kpipe = KPIPE;
+    if (const char* e = getenv("NLOT_PIPE")) kpipe = std::max(1, std::min(KPIPE, atoi(e)));
     const int max_steps = (o.max_iter + 2) * 64;
     int rc = NLOT_OK, n_active = Bi, cur = 0;
     NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 16 * sizeof(int), st));
+    res.hcnt[0] = Bi;  // step 0's active count (cnt[2] of counter set 0)
+    NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
+    NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
     for (int step = 0; step < max_steps && n_active > 0; ++step) {
         const int* act = ws.act[cur];
         int* nxt = ws.act[cur ^ 1];
+        const int kq = step % kpipe;
+        hipEvent_t* ev = res.ev[kq];
         // Point lists are appended to by the kernel that moves an instance into the phase needing them
         // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
         // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
@@ -2936,12 +2952,12 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         if (step == 0) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
             hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C);
             hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
-                               dP, dD, dW, act, n_active, (int)MODE_LSQ);
+                               dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ);
         }
         hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C);
         if (ev[6]) hipEventRecord(ev[6], st);
         hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st, dP, dD,
-                           dW, act, n_active, (int)MODE_NEWTON);
+                           dW, act, n_active, C + 2, (int)MODE_NEWTON);
         if (ev[6]) hipEventRecord(ev[7], st);
         hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
                            use_mlp ? ws.tpts[q] : nullptr);
@@ -2952,38 +2968,49 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
                                     mo_t[q], false, st);
             if (rc) break;
             if (ev[0]) hipEventRecord(ev[3], st);
-            g_stats.mlp_full_launches++;
-            g_stats.mlp_value_launches++;
         }
         // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
-        // starts at most one step late; the accepted alpha is the same either way)
+        // starts at most KPIPE steps late; the accepted alpha is the same either way)
         hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, C, Cn,
                            use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
-        NLOT_HIP_CHECK(hipMemcpyAsync(hcnt, C, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
-        NLOT_HIP_CHECK(hipStreamSynchronize(st));
-        g_stats.iterations = step + 1;
-        g_stats.mlp_points_full += (int64_t)hcnt[0] * P;
-        g_stats.mlp_points_value += (int64_t)hcnt[1] * P;
-        g_stats.mlp_points_full_reused += (int64_t)hcnt[3];
-        if (ev[0] && use_mlp) {
-            float a = 0, c = 0;
-            hipEventElapsedTime(&a, ev[0], ev[1]);
-            hipEventElapsedTime(&c, ev[2], ev[3]);
-            g_stats.mlp_full_ms += a;
-            g_stats.mlp_value_ms += c;
-        }
-        if (ev[4]) {
-            float a = 0, r = 0;
-            hipEventElapsedTime(&a, ev[4], ev[5]);
-            hipEventElapsedTime(&r, ev[6], ev[7]);
-            g_stats.iterate_ms += a;
-            g_stats.ric_ms += r;
-        }
-        g_stats.ric_launches++;
-        g_stats.ric_solves += hcnt[4];
-        n_active = hcnt[2];
+        // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
+        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 16 * kq, ws.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
         cur ^= 1;
+        if (kq != kpipe - 1) continue;
+        NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        for (int j = 0; j <= kq; ++j) {  // steps step - kq .. step
+            const int sj = step - kq + j, qj = sj & 1;
+            const int* hc = res.hcnt + 16 * j + 8 * qj;
+            const int next_active = res.hcnt[16 * j + 8 * (qj ^ 1) + 2];
+            g_stats.iterations = sj + 1;
+            if (use_mlp) {
+                g_stats.mlp_points_full += (int64_t)hc[0] * P;
+                g_stats.mlp_points_value += (int64_t)hc[1] * P;
+                g_stats.mlp_points_full_reused += (int64_t)hc[3];
+                g_stats.mlp_full_launches++;
+                g_stats.mlp_value_launches++;
+            }
+            g_stats.ric_launches++;
+            g_stats.ric_solves += hc[4];
+            hipEvent_t* e = res.ev[j];
+            if (e[0] && use_mlp) {
+                float a = 0, c = 0;
+                hipEventElapsedTime(&a, e[0], e[1]);
+                hipEventElapsedTime(&c, e[2], e[3]);
+                g_stats.mlp_full_ms += a;
+                g_stats.mlp_value_ms += c;
+            }
+            if (e[4]) {
+                float a = 0, r = 0;
+                hipEventElapsedTime(&a, e[4], e[5]);
+                hipEventElapsedTime(&r, e[6], e[7]);
+                g_stats.iterate_ms += a;
+                g_stats.ric_ms += r;
+            }
+            n_active = next_active;
+            if (n_active == 0) break;  // the later steps of this batch found nothing to do
+        }
     }
     if (rc) return rc;
     hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);

@@ -97,3 +97,22 @@ def test_l4casadi_wrapper_signature(artefact, golden):
     assert r["iters"][0].item() == 2
     with pytest.raises(ValueError):
         L4CasADi(model, generate_jac_jac=True)
+
+
+def test_hess_without_grad(artefact):
+    """nlot_sdf_mlp_eval with grad = NULL and hess != NULL (jac_adj1 alone) equals the full call's Hessian."""
+    import ctypes as C
+
+    from nlotrajectories_amd._lib import lib, stream_ptr
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    dm = DeviceMlp(artefact)
+    pts = torch.tensor(np.random.default_rng(5).uniform(-0.5, 1.5, (333, 2)), dtype=torch.float32, device="cuda")
+    lam = torch.linspace(-2, 2, 333, device="cuda")
+    v, _, h = sdf_mlp_eval(dm, pts, lam=lam)
+    val = torch.empty(333, device="cuda")
+    hess = torch.full((333, 2, 2), float("nan"), device="cuda")
+    p = lambda t: C.c_void_p(t.data_ptr())
+    assert lib().nlot_sdf_mlp_eval(dm.handle, p(pts), 333, p(val), None, p(lam), p(hess), stream_ptr()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(val, v) and torch.equal(hess, h)
