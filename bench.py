@@ -243,6 +243,8 @@ def main():
             "launches": agg["ric_launches"],
             "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
                     "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline",
+            "pmc_note": "profiles/r02/kric_sq.json (B = 16384): 25.5 % of wave cycles issue (15.4 % VALU), 50.4 % "
+                        "wait on s_waitcnt (LDS hand-offs, DMA ring), 24.0 % issue-stalled (fp64 VALU pipe)",
         }
         mlp_full = {
             "kernel": kname % "full" + ": SDF-MLP value + gradient + Hessian",
