@@ -102,9 +102,17 @@ def ric_bytes_per_solve(prob, nr=2):
 def main():
     a = parse()
     rank, local, world = rank_world()
+    # NLOT_DIST_BACKEND=gloo: a rehearsal of the multi-rank path with several ranks sharing the visible GPUs
+    # (local rank modulo the device count; CPU collectives); the driver's multi-GPU runs use RCCL ("nccl")
+    backend = os.environ.get("NLOT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     stress, b6 = a.workload == "stress", a.workload == "b6"
     if a.batch is None:

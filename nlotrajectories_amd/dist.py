@@ -26,19 +26,26 @@ def gather_solutions(r: dict, keys=("X", "U", "S", "cost", "status", "iters"), d
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return {k: r[k] for k in keys}
     world, me = dist.get_world_size(), dist.get_rank()
+    host = dist.get_backend() == "gloo"  # gloo gathers host tensors (the CPU tests and the 1-GPU rehearsal)
     out = {}
     for k in keys:
         t = r[k].contiguous()
+        if host:
+            t = t.cpu()
         parts = [torch.empty_like(t) for _ in range(world)] if me == dst else None
         dist.gather(t, parts, dst=dst)
         out[k] = torch.cat(parts, 0) if me == dst else None
     return out
 
 
+def _coll_device(device):
+    return "cpu" if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(x: float, device) -> float:
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -46,6 +53,6 @@ def max_over_ranks(x: float, device) -> float:
 def sum_over_ranks(n: int, device) -> int:
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return n
-    t = torch.tensor([n], dtype=torch.int64, device=device)
+    t = torch.tensor([n], dtype=torch.int64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
