@@ -64,6 +64,12 @@ def parse():
     ap.add_argument("--cpu-sample-1core", type=int, default=None,
                     help="instances for the single-core CPU baseline (default 8 metric / 2 stress)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--continuous", choices=["on", "off"], default="on",
+                    help="on (metric / stress): the timed steps' batches flow through the solver with --batch slots "
+                         "(continuous batching, NlotSolverOptions.max_active; up to 4 batches per solve call), so one "
+                         "batch's latency-bound tail overlaps the next batch's bulk; off: one solve call per batch")
+    ap.add_argument("--slots", type=int, default=None,
+                    help="continuous batching: instances in flight (default --batch)")
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
     return ap.parse_args()
@@ -149,7 +155,15 @@ def main():
 
     from nlotrajectories_amd.solver import workspace_bytes
 
-    ws = torch.empty(workspace_bytes(prob, a.batch), dtype=torch.uint8, device=dev)
+    # continuous batching: the K timed batches go through ceil(K / G) solve calls of G <= 4 batches each, with
+    # a.batch concurrent slots (the per-instance iterations are the same as in one call per batch)
+    cont = a.continuous == "on" and not b6 and a.steps > 1
+    G = min(a.steps, 4) if cont else 1
+    calls = [min(G, a.steps - i) for i in range(0, a.steps, G)] if cont else [1] * a.steps
+    ws = torch.empty(workspace_bytes(prob, a.batch * G), dtype=torch.uint8, device=dev)
+    opt_cont = _abi.gpu_options(**{f: getattr(opt, f) for f, _ in opt._fields_})
+    slots = a.slots or a.batch
+    opt_cont.max_active = slots
     agg_keys = ("mlp_full_ms", "mlp_full_launches", "mlp_points_full", "mlp_value_ms", "mlp_value_launches",
                 "mlp_points_value", "iterations", "iterate_ms", "mlp_points_full_reused", "ric_ms", "ric_launches",
                 "ric_solves")
@@ -158,12 +172,17 @@ def main():
 
     nstep = {"n": 0}
 
-    def step():
+    call_iter = {"i": 0}
+
+    def step(g=1):
         X_init = None
         if b6:  # benchmark 6's own initializer: RRT against the exact ring scene (YAML rrt settings), timed
             X_init, _ = rrt_initial_guess(prob, x0, xg, bounds=[[0.0, 0.0], [1.3, 1.3]], step_size=0.02,
                                           max_iter=5000, margin=0.01, seed=a.seed + 7919 * rank)
-        r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws, X_init=X_init)
+        if g > 1:  # g batches through a.batch slots
+            r = solve_batch(prob, x0.repeat(g, 1), xg.repeat(g, 1), mlp=mlp, options=opt_cont, workspace=ws)
+        else:
+            r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws, X_init=X_init)
         nstep["n"] += 1
         print(f"[bench] rank {rank} solve {nstep['n']} done", file=sys.stderr, flush=True)
         if timing["on"]:
@@ -179,9 +198,16 @@ def main():
         timing["on"] = not timing["on"]  # hipEvent timing inside the timed steps only
         set_timing(timing["on"])
 
-    results, elapsed = timed_loop(step, a.steps, a.warmup, world, sync, dev)
+    def timed_call():  # the timed region's i-th solve call (warm-up calls: one batch)
+        if not timing["on"]:
+            return step(1)
+        g = calls[call_iter["i"]]
+        call_iter["i"] += 1
+        return step(g)
+
+    results, elapsed = timed_loop(timed_call, len(calls), a.warmup, world, sync, dev)
     set_timing(False)
-    r = results[-1]
+    r = {k: v[:a.batch] for k, v in results[-1].items()}  # per-batch figures: the last call's first batch
     solved_total = sum_over_ranks(sum(int((x["status"] == 0).sum().item()) for x in results), dev)
     iters_solved = [x["iters"][x["status"] == 0].float().mean().item() for x in results if (x["status"] == 0).any()]
     status_counts = torch.bincount(r["status"].long(), minlength=len(_abi.STATUS_NAMES)).cpu().numpy().tolist()
@@ -325,6 +351,10 @@ def main():
                 "global_batch": B_all,
                 "knots": prob.N + 1,
                 "parallelism": f"instances sharded over {world} GPU(s); RCCL gather of solutions to rank 0",
+                "scheduling": (f"continuous batching: the {a.steps} timed batches of {a.batch} instances in "
+                               f"{len(calls)} solve call(s) of up to {G} batches through {slots} concurrent slots "
+                               "(NlotSolverOptions.max_active); each instance runs the same iterations as alone"
+                               if cont else "one solve call per batch"),
                 "solved_per_step_rank0": int((r["status"] == 0).sum().item()),
                 "status_counts_rank0": status_counts,
                 "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / a.batch for i, c in enumerate(status_counts)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 8
+#define NLOT_ABI_VERSION 9
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -147,7 +147,9 @@ typedef struct NlotSolverOptions {
     int32_t watchdog_shortened_iter_trigger; /* 10 (IPOPT default; 0 switches the watchdog off) */
     int32_t watchdog_trial_iter_max;         /* 3 */
     int32_t max_soft_resto_iters;            /* 10 */
-    int32_t pad_;
+    int32_t max_active;          /* solver scheduling, not an IPOPT option: 0 = all B instances from the start;
+                                    n > 0 = continuous batching, at most n instances in flight and the next ones
+                                    admitted (in index order) as others finish — per-instance results are the same */
     double kappa_soc;                        /* 0.99 */
     double tiny_step_tol;                    /* 10 eps = 2.22e-15 */
     double tiny_step_y_tol;                  /* 1e-2 */

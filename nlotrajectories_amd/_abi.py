@@ -48,7 +48,7 @@ class NlotSolverOptions(C.Structure):
         ("constr_viol_tol", C.c_double), ("compl_inf_tol", C.c_double),
         ("constr_mult_init_max", C.c_double), ("bound_push", C.c_double), ("bound_frac", C.c_double),
         ("max_soc", C.c_int32), ("resto", C.c_int32), ("watchdog_shortened_iter_trigger", C.c_int32),
-        ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32), ("pad_", C.c_int32),
+        ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32), ("max_active", C.c_int32),
         ("kappa_soc", C.c_double), ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
         ("soft_resto_pderror_reduction_factor", C.c_double), ("required_infeasibility_reduction", C.c_double),
         ("resto_penalty_parameter", C.c_double), ("resto_proximity_weight", C.c_double),

@@ -1453,6 +1453,14 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
     }
 }
 
+// continuous batching: instances first .. first + n - 1 join the active list of the next step (its count cnt[2])
+__global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, int* __restrict__ cnt, int first, int n) {
+    const int base = cnt[2];
+    for (int t = threadIdx.x; t < n; t += blockDim.x) act[base + t] = first + t;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[2] = base + n;
+}
+
 // number of step lengths of a later line-search round starting at alpha a: a, a/2, ... while >= alpha_min,
 // at most nspec (speculative backtracking: the same accepted alpha as sequential halving, because the
 // acceptance test of one candidate does not depend on the others; the first round tries alpha_max alone)
@@ -2918,9 +2926,18 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     int kpipe = KPIPE;
     if (const char* e = getenv("NLOT_PIPE")) kpipe = std::max(1, std::min(KPIPE, atoi(e)));
     const int max_steps = (o.max_iter + 2) * 64;
-    int rc = NLOT_OK, n_active = Bi, cur = 0;
+    // Continuous batching (o.max_active = capacity < B): the first `capacity` instances start; whenever a host
+    // synchronisation finds at least capacity / 32 slots free, the next instances (index order) join the active
+    // list and run their INIT step (corners, slack push, least-squares multipliers) in the next step.  Every
+    // instance runs the same iteration sequence whenever it starts, so the results do not depend on capacity;
+    // what changes is that the latency-bound tail of one group overlaps the bulk of the next.
+    const int capacity = o.max_active > 0 && o.max_active < Bi ? o.max_active : Bi;
+    const int min_admit = std::max(1, capacity / 32);
+    int next_admit = capacity;
+    bool init_step = true;  // this step runs the INIT pass (step 0, and the step after an admission)
+    int rc = NLOT_OK, n_active = capacity, cur = 0;
     NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 16 * sizeof(int), st));
-    res.hcnt[0] = Bi;  // step 0's active count (cnt[2] of counter set 0)
+    res.hcnt[0] = capacity;  // step 0's active count (cnt[2] of counter set 0)
     NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
     for (int step = 0; step < max_steps && n_active > 0; ++step) {
@@ -2939,7 +2956,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
         if (use_mlp) {
-            if (step == 0) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
+            if (init_step) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
             if (ev[0]) hipEventRecord(ev[0], st);
             // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
             MlpReuse ru = reuse[q ^ 1];  // the previous step's trial list
@@ -2949,7 +2966,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             if (ev[0]) hipEventRecord(ev[1], st);
         }
         if (ev[4]) hipEventRecord(ev[4], st);
-        if (step == 0) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
+        if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
             hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C);
             hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
                                dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ);
@@ -2977,6 +2994,7 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
         NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 16 * kq, ws.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
         cur ^= 1;
+        init_step = false;
         if (kq != kpipe - 1) continue;
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         for (int j = 0; j <= kq; ++j) {  // steps step - kq .. step
@@ -3010,6 +3028,16 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             }
             n_active = next_active;
             if (n_active == 0) break;  // the later steps of this batch found nothing to do
+        }
+        if (next_admit < Bi && (capacity - n_active >= min_admit || n_active == 0)) {
+            // append instances next_admit .. next_admit + n_new - 1 to the next step's active list and count
+            const int n_new = std::min(capacity - n_active, Bi - next_admit);
+            hipLaunchKernelGGL(k_admit, dim3(1), dim3(1024), 0, st, ws.act[cur], ws.cnt + 8 * ((step + 1) & 1), next_admit,
+                               n_new);
+            NLOT_HIP_CHECK(hipGetLastError());
+            next_admit += n_new;
+            n_active += n_new;
+            init_step = true;
         }
     }
     if (rc) return rc;

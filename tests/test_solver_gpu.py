@@ -233,3 +233,32 @@ def test_solution_satisfies_constraints():
             F = X[b, k] + p.dt * O.dynamics(p, X[b, k], U[b, k])
             assert np.abs(X[b, k + 1] - F).max() < 1e-4
         assert (U[b] >= -2 - 1e-9).all() and (U[b] <= 2 + 1e-9).all() and (S[b] >= 0).all()
+
+
+@pytest.mark.parametrize("case", ["metric", "b2"])
+def test_continuous_batching_same_results(artefact, case):
+    """NlotSolverOptions.max_active < B (continuous batching: at most max_active instances in flight, the next
+    ones admitted as others finish) gives every instance the same status, iterations, cost and trajectory as
+    the all-at-once solve, bitwise: an instance's arithmetic does not depend on which others share its steps."""
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import BENCHMARKS, METRIC_PROBLEM
+    from nlotrajectories_amd.sampling import sample_start_goal
+    from nlotrajectories_amd.solver import solve_batch
+
+    if case == "metric":
+        p, mlp = METRIC_PROBLEM, DeviceMlp(artefact)
+        tm = artefact.torch_module()
+        sdf = lambda P: tm(torch.tensor(np.asarray(P), dtype=torch.float32)).detach().numpy()[:, 0]
+        x0, xg = sample_start_goal(p, 160, seed=3, sdf=sdf)
+        slots = 40
+    else:
+        p, mlp = BENCHMARKS["b2"]["problem"], None
+        sdf = lambda P: np.sqrt(((np.asarray(P) - 0.5) ** 2).sum(1)) - 0.25
+        x0, xg = sample_start_goal(p, 48, seed=4, sdf=sdf, lo=(0, 0), hi=(1, 1))
+        slots = 7
+    ra = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options())
+    rc = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options(max_active=slots))
+    print(case, "statuses", np.bincount(ra["status"].cpu().numpy(), minlength=7).tolist())
+    for k in ("status", "iters", "cost", "X", "U", "S"):
+        assert torch.equal(ra[k], rc[k]), k
