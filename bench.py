@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark: solved trajectories/sec for the 50-knot unicycle + learned-SDF workload (BASELINE.json).
 
-One step = one batched solve (nlot_solve_batch) of B synthetic start/goal instances per GPU of the
-metric NLP: benchmark_3's body/bounds/slack penalty, N = 50 knots, learned SDF = the reference
-artefact FourierMLP (2-128-128-1, scale 10), linear initial guess.  Instances are independent, so each
-rank solves its own seeded batch (weak scaling) and the solved trajectories are gathered to rank 0
-over RCCL at the end of every step (the only collective).
+One step = one batch of B synthetic start/goal instances per GPU of the metric NLP solved to completion:
+benchmark_3's body/bounds/slack penalty, N = 50 knots, learned SDF = the reference artefact FourierMLP
+(2-128-128-1, scale 10), linear initial guess.  By default (--continuous on) the K timed batches stream
+through the solver with B instances in flight (continuous batching, NlotSolverOptions.max_active; up to 4
+batches per nlot_solve_batch call), so one batch's latency-bound tail overlaps the next batch's bulk; every
+instance's result is the same as in a call of its own.  Instances are independent, so each rank solves its
+own seeded batches (weak scaling) and the solved trajectories are gathered to rank 0 over RCCL after every
+solve call (the only collective).
 
 value = solved instances of all ranks in the timed steps / max-over-ranks wall time of those steps.
 
@@ -50,7 +53,7 @@ PEAK_F32_MFMA_NOTE = "dense f32-input MFMA peak (v_mfma_f32_16x16x4_f32; exact f
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["metric", "stress", "b6"], default="metric",
                     help="metric = BASELINE.json's headline config; stress = configs[4] (2-256x4-1 SDF MLP, N = 256); "
