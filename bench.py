@@ -379,7 +379,7 @@ def main():
 def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu_iters_per_solved=None):
     """The oracle (C restatement, OpenMP over instances) on bounded samples of the same workload: the first
     n_all instances of rank 0's batch on `threads` host threads, and the first n_one on one thread, in chunks
-    of `threads` instances with a progress line after each.
+    of 4 x `threads` instances with a progress line after each.
 
     iter_cap (the stress workload, where one oracle iteration costs ~1 s of fp32 MLP work on a core): the
     sample runs at most iter_cap iterations per instance, and the value is an ESTIMATE = 1 / (measured
@@ -400,13 +400,16 @@ def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu
         run_opt.max_iter = iter_cap
 
     def run(n, th):
+        # chunks of 4 instances per thread (OpenMP dynamic schedule inside a chunk): a progress line every chunk,
+        # and a max_iter straggler holds up one chunk of 4 x th instances rather than one of th
         t = time.perf_counter()
         st, its = [], []
-        for c0 in range(0, n, th):
-            r = O.solve_batch(prob, x0[c0:min(n, c0 + th)], xg[c0:min(n, c0 + th)], hm, opt=run_opt, threads=th)
+        ch = 4 * th
+        for c0 in range(0, n, ch):
+            r = O.solve_batch(prob, x0[c0:min(n, c0 + ch)], xg[c0:min(n, c0 + ch)], hm, opt=run_opt, threads=th)
             st.append(r["status"])
             its.append(r["iters"])
-            print(f"[bench] cpu baseline: {min(n, c0 + th)}/{n} instances on {th} thread(s), "
+            print(f"[bench] cpu baseline: {min(n, c0 + ch)}/{n} instances on {th} thread(s), "
                   f"{time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
         st, its = np.concatenate(st), np.concatenate(its)
         return int((st == 0).sum()), time.perf_counter() - t, np.bincount(st, minlength=7).tolist(), int(its.sum())
