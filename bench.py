@@ -78,6 +78,16 @@ def parse():
     return ap.parse_args()
 
 
+def batch_calls(steps, continuous, per_call=4):
+    """(G, calls): the timed batches per solve call.  Continuous batching streams up to `per_call` batches
+    through one call (the workspace grows with them: 19 GiB per 65,536 metric instances); otherwise one call
+    per batch.  sum(calls) == steps."""
+    if not continuous:
+        return 1, [1] * steps
+    G = max(1, min(steps, per_call))
+    return G, [min(G, steps - i) for i in range(0, steps, G)]
+
+
 def timed_loop(step, steps, warmup, world, sync, device):
     """W untimed warm-up steps, then EXACTLY `steps` timed steps bracketed by a barrier + device sync on
     both sides; returns (per-step results, max-over-ranks elapsed seconds)."""
@@ -161,8 +171,7 @@ def main():
     # continuous batching: the K timed batches go through ceil(K / G) solve calls of G <= 4 batches each, with
     # a.batch concurrent slots (the per-instance iterations are the same as in one call per batch)
     cont = a.continuous == "on" and not b6 and a.steps > 1
-    G = min(a.steps, 4) if cont else 1
-    calls = [min(G, a.steps - i) for i in range(0, a.steps, G)] if cont else [1] * a.steps
+    G, calls = batch_calls(a.steps, cont)
     ws = torch.empty(workspace_bytes(prob, a.batch * G), dtype=torch.uint8, device=dev)
     opt_cont = _abi.gpu_options(**{f: getattr(opt, f) for f, _ in opt._fields_})
     slots = a.slots or a.batch

@@ -112,3 +112,17 @@ def test_bench_timed_loop_two_ranks(tmp_path):
     assert r0["calls"] == r1["calls"] == 3  # 1 warm-up + 2 timed
     assert r0["elapsed"] == r1["elapsed"] >= 0.6  # max over ranks: rank 1 sleeps 0.3 s per timed step
     assert r0["solved"] == r1["solved"]
+
+
+def test_bench_batch_calls():
+    """bench.batch_calls: the timed batches per solve call under continuous batching (<= 4 per call, every
+    timed batch exactly once) and one call per batch otherwise."""
+    import bench
+
+    assert bench.batch_calls(4, True) == (4, [4])
+    assert bench.batch_calls(2, True) == (2, [2])
+    assert bench.batch_calls(10, True) == (4, [4, 4, 2])
+    assert bench.batch_calls(3, False) == (1, [1, 1, 1])
+    for k in range(1, 13):
+        G, calls = bench.batch_calls(k, True)
+        assert sum(calls) == k and max(calls) <= G <= 4
