@@ -32,7 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from nlotrajectories_amd import _abi  # noqa: E402
-from nlotrajectories_amd.dist import gather_solutions, max_over_ranks, rank_world, sum_over_ranks  # noqa: E402
+from nlotrajectories_amd.dist import (gather_rank_rows, gather_solutions, max_over_ranks, rank_world,  # noqa: E402
+                                      sum_over_ranks)
 from nlotrajectories_amd.nn import MlpWeights  # noqa: E402
 from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval  # noqa: E402
 from nlotrajectories_amd.rrt import rrt_initial_guess  # noqa: E402
@@ -66,7 +67,8 @@ def parse():
                     help="instances for the CPU baseline on all threads (0 = skip; default 256 metric / 32 stress)")
     ap.add_argument("--cpu-sample-1core", type=int, default=None,
                     help="instances for the single-core CPU baseline (default 8 metric / 2 stress)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU-baseline threads (default: the host's CPU share: min(affinity, cgroup cpu.max quota))")
     ap.add_argument("--continuous", choices=["on", "off"], default="on",
                     help="on (metric / stress): the timed steps' batches flow through the solver with --batch slots "
                          "(continuous batching, NlotSolverOptions.max_active; up to 4 batches per solve call), so one "
@@ -139,7 +141,7 @@ def main():
     if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
         a.cpu_sample = 16 if stress else 32 if b6 else 256
     if a.cpu_sample_1core is None:
-        a.cpu_sample_1core = 1 if stress else 2 if b6 else 8
+        a.cpu_sample_1core = 1 if stress else 2 if b6 else 16
     prob = STRESS_PROBLEM if stress else B6_PROBLEM if b6 else METRIC_PROBLEM
     if b6:
         wpath = os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")
@@ -153,16 +155,19 @@ def main():
         v, _, _ = sdf_mlp_eval(mlp, torch.as_tensor(pts, dtype=torch.float32, device=dev), derivatives=False)
         return v.cpu().numpy()
 
-    if b6:  # benchmark 6's start / goal, xy +- U[-0.05, 0.05]^2 (seeded per rank)
-        rng = np.random.default_rng(a.seed + 1000003 * rank)
-        x0 = np.repeat(np.array([BENCHMARKS["b6"]["start"]], float), a.batch, 0)
-        xg = np.repeat(np.array([BENCHMARKS["b6"]["goal"]], float), a.batch, 0)
-        x0[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
-        xg[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
-    else:  # start/goal uniform in [-0.3, 1.3]^2, all corners sdf >= 0.02
-        x0, xg = sample_start_goal(prob, a.batch, seed=a.seed, sdf=sdf_gpu, rank=rank)
-    x0 = torch.tensor(x0, dtype=torch.float64, device=dev)
-    xg = torch.tensor(xg, dtype=torch.float64, device=dev)
+    def draw(k):  # batch k (warm-up batches first, then the timed ones): a distinct seeded draw per batch and rank
+        if b6:  # benchmark 6's start / goal, xy +- U[-0.05, 0.05]^2
+            rng = np.random.default_rng(a.seed + k + 1000003 * rank)
+            x0 = np.repeat(np.array([BENCHMARKS["b6"]["start"]], float), a.batch, 0)
+            xg = np.repeat(np.array([BENCHMARKS["b6"]["goal"]], float), a.batch, 0)
+            x0[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
+            xg[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
+        else:  # start/goal uniform in [-0.3, 1.3]^2, all corners sdf >= 0.02
+            x0, xg = sample_start_goal(prob, a.batch, seed=a.seed + k, sdf=sdf_gpu, rank=rank)
+        return (torch.tensor(x0, dtype=torch.float64, device=dev), torch.tensor(xg, dtype=torch.float64, device=dev))
+
+    batches = [draw(k) for k in range(a.warmup + a.steps)]  # resident in HBM before the timed region
+    x0, xg = batches[a.warmup]  # the first timed batch (CPU baseline sample)
     opt = _abi.gpu_options() if a.mu_strategy == "adaptive" else \
         _abi.gpu_options(mu_strategy=0, barrier_tol_factor=10.0)
 
@@ -185,16 +190,23 @@ def main():
     nstep = {"n": 0}
 
     call_iter = {"i": 0}
+    t_solve = {"s": 0.0}  # this rank's own solve-call time inside the timed region (straggler balance)
 
-    def step(g=1):
+    def step(first, g=1):
         X_init = None
+        bx0 = torch.cat([batches[first + i][0] for i in range(g)])
+        bxg = torch.cat([batches[first + i][1] for i in range(g)])
         if b6:  # benchmark 6's own initializer: RRT against the exact ring scene (YAML rrt settings), timed
-            X_init, _ = rrt_initial_guess(prob, x0, xg, bounds=[[0.0, 0.0], [1.3, 1.3]], step_size=0.02,
-                                          max_iter=5000, margin=0.01, seed=a.seed + 7919 * rank)
+            X_init, _ = rrt_initial_guess(prob, bx0, bxg, bounds=[[0.0, 0.0], [1.3, 1.3]], step_size=0.02,
+                                          max_iter=5000, margin=0.01, seed=a.seed + first + 7919 * rank)
+        t0 = time.perf_counter()
         if g > 1:  # g batches through a.batch slots
-            r = solve_batch(prob, x0.repeat(g, 1), xg.repeat(g, 1), mlp=mlp, options=opt_cont, workspace=ws)
+            r = solve_batch(prob, bx0, bxg, mlp=mlp, options=opt_cont, workspace=ws)
         else:
-            r = solve_batch(prob, x0, xg, mlp=mlp, options=opt, workspace=ws, X_init=X_init)
+            r = solve_batch(prob, bx0, bxg, mlp=mlp, options=opt, workspace=ws, X_init=X_init)
+        if timing["on"]:
+            torch.cuda.synchronize()
+            t_solve["s"] += time.perf_counter() - t0
         nstep["n"] += 1
         print(f"[bench] rank {rank} solve {nstep['n']} done", file=sys.stderr, flush=True)
         if timing["on"]:
@@ -210,19 +222,27 @@ def main():
         timing["on"] = not timing["on"]  # hipEvent timing inside the timed steps only
         set_timing(timing["on"])
 
-    def timed_call():  # the timed region's i-th solve call (warm-up calls: one batch)
+    warm_i = {"i": 0}
+
+    def timed_call():  # the timed region's i-th solve call (warm-up calls: one batch each)
         if not timing["on"]:
-            return step(1)
-        g = calls[call_iter["i"]]
+            warm_i["i"] += 1
+            return step(warm_i["i"] - 1, 1)
+        i = call_iter["i"]
+        g = calls[i]
         call_iter["i"] += 1
-        return step(g)
+        return step(a.warmup + sum(calls[:i]), g)
 
     results, elapsed = timed_loop(timed_call, len(calls), a.warmup, world, sync, dev)
     set_timing(False)
-    r = {k: v[:a.batch] for k, v in results[-1].items()}  # per-batch figures: the last call's first batch
-    solved_total = sum_over_ranks(sum(int((x["status"] == 0).sum().item()) for x in results), dev)
+    st_all = torch.cat([x["status"] for x in results]).long()
+    it_all = torch.cat([x["iters"] for x in results]).double()
+    solved_total = sum_over_ranks(int((st_all == 0).sum().item()), dev)
     iters_solved = [x["iters"][x["status"] == 0].float().mean().item() for x in results if (x["status"] == 0).any()]
-    status_counts = torch.bincount(r["status"].long(), minlength=len(_abi.STATUS_NAMES)).cpu().numpy().tolist()
+    # pooled over the K distinct timed batches of rank 0
+    status_counts = torch.bincount(st_all, minlength=len(_abi.STATUS_NAMES)).cpu().numpy().tolist()
+    q = torch.quantile(it_all, torch.tensor([0.5, 0.99], dtype=torch.float64, device=it_all.device)).cpu().tolist()
+    rank_rows = gather_rank_rows([rank, t_solve["s"], q[0], q[1], float(it_all.max().item())] + status_counts, dev)
 
     # rooflines.  Dominant kernel by device time: k_ric (the Newton solve, latency/occupancy-bound fp64 with
     # ~2.8 KB of stage data per knot): HBM roofline on its algorithmic bytes.  The two SDF-MLP launches:
@@ -367,10 +387,19 @@ def main():
                                f"{len(calls)} solve call(s) of up to {G} batches through {slots} concurrent slots "
                                "(NlotSolverOptions.max_active); each instance runs the same iterations as alone"
                                if cont else "one solve call per batch"),
-                "solved_per_step_rank0": int((r["status"] == 0).sum().item()),
+                "batches": f"{a.steps} distinct seeded draws per rank (seed + k, rank offset), resident in HBM "
+                           "before the timed region",
+                "solved_per_step_rank0": (int((st_all == 0).sum().item())) / max(a.steps, 1),
                 "status_counts_rank0": status_counts,
-                "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / a.batch for i, c in enumerate(status_counts)
-                                       if i in _abi.STATUS_NAMES},
+                "status_counts_note": "summed over rank 0's timed batches",
+                "status_rates_rank0": {_abi.STATUS_NAMES[i]: c / max(len(st_all), 1) for i, c in
+                                       enumerate(status_counts) if i in _abi.STATUS_NAMES},
+                "ipopt_safeguards": ("second-order correction (max_soc 4), watchdog, tiny step, filter reset, soft "
+                                     "restoration and the feasibility restoration phase (MinC_1Nrm) all on: IPOPT's "
+                                     "defaults (runner.py:113-125)" if opt.resto else
+                                     "restoration phase OFF: line-search failures end as line_search_failed"),
+                "per_rank": [{"rank": int(rw[0]), "solve_s": rw[1], "iters_p50": rw[2], "iters_p99": rw[3],
+                              "iters_max": int(rw[4]), "status_counts": [int(c) for c in rw[5:]]} for rw in rank_rows],
                 "mean_iters_solved": float(np.mean(iters_solved)) if iters_solved else 0.0,
                 "lockstep_global_steps": agg["iterations"] // max(a.steps, 1),
                 "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
@@ -385,10 +414,34 @@ def main():
         dist.destroy_process_group()
 
 
+def host_cpu_share():
+    """(cores, note): the CPUs this process may use: min(scheduler affinity, cgroup v2 cpu.max quota, rounded down),
+    read at run time (the GPU box's affinity lists the whole machine while its cgroup grants a share)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    quota, note = None, f"os.cpu_count() = {os.cpu_count()}, affinity = {avail}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(per)))
+            note += f", cgroup cpu.max = {q} / {per} = {float(q) / float(per):.1f} CPUs"
+        else:
+            note += ", cgroup cpu.max = max"
+    except (OSError, ValueError):
+        note += ", no cgroup v2 cpu.max"
+    cores = min(avail, quota) if quota else avail
+    return cores, note
+
+
 def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu_iters_per_solved=None):
-    """The oracle (C restatement, OpenMP over instances) on bounded samples of the same workload: the first
-    n_all instances of rank 0's batch on `threads` host threads, and the first n_one on one thread, in chunks
-    of 4 x `threads` instances with a progress line after each.
+    """The oracle (C restatement) on bounded samples of the same workload: the first n_all instances of rank 0's
+    first timed batch in ONE OpenMP call (dynamic schedule, one instance per thread at a time, so a long-running
+    instance holds one thread, not a chunk), on the host's CPU share (host_cpu_share) or `threads`; and the first
+    n_one of them on one thread.  Parallel efficiency is compared on instance-iterations per second (the two samples
+    differ in status mix).
 
     iter_cap (the stress workload, where one oracle iteration costs ~1 s of fp32 MLP work on a core): the
     sample runs at most iter_cap iterations per instance, and the value is an ESTIMATE = 1 / (measured
@@ -398,50 +451,44 @@ def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu
         import oracle as O
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        avail = os.cpu_count() or 1
-    threads = max(1, min(threads, avail))
+    share, host = host_cpu_share()
+    threads = max(1, min(threads, share)) if threads else share
     hm = O.HostMlp(w)
     run_opt = type(opt).from_buffer_copy(opt)
     if iter_cap is not None:
         run_opt.max_iter = iter_cap
 
     def run(n, th):
-        # chunks of 4 instances per thread (OpenMP dynamic schedule inside a chunk): a progress line every chunk,
-        # and a max_iter straggler holds up one chunk of 4 x th instances rather than one of th
         t = time.perf_counter()
-        st, its = [], []
-        ch = 4 * th
-        for c0 in range(0, n, ch):
-            r = O.solve_batch(prob, x0[c0:min(n, c0 + ch)], xg[c0:min(n, c0 + ch)], hm, opt=run_opt, threads=th)
-            st.append(r["status"])
-            its.append(r["iters"])
-            print(f"[bench] cpu baseline: {min(n, c0 + ch)}/{n} instances on {th} thread(s), "
-                  f"{time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
-        st, its = np.concatenate(st), np.concatenate(its)
-        return int((st == 0).sum()), time.perf_counter() - t, np.bincount(st, minlength=7).tolist(), int(its.sum())
+        r = O.solve_batch(prob, x0[:n], xg[:n], hm, opt=run_opt, threads=th)
+        dt = time.perf_counter() - t
+        st, its = r["status"], r["iters"]
+        print(f"[bench] cpu baseline: {n} instances on {th} thread(s), {dt:.1f} s", file=sys.stderr, flush=True)
+        return int((st == 0).sum()), dt, np.bincount(st, minlength=7).tolist(), int(its.sum())
 
-    host = (f"(host: os.cpu_count() = {os.cpu_count()}, affinity = {avail} CPUs; the box's CPU share is 16)")
     ns, dt, sc, it = run(n_all, threads)
+    ips = it / dt  # instance-iterations per second
     if iter_cap is None:
         out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
-               "sample": f"first {n_all} instances of rank 0's seeded batch: {ns} solved (status counts {sc}) in "
-                         f"{dt:.1f} s on {threads} OpenMP threads {host}"}
+               "sample": f"first {n_all} instances of rank 0's first timed batch: {ns} solved (status counts {sc}), "
+                         f"{it} instance-iterations in {dt:.1f} s on {threads} OpenMP threads (host: {host})"}
     else:
         per_it = dt / max(it, 1)
         out = {"value": 1.0 / (per_it * gpu_iters_per_solved), "unit": "trajectories/s", "cores": threads,
                "kind": "port", "estimate": True,
-               "sample": f"first {n_all} instances of rank 0's seeded batch, at most {iter_cap} iterations each: "
-                         f"{it} instance-iterations in {dt:.1f} s on {threads} OpenMP threads {host} = "
+               "sample": f"first {n_all} instances of rank 0's first timed batch, at most {iter_cap} iterations each: "
+                         f"{it} instance-iterations in {dt:.1f} s on {threads} OpenMP threads (host: {host}) = "
                          f"{per_it * 1e3:.1f} ms per instance-iteration; value = 1 / (that x the GPU run's "
                          f"{gpu_iters_per_solved:.1f} iterations per solved instance)"}
     if n_one > 0:
-        ns1, dt1, _, it1 = run(n_one, 1)
+        ns1, dt1, sc1, it1 = run(n_one, 1)
+        ips1 = it1 / dt1
+        out["parallel_efficiency"] = ips / (threads * ips1)
+        out["efficiency_note"] = (f"instance-iterations/s: {ips:.1f} on {threads} threads vs {ips1:.2f} on 1 thread")
         if iter_cap is None:
             out["single_core"] = {"value": ns1 / dt1, "cores": 1,
-                                  "sample": f"first {n_one} instances: {ns1} solved in {dt1:.1f} s on 1 thread"}
+                                  "sample": f"first {n_one} instances: {ns1} solved (status counts {sc1}), {it1} "
+                                            f"instance-iterations in {dt1:.1f} s on 1 thread"}
         else:
             out["single_core"] = {"value": 1.0 / (dt1 / max(it1, 1) * gpu_iters_per_solved), "cores": 1,
                                   "estimate": True,

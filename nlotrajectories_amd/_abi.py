@@ -98,12 +98,14 @@ def default_options(**kw) -> NlotSolverOptions:
 
 
 def gpu_options(**kw) -> NlotSolverOptions:
-    """The IPOPT settings the GPU path runs: the defaults above (second-order corrections, watchdog, tiny-step
-    test) without the feasibility restoration phase and the soft restoration, which only the CPU oracle
-    implements: where IPOPT would restore, the GPU ends the instance with NLOT_LS_FAILED."""
-    base = dict(resto=0, soft_resto_pderror_reduction_factor=0.0)
-    base.update(kw)
-    return default_options(**base)
+    """The IPOPT settings the GPU path runs: since round 3 exactly default_options() (second-order corrections,
+    watchdog, tiny-step test, soft restoration and the feasibility restoration phase).  Kept as a
+    name for callers; NO_RESTO gives the round-2 behaviour (line-search failure ends an instance)."""
+    return default_options(**kw)
+
+
+# restoration switched off: an instance whose line search fails ends with NLOT_LS_FAILED (round-2 GPU behaviour)
+NO_RESTO = dict(resto=0, soft_resto_pderror_reduction_factor=0.0)
 
 
 class NlotRrtOptions(C.Structure):

@@ -37,7 +37,12 @@
 
 namespace nlot {
 
-enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4 };
+// PH_SOFT1 / PH_SOFT2: IPOPT's soft restoration step (BacktrackingLineSearch::TrySoftRestoStep) — the damped
+// step's filter test on a value launch, then (not filter-acceptable) the primal-dual error at the tentatively
+// accepted point on a full launch.  PH_RINIT: first step of a feasibility restoration phase (its point's full
+// evaluation, then MinC_1NrmRestorationPhase's initialisation); while SC_RESTO = 1 the EVAL / LS phases belong to
+// the restoration problem (k_resto_a / k_ric<DYN, true> / k_resto_b / k_resto_ls).
+enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4, PH_SOFT1 = 5, PH_SOFT2 = 6, PH_RINIT = 7 };
 
 // Minimum waves per SIMD the per-instance kernels are compiled for (register budget 512 / w per lane),
 // and the depth of k_ric's stage ring (its LDS per wavefront sets k_ric's occupancy).  These kernels wait
@@ -80,6 +85,13 @@ enum Scal {
     // IPOPT's filter reset heuristic: last rejection of this line search was by the filter, successive such
     // iterations, resets done
     SC_LASTREJF, SC_NFREJ, SC_NFRES,
+    // soft restoration: active, iterations, primal-dual error at the current point and the mu it was taken at
+    SC_INSOFT, SC_SOFTCNT, SC_PDC, SC_MUPD,
+    // feasibility restoration (MinC_1Nrm): active, first iteration, the original problem's mu / tau / last
+    // delta_w, theta_R and phi_R at the restoration's start, rho, zeta, the restoration's theta_max / theta_min
+    // and filter entries, restoration phases started (statistics)
+    SC_RESTO, SC_RFIRST, SC_RMUO, SC_RTAUO, SC_RDWO, SC_THR, SC_PHR, SC_RHO, SC_ZETA, SC_RTHMAX, SC_RTHMIN,
+    SC_RNFILT, SC_NRESTO,
     SC_COUNT
 };
 constexpr int FILT_MAX = 64;
@@ -137,6 +149,10 @@ __host__ __device__ constexpr int it_len(int N, int nx, int nu, int M) {
     return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + 8;
 }
 
+// restoration rows (oracle Sol::rp ...): [initial state nx][dynamics N nx][terminal nc][inequalities (N+1) M],
+// allocated with the terminal block padded to 8
+__host__ __device__ constexpr int ne_len(int N, int nx, int M) { return nx + N * nx + 8 + (N + 1) * M; }
+
 // instance-major arrays: (name, per-instance length)
 #define NLOT_WS_ARRAYS(X_)                                                                             \
     X_(X, (N + 1) * nx) X_(U, N * nu) X_(S, N + 1) X_(T, (N + 1) * M) X_(yi, nx) X_(yk, N * nx) X_(yt, 8) \
@@ -149,7 +165,9 @@ __host__ __device__ constexpr int it_len(int N, int nx, int nu, int M) {
     X_(stg, (N + 1) * slot_len(nx, nu)) X_(hg, (N + 1) * hg_len(nx, nu)) X_(vf, (N + 1) * vf_len(nx, nu))   \
     X_(dX2, (N + 1) * nx) X_(dU2, N * nu) X_(dS2, N + 1) X_(yi2, nx) X_(yk2, N * nx) X_(yt2, 8)         \
     X_(sts, it_len(N, nx, nu, M)) X_(rcs, nx + N * nx + 8 + (N + 1) * M) X_(wdi, it_len(N, nx, nu, M))       \
-    X_(wdd, it_len(N, nx, nu, M))
+    X_(wdd, it_len(N, nx, nu, M)) X_(rp, ne_len(N, nx, M)) X_(rn, ne_len(N, nx, M)) X_(rzp, ne_len(N, nx, M))     \
+    X_(rzn, ne_len(N, nx, M)) X_(rdp, ne_len(N, nx, M)) X_(rdn, ne_len(N, nx, M)) X_(rdzp, ne_len(N, nx, M))      \
+    X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -166,8 +184,9 @@ struct Ws {
     uint32_t* tmask[2];  // its hidden-layer ReLU patterns [4][slot][P]
     int* tsrc;           // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
     int* cnt;  // counters of step parity q at cnt + 8 q: [0] evaluation ranks, [1] trial slots, [2] next active
-               // count, [3] full-launch points whose forward was reused
+               // count, [3] full-launch points whose forward was reused, [4] Newton solves, [5] restoration list count
     int* act[2]; // active instance lists (ping-pong)
+    int* actr[2]; // the instances of act in a restoration phase (count: counter [5] of the step's set)
     int64_t cap;
     int ppk;
 };
@@ -200,6 +219,7 @@ static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
         b += align256((size_t)B * sizeof(int));                    // tsrc
     }
     b += align256(2 * (size_t)B * sizeof(int));
+    b += align256(2 * (size_t)B * sizeof(int));  // restoration lists
     b += 256;  // counters
     return b;
 }
@@ -237,6 +257,9 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
     }
     w.act[0] = (int*)c;
     w.act[1] = (int*)c + B;
+    c += align256(2 * (size_t)B * sizeof(int));
+    w.actr[0] = (int*)c;
+    w.actr[1] = (int*)c + B;
     c += align256(2 * (size_t)B * sizeof(int));
     w.cnt = (int*)c;
     return w;
@@ -673,6 +696,189 @@ struct Solver {
         __syncthreads();  // hg is in HBM: full fence
     }
 
+    // ---------------- the feasibility restoration problem (IPOPT MinC_1NrmRestorationPhase) ----------------
+    //   min rho sum(p + n) + zeta/2 ||D_R (x - x_R)||^2  s.t.  c(x) - p + n = 0, p, n >= 0  (every equality row,
+    //   d(x) - t included).  Newton system (oracle build(), resto branch): the objective's curvature is zeta D_R^2;
+    //   on an inequality row t, p and n are eliminated (D = 1 / C, rhs = (r - E) / C); on an equality row p and n
+    //   are eliminated into a soft equality J dz - D y = -r + e (dsoft, esoft), folded into the Riccati recursion
+    //   by k_ric<DYN, true>.  x_R and the original bound multipliers are the iterate saved in wdi at the start.
+    __device__ __forceinline__ static void stage_resto(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k,
+                                                       double dw, double mu, double* o) {
+        const int N = dm.N, M = dm.M, nc = dm.nc;
+        const double kappa_d = 1e-5, rho = SC(SC_RHO), zeta = SC(SC_ZETA);
+        const double* ori = &AT(wdi, 0);
+        const int oU = ws.L_X, oS = oU + ws.L_U;
+        double Pp[3][3], ps[3], hx[NX], gp[NX], gu[NU], uu[NU], ss = 0, gs = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            ps[i] = 0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Pp[i][j] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {  // proximity term: gradient zeta D_R^2 (x - x_R), curvature zeta D_R^2
+            const double xr = ori[k * NX + i], dr = fmin(1.0, 1.0 / fabs(xr));
+            hx[i] = zeta * dr * dr;
+            gp[i] = hx[i] * (AT(X, k * NX + i) - xr);
+        }
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            uu[i] = gu[i] = 0;
+            if (k < N) {
+                const double ur = ori[oU + k * NU + i], dr = fmin(1.0, 1.0 / fabs(ur));
+                uu[i] = zeta * dr * dr;
+                gu[i] = uu[i] * (AT(U, k * NU + i) - ur);
+            }
+        }
+        const double Sk = AT(S, k);
+        if (dm.ns) {
+            const double sr = ori[oS + k], dr = fmin(1.0, 1.0 / fabs(sr));
+            ss = zeta * dr * dr;
+            gs = ss * (Sk - sr);
+        }
+        double Hz[NX + NU][NX + NU];
+#pragma unroll
+        for (int i = 0; i < NX + NU; ++i)
+#pragma unroll
+            for (int j = 0; j < NX + NU; ++j) Hz[i][j] = 0;
+        if (k < N) {  // dynamics c_k = x_{k+1} - F_k  =>  W -= sum_i y_i d2F_i
+            double x[NX], u[NU], l[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+            for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) l[i] = AT(yk, k * NX + i);
+            D::hess(x, u, l, p.dt, p.wheelbase, Hz);
+        }
+        {
+            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const double v = AT(Hd, k * 6 + q);
+                Pp[ia[q]][ib[q]] += v;
+                if (ia[q] != ib[q]) Pp[ib[q]][ia[q]] += v;
+            }
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                const double uv = AT(U, k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
+                uu[i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
+                gu[i] += -mu / sl + mu / su;
+            }
+        if (dm.ns) {
+            ss += AT(zs, k) / Sk;
+            gs += -mu / Sk + kappa_d * mu;
+        }
+        const int q0 = NX + N * NX + nc;  // first inequality row
+        for (int j = 0; j < M; ++j) {
+            double J[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + j) * 3 + a);
+            const int r = q0 + k * M + j;
+            const double t = AT(T, k * M + j), v = AT(vt, k * M + j), pp = AT(rp, r), nn = AT(rn, r);
+            const double st = v / t + dw, sp = AT(rzp, r) / pp + dw, sn = AT(rzn, r) / nn + dw;
+            const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+            const double E = (mu / t - kappa_d * mu) / st + (mu / pp - rho - kappa_d * mu) / sp -
+                             (mu / nn - rho - kappa_d * mu) / sn;
+            const double Dj = 1.0 / C, rhs = (AT(rcq, k * M + j) - E) / C;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                gp[a] += J[a] * rhs;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) Pp[a][c] += Dj * J[a] * J[c];
+                if (dm.sd) ps[a] += Dj * J[a];
+            }
+            if (dm.sd) {
+                ss += Dj;
+                gs += rhs;
+            }
+        }
+        auto emit = [&](auto has_u) {
+            constexpr bool HU = decltype(has_u)::value;
+            constexpr int is = HU ? NX + NU : NX;
+            const bool hs = dm.ns != 0;
+            const int nz = is + (hs ? 1 : 0);
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+#pragma unroll
+                for (int j = 0; j < NZ; ++j) {
+                    double h = 0;
+                    if (i < 3 && j < 3) h += Pp[i][j];
+                    if (i == j && i < NX) h += hx[i];
+                    if (HU && i == j && i >= NX && i < NX + NU) h += uu[i - NX];
+                    if (HU && i < NX + NU && j < NX + NU) h -= Hz[i][j];
+                    if (hs) {
+                        if (i == is && j == is) h += ss;
+                        if (i == is && j < 3) h += ps[j];
+                        if (j == is && i < 3) h += ps[i];
+                    }
+                    if (i == j && i < nz) h += dw;
+                    o[i * (NZ + 2) + j] = h;
+                }
+                double gi = 0;
+                if (i < NX) gi = gp[i];
+                else if (HU && i < NX + NU) gi = gu[i - NX];
+                if (hs && i == is) gi = gs;
+                o[i * (NZ + 2) + NZ] = gi;
+                o[i * (NZ + 2) + NZ + 1] = 0.0;
+            }
+        };
+        if (k < N) emit(std::true_type{});
+        else emit(std::false_type{});
+    }
+
+    // the soft equality rows' compliance and offset (oracle build(), resto branch) for delta_w dw, rows lane.. by
+    // stride: D = 1/sp + 1/sn, e = (mu/p - rho - kd mu)/sp - (mu/n - rho - kd mu)/sn, sp = zp/p + dw, sn = zn/n + dw
+    __device__ static void soft_rows(const Dims& dm, const Ws& ws, int b, int lane, int stride, double dw, double mu) {
+        const double kappa_d = 1e-5, rho = SC(SC_RHO);
+        const int nrow = NX + dm.N * NX + dm.nc;
+        for (int i = lane; i < nrow; i += stride) {
+            const double pp = AT(rp, i), nn = AT(rn, i);
+            const double sp = AT(rzp, i) / pp + dw, sn = AT(rzn, i) / nn + dw;
+            AT(dsoft, i) = 1.0 / sp + 1.0 / sn;
+            AT(esoft, i) = (mu / pp - rho - kappa_d * mu) / sp - (mu / nn - rho - kappa_d * mu) / sn;
+        }
+    }
+
+    // every stage of the restoration Newton system (lane = knot): hg, and the slot [A B 0 | c + e] with M = 0
+    __device__ static void build_stages_resto(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane,
+                                              double dw, double mu, double* SL) {
+        const int N = dm.N;
+        soft_rows(dm, ws, b, lane, 64, dw, mu);
+        __syncthreads();
+        for (int k = lane; k <= N; k += 64) {
+            double* o = SL + (size_t)k * SLOT;
+            stage_resto(p, dm, ws, b, k, dw, mu, &AT(hg, k * HG));
+            double A[NX][NX], Bu[NX][NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                for (int j = 0; j < NX; ++j) A[i][j] = 0;
+#pragma unroll
+                for (int j = 0; j < NU; ++j) Bu[i][j] = 0;
+            }
+            if (k < N) {
+                double x[NX], u[NU];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+                D::jac(x, u, p.dt, p.wheelbase, A, Bu);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                for (int j = 0; j < NZ; ++j) o[sAB + i * NAB + j] = j < NX ? A[i][j] : (j < NX + NU ? Bu[i][j - NX] : 0.0);
+                o[sAB + i * NAB + NZ] = k < N ? -AT(rcd, k * NX + i) + AT(esoft, NX + k * NX + i) : 0.0;
+#pragma unroll
+                for (int j = NZ + 1; j < NAB; ++j) o[sAB + i * NAB + j] = 0.0;
+            }
+            o[sM + 0] = o[sM + 1] = o[sM + 2] = o[sM + 3] = 0.0;  // the restoration objective has no path length
+        }
+        __syncthreads();
+    }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -741,7 +947,12 @@ template <int DYN>
 struct RicWpe {
     static constexpr int value = DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
 };
-template <int DYN>
+// RESTO = true: the restoration problem's Newton solve (instances with SC_RESTO = 1, list ws.actr): every
+// equality row is soft (p, n eliminated, oracle soft_transform): before stage k uses the value function of
+// x_{k+1} it becomes that of y = x_{k+1} - w (P <- (I + P D)^-1 P, [p | G] likewise, Psi / psi corrected), the
+// initial state likewise after the sweep, the terminal rows get (-Psi + D_t) nu = ..., and the forward sweep
+// maps x_{k+1} = (I + D P)^-1 (y - D (p + G nu)); every stage block must be positive definite.
+template <int DYN, bool RESTO>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
                                             const int* __restrict__ nact, int mode) {
@@ -757,10 +968,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     __shared__ typename R::Sh shg[R::IPW];
     __shared__ __attribute__((aligned(16))) double ring[RING][NDMA][R::IPW][DW];  // DMA'd stage inputs
     const int grp = threadIdx.x / G, l = threadIdx.x % G, gb = grp * G;
-    const int si = blockIdx.x * R::IPW + grp;
-    if (si >= n_active || si >= *nact) return;
+    // RESTO: grid-stride over the restoration list (the host sizes the grid by a stale bound); else one instance
+    // per group
+    const int nlist = std::min(n_active, *nact);
+    auto body = [&](const int si) {
     const int b = active[si];
     if ((int)SC(SC_RIC) != 1) return;
+    if ((SC(SC_RESTO) != 0.0) != RESTO) return;
     typename R::Sh& sh = shg[grp];
     const int N = dm.N, nc = dm.nc, ns = dm.ns;
     const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
@@ -771,6 +985,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     const int a_pe = j - (NZ + 2);                                              // [Psi | psi] row
     const bool own_pe = a_pe >= 0 && a_pe < NC;
     double nu_[2][NC], dx0[NX];
+    const int neg_lim = RESTO ? 0 : nc;  // negative stage pivots the terminal block can absorb (none: all rows soft)
+    const int q0r = NX + N * NX + nc;   // restoration rows: first inequality row (terminal rows at q0r - nc)
 
     // backward sweep + terminal multipliers; 0, or 1 on a wrong inertia (uniform within the group)
     auto backward = [&]() -> int {
@@ -816,6 +1032,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
 #pragma unroll
         for (int r = 0; r < RING; ++r) issue(N - r);
         int negsum = 0;
+        // RESTO: the value function in sh.VE becomes that of y = x - w for the soft rows with compliance Dp[0..NX):
+        // columns [P | p | G] <- S^-1 K^-1 S [P | p | G] (K = I + S P S, S = D^1/2, redundantly factorised by every
+        // lane), Psi -= G' D G~, psi -= G' D p~ (the terminal lanes' registers).  1 if K is not positive definite.
+        auto soft_step = [&](const double* Dp) -> int {
+            double Dd[NX], Sd[NX], K[NX][NX], v[NX], ga[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                Dd[i] = Dp[i];
+                Sd[i] = sqrt(Dd[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int c = 0; c < NX; ++c) K[i][c] = (i == c ? 1.0 : 0.0) + Sd[i] * sh.VE[i][c] * Sd[c];
+            int perm[NX], nneg;
+            if (ldl_factor<NX>(K, NX, perm, &nneg) || nneg) return 1;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                v[i] = gc >= 0 ? Sd[i] * sh.VE[i][gc] : 0.0;
+                ga[i] = own_pe ? sh.VE[i][NX + 2 + a_pe] : 0.0;
+            }
+            ric_sync();
+            if (gc >= 0) {
+                ldl_solve1<NX>(K, NX, perm, v);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) sh.VE[i][gc] = v[i] / Sd[i];
+            }
+            ric_sync();
+            if (own_pe) {
+#pragma unroll
+                for (int c = 0; c < NC + 2; ++c) {
+                    const int vc_ = c < NC ? NX + 2 + c : NX + (c - NC);
+                    double t = 0;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) t += Dd[i] * ga[i] * sh.VE[i][vc_];
+                    pe[c] -= t;
+                }
+            }
+            return 0;
+        };
         const bool wcol = j < NZ + 2;              // W column j is P AB (+ p_r), not a Gamma pass-through
         const int cc = j < NZ ? j : NZ;            // AB column (the c column for the p_r columns)
         const int jc = j >= NZ && j < NQE ? NX + j - NZ : 0;  // VE column carried into W
@@ -829,6 +1085,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
             long long tq = wall_clock64();
 #endif
             const int nv = (k < N ? NU : 0) + ns;
+            if constexpr (RESTO)
+                if (k < N && soft_step(&AT(dsoft, NX + k * NX))) return 1;  // soft dynamics rows of stage k
             wait_dma(k >= RING - 1 ? 1 : 0);  // stage k's DMA landed (the later RING-1 stages may be in flight)
             const double* hrow = &ring[k % RING][0][grp][0];  // hg of stage k, element e at (e / DW) * IPW * DW + e % DW
             auto HGe = [&](int e) { return hrow[(e / DW) * (R::IPW * DW) + e % DW]; };
@@ -960,7 +1218,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
                 if (!(fabs(d2) > 1e-13 * scale) || !isfinite(d2)) return 1;
                 const double i2 = 1.0 / d2;
                 negsum += (d0 < 0) + (d1 < 0) + (d2 < 0);
-                if (negsum > nc) return 1;
+                if (negsum > neg_lim) return 1;
                 if (gc >= 0) {
                     const double x0 = q[NX], x1 = q[NX + 1], x2 = q[NX + 2];
                     // permutations as exact 0/1 blends (selects by a run-time index become scratch arrays)
@@ -988,7 +1246,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
                     for (int c = 0; c < NV; ++c) L[a][c] = (a < nv && c < nv) ? Qv[c][NX + a] : 0.0;
                 if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
                 negsum += nneg;
-                if (negsum > nc) return 1;
+                if (negsum > neg_lim) return 1;
                 if (gc >= 0) {
                     double col[NV];
 #pragma unroll
@@ -1055,7 +1313,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
 #pragma unroll
                 for (int rr = 0; rr < 2; ++rr) {
                     if (k == N) {
-                        pe[NC + rr] = (a_pe < nc && mode == MODE_NEWTON) ? AT(rct, a_pe) : 0.0;
+                        pe[NC + rr] = (a_pe < nc && mode == MODE_NEWTON)
+                                          ? AT(rct, a_pe) - (RESTO ? AT(esoft, q0r - nc + a_pe) : 0.0)
+                                          : 0.0;
                     } else {
                         const d2v* cs = reinterpret_cast<const d2v*>(&sh.cols[NX + rr][0]);
                         const d2v g01 = cs[0], g23 = cs[1];
@@ -1084,18 +1344,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
             printf("RICG stage phases: WQ %lld syncA+Qv %lld ldl+gains+VU %lld sym+PE+stage %lld syncC %lld (x10ns, sum over stages)\n",
                    ph[0], ph[1], ph[2], ph[3], ph[4]);
 #endif
+        if constexpr (RESTO)
+            if (soft_step(&AT(dsoft, 0))) return 1;  // soft initial-state rows
         if (own_pe)
 #pragma unroll
             for (int c = 0; c < NC + 2; ++c) sh.PE[a_pe][c] = pe[c];
         __syncthreads();  // gains (slot) and vf in HBM are read across lanes by the forward sweep
         // terminal multipliers (every lane, identical): -Psi nu_r = G0' dx0 + psi_r, delta_c on the terminal block
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) : 0.0;
+        for (int i = 0; i < NX; ++i) dx0[i] = mode == MODE_NEWTON ? -AT(rci, i) + (RESTO ? AT(esoft, i) : 0.0) : 0.0;
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc) nu_[rr][cc] = 0.0;
-        if (nc) {
+        if (RESTO && nc) {  // soft terminal rows: (-Psi + D_t) nu = G0' dx0 + psi, positive definite
+            double L[NC][NC];
+            int perm[NC], nneg;
+#pragma unroll
+            for (int i = 0; i < NC; ++i)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    L[i][c] = (i < nc && c < nc) ? -sh.PE[i][c] + (i == c ? AT(dsoft, q0r - nc + i) : 0.0)
+                                                 : 0.0;
+            if (ldl_factor<NC>(L, nc, perm, &nneg) || nneg) return 1;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) {
+                double t = 0;
+                if (cc < nc) {
+                    t = sh.PE[cc][NC];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) t += sh.VE[r][NX + 2 + cc] * dx0[r];
+                }
+                nu_[0][cc] = t;
+            }
+            ldl_solve1<NC>(L, nc, perm, nu_[0]);
+        } else if (nc) {
             double L[NC][NC];
             int perm[NC], nneg;
 #pragma unroll
@@ -1170,6 +1453,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
         __syncthreads();
     };
 
+    // RESTO: the restoration system is not affine in delta_w (an inequality row's D = 1 / C, C = 1/(v/t + dw) +
+    // 1/(zp/p + dw) + 1/(zn/n + dw)): the retry adds the differences of D J J' and J rhs per row, the diagonal
+    // step, and recomputes the soft equality rows (dsoft / esoft, the slots' c columns)
+    auto add_dw_resto = [&](double dw_old, double dw_new) {
+        const int M = dm.M, sd = dm.sd;
+        const bool hs = ns != 0;
+        const double kappa_d = 1e-5, rho = SC(SC_RHO);
+        SV::soft_rows(dm, ws, b, l, G, dw_new, mu0);
+        __syncthreads();
+        auto dr = [&](int r, int q, double dw_, double* Dq) {  // D and rhs of inequality row q (restoration row r)
+            const double t = AT(T, q), v = AT(vt, q), pp = AT(rp, r), nn = AT(rn, r);
+            const double st = v / t + dw_, sp = AT(rzp, r) / pp + dw_, sn = AT(rzn, r) / nn + dw_;
+            const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+            const double E = (mu0 / t - kappa_d * mu0) / st + (mu0 / pp - rho - kappa_d * mu0) / sp -
+                             (mu0 / nn - rho - kappa_d * mu0) / sn;
+            *Dq = 1.0 / C;
+            return (AT(rcq, q) - E) / C;
+        };
+        for (int k = l; k <= N; k += G) {
+            double* o = &AT(hg, k * HG);
+            const int is = k < N ? NX + NU : NX, nz = is + (hs ? 1 : 0);
+            for (int i = 0; i < nz; ++i) o[i * (NZ + 2) + i] += dw_new - dw_old;
+            for (int qq = 0; qq < M; ++qq) {
+                double J[3], D0, D1;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + qq) * 3 + a);
+                const int q = k * M + qq;
+                const double r0 = dr(q0r + q, q, dw_old, &D0), r1 = dr(q0r + q, q, dw_new, &D1);
+                const double dD = D1 - D0, dg = r1 - r0;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) o[a * (NZ + 2) + c] += dD * J[a] * J[c];
+                    o[a * (NZ + 2) + NZ] += J[a] * dg;
+                    if (sd) {
+                        o[is * (NZ + 2) + a] += dD * J[a];
+                        o[a * (NZ + 2) + is] += dD * J[a];
+                    }
+                }
+                if (sd) {
+                    o[is * (NZ + 2) + is] += dD;
+                    o[is * (NZ + 2) + NZ] += dg;
+                }
+            }
+            if (k < N)
+                for (int i = 0; i < NX; ++i)
+                    SL[(size_t)k * SLOT + sAB + i * NAB + NZ] = -AT(rcd, k * NX + i) + AT(esoft, NX + k * NX + i);
+        }
+        __syncthreads();
+    };
+
     // inertia correction (IPOPT): delta_w = 0, then 1e-4 (or last / 3), x100 (x8 once one was used)
     const double fixdw = SC(SC_RICFIX);  // >= 0: second-order correction, stages built with this delta_w
     const bool fixed = fixdw >= 0.0;
@@ -1186,7 +1520,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
         ++n_att;
 #endif
         if (attempt > 0) {
-            add_dw(dw - dw_in_hg);
+            if constexpr (RESTO) add_dw_resto(dw_in_hg, dw);
+            else add_dw(dw - dw_in_hg);
             dw_in_hg = dw;
         }
 #ifdef NLOT_PHASE_PROF
@@ -1262,6 +1597,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
             r_[NX + NU] = o0;
             r_[NZ] = o1;
         }
+        if constexpr (RESTO) {  // soft dynamics rows: x_{k+1} = S K^-1 S^-1 (Phi x_k + off - D (p + G nu))
+            const double* v1 = &AT(vf, (k + 1) * VF);
+            double Dd[NX], Sd[NX], K[NX][NX], w[NX], col[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                Dd[i] = AT(dsoft, NX + k * NX + i);
+                Sd[i] = sqrt(Dd[i]);
+                double t = v1[i * NCOL + NX];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += v1[i * NCOL + NX + 2 + cc] * nu_[0][cc];
+                w[i] = t;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int c = 0; c < NX; ++c) K[i][c] = (i == c ? 1.0 : 0.0) + Sd[i] * v1[i * NCOL + c] * Sd[c];
+            int perm[NX], nneg;
+            ldl_factor<NX>(K, NX, perm, &nneg);  // positive definite: the backward sweep factorised it
+#pragma unroll 1
+            for (int c = 0; c <= NX; ++c) {  // the NX columns of Phi, then the offset
+                const int cs = c < NX ? c : NX + NU;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    const double y = slot[sAB + i * NAB + cs];
+                    col[i] = (c < NX ? y : y - Dd[i] * w[i]) / Sd[i];
+                }
+                ldl_solve1<NX>(K, NX, perm, col);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) slot[sAB + i * NAB + cs] = Sd[i] * col[i];
+            }
+        }
     }
     __syncthreads();
     // (F2) the chain dx_{k+1} = Phi_k dx_k + off_k: lane i < NX of the group carries dx[i] of both
@@ -1272,6 +1638,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     {
         const int li = l < NX ? l : 0;
         double xv = 0;
+        if constexpr (RESTO) {  // soft initial-state rows: x_0 = S K^-1 S^-1 (dx0 - D (p_0 + G_0 nu))
+            const double* v0 = &AT(vf, 0);
+            double Dd[NX], Sd[NX], K[NX][NX], col[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                Dd[i] = AT(dsoft, i);
+                Sd[i] = sqrt(Dd[i]);
+                double t = v0[i * NCOL + NX];
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) t += v0[i * NCOL + NX + 2 + cc] * nu_[0][cc];
+                col[i] = (dx0[i] - Dd[i] * t) / Sd[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int c = 0; c < NX; ++c) K[i][c] = (i == c ? 1.0 : 0.0) + Sd[i] * v0[i * NCOL + c] * Sd[c];
+            int perm[NX], nneg;
+            ldl_factor<NX>(K, NX, perm, &nneg);
+            ldl_solve1<NX>(K, NX, perm, col);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dx0[i] = Sd[i] * col[i];
+        }
 #pragma unroll
         for (int i = 0; i < NX; ++i)
             if (i == l) xv = dx0[i];
@@ -1390,6 +1778,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
         SC(SC_DW) = dw;
         SC(SC_RIC) = 2;
     }
+    };
+    if constexpr (RESTO) {
+        for (int si = blockIdx.x * R::IPW + grp; si < nlist; si += gridDim.x * R::IPW) {
+            body(si);
+            __syncthreads();
+        }
+    } else {
+        const int si = blockIdx.x * R::IPW + grp;
+        if (si < nlist) body(si);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1449,6 +1847,11 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
         SC(SC_LASTREJF) = 0;
         SC(SC_NFREJ) = 0;
         SC(SC_NFRES) = 0;
+        SC(SC_INSOFT) = 0;
+        SC(SC_SOFTCNT) = 0;
+        SC(SC_RESTO) = 0;
+        SC(SC_RNFILT) = 0;
+        SC(SC_NRESTO) = 0;
         ws.act[0][b] = b;
     }
 }
@@ -1564,6 +1967,89 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
     return wsum(f) + p.slack_penalty * wsum(sq) + p.smooth_weight * wsum(uq);
 }
 
+// IPOPT filter augmentation (lane 0): drop the entries the new one dominates, append it (the oldest entry is
+// forgotten at capacity).  filt: the original problem's filter (count SC_NFILT) or the restoration's (SC_RNFILT).
+__device__ inline void filter_add(const Ws& ws, int b, double* filt, int sc_n, double theta, double phi) {
+    const double gt = 1e-5, gp = 1e-8, ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
+    const int nfc = (int)SC(sc_n);
+    int w = 0;
+    for (int i = 0; i < nfc; ++i) {
+        const double ft = filt[2 * i], fp = filt[2 * i + 1];
+        if (!(ft >= ntv && fp >= npv)) {
+            filt[2 * w] = ft;
+            filt[2 * w + 1] = fp;
+            ++w;
+        }
+    }
+    if (w == FILT_MAX) {
+        for (int i = 0; i + 1 < FILT_MAX; ++i) {
+            filt[2 * i] = filt[2 * (i + 1)];
+            filt[2 * i + 1] = filt[2 * (i + 1) + 1];
+        }
+        w--;
+    }
+    filt[2 * w] = ntv;
+    filt[2 * w + 1] = npv;
+    SC(sc_n) = w + 1;
+}
+
+// The line search of the original problem failed and the soft restoration did not help: IPOPT's feasibility
+// restoration phase (BacktrackingLineSearch::FindAcceptableTrialPoint).  At an almost feasible point (theta <=
+// 1e-2 tol) IPOPT does not restore: without an acceptable iterate to fall back to it stops with Restoration_Failed.
+// Otherwise the current point enters the filter with the line search's reference values and the instance moves to
+// PH_RINIT: the next step's full launch evaluates its corners (emitted here into that step's list, counters
+// cnt_next), and k_resto_a initialises the restoration problem there.  Returns the new phase (uniform).
+__device__ int resto_enter(const NlotSolverOptions& o, const NlotProblem& p, const Dims& dm, const Ws& ws, int b,
+                           int lane, int* cnt_next) {
+    const double th = SC(SC_THETA);
+    wsync();
+    if (th <= 1e-2 * o.tol) {
+        if (lane == 0) {
+            SC(SC_STATUS) = NLOT_RESTO_FAILED;
+            SC(SC_PHASE) = PH_DONE;
+        }
+        wsync();
+        return PH_DONE;
+    }
+    if (lane == 0) {
+        filter_add(ws, b, &AT(filt, 0), SC_NFILT, th, SC(SC_PHI));
+        SC(SC_RESTO) = 1;
+        SC(SC_PHASE) = PH_RINIT;
+        SC(SC_ACCSLOT) = -1;
+    }
+    wsync();
+    emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+    return PH_RINIT;
+}
+
+// The backtracking line search of the original problem ended (alpha < alpha_min): IPOPT TrySoftRestoStep first
+// (phase PH_SOFT1: the step min(alpha_max, alpha_z) for both primal and dual variables, one trial point emitted
+// into (tp, cnt)), else the restoration phase, else (resto = 0) NLOT_LS_FAILED.  Returns the new phase.
+__device__ int ls_failed(const NlotSolverOptions& o, const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane,
+                         float* tp, int* cnt, int* cnt_next) {
+    if (!o.resto) {
+        wsync();
+        if (lane == 0) {
+            SC(SC_STATUS) = NLOT_LS_FAILED;
+            SC(SC_PHASE) = PH_DONE;
+        }
+        wsync();
+        return PH_DONE;
+    }
+    if (o.soft_resto_pderror_reduction_factor > 0) {
+        const double a = fmin(SC(SC_AMAX), SC(SC_AZ));
+        wsync();
+        if (lane == 0) {
+            SC(SC_ALPHA) = a;
+            SC(SC_PHASE) = PH_SOFT1;
+        }
+        wsync();
+        emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, a);
+        return PH_SOFT1;
+    }
+    return resto_enter(o, p, dm, ws, b, lane, cnt_next);
+}
+
 // k_iter_a: evaluation, optimality test, barrier update, then the stage matrices of the Newton system
 // (k_ric solves it).  init_pass = 1 (first step only): slack push and the least-squares multiplier
 // system of the instances in INIT; init_pass = 0: everything else (INIT instances first take their
@@ -1571,7 +2057,7 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
-                                               const double* __restrict__ xg, int init_pass, int* cnt) {
+                                               const double* __restrict__ xg, int init_pass, int* cnt, int* cnt_next) {
     if ((int)blockIdx.x >= cnt[2]) return;  // grid sized by a stale (larger) host count: steps run ahead of the host
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -1579,8 +2065,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     using SV = Solver<DYN>;
     constexpr int NX = SV::NX, NU = SV::NU;
     const int b = active[blockIdx.x], lane = threadIdx.x;
+    if (SC(SC_RESTO) != 0.0) return;  // k_resto_a
     const int ph = (int)SC(SC_PHASE);
-    if (ph != PH_INIT && ph != PH_EVAL && ph != PH_SOC) return;
+    if (ph != PH_INIT && ph != PH_EVAL && ph != PH_SOC && ph != PH_SOFT2) return;
     if (init_pass && ph != PH_INIT) return;
     double* SL = &AT(stg, 0);
     if (ph == PH_SOC) {
@@ -1728,6 +2215,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     // ---- optimality measures (IPOPT scaled E_0 / E_mu) ----
     double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0, nzc = 0;
     double dsq = 0, psq = 0, csum = 0;  // quality-function oracle: ||grad L||^2, ||c, d - t||^2, sum z s
+    double d1 = 0, p1 = 0;              // soft restoration: 1-norms of the dual and primal residuals
     for (int k = lane; k <= N; k += 64) {
         double r[NX];
 #pragma unroll
@@ -1774,6 +2262,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         for (int i = 0; i < NX; ++i) {
             dual = fmax(dual, fabs(r[i]));
             dsq += r[i] * r[i];
+            d1 += fabs(r[i]);
         }
         if (k < N)
 #pragma unroll
@@ -1784,6 +2273,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                 for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
                 dual = fmax(dual, fabs(t));
                 dsq += t * t;
+                d1 += fabs(t);
             }
         if (dm.ns) {
             double t = 2.0 * p.slack_penalty * AT(S, k) - AT(zs, k);
@@ -1791,16 +2281,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                 for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
             dual = fmax(dual, fabs(t));
             dsq += t * t;
+            d1 += fabs(t);
         }
         for (int j = 0; j < M; ++j) {
             const double t = -AT(yd, k * M + j) - AT(vt, k * M + j);
             dual = fmax(dual, fabs(t));
             dsq += t * t;
+            d1 += fabs(t);
         }
     }
     auto pri_ = [&](double v) {
         primal = fmax(primal, fabs(v));
         psq += v * v;
+        p1 += fabs(v);
     };
     for (int i = lane; i < NX; i += 64) pri_(AT(rci, i));
     for (int i = lane; i < nc; i += 64) pri_(AT(rct, i));
@@ -1838,10 +2331,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     ysum = wsum(ysum);
     nzc = wsum(nzc);
     const double csum_w = wsum(csum), dsq_w = wsum(dsq), psq_w = wsum(psq);
+    const double d1_w = wsum(d1), p1_w = wsum(p1);
     const double ny = NX + N * NX + nc + (N + 1) * M;
     const double sd = fmax(100.0, (ysum + zsum) / (ny + nzc)) / 100.0;
     const double scc = fmax(100.0, zsum / nzc) / 100.0;
     const double E0 = fmax(fmax(dual / sd, primal), c0 / scc);
+    // IPOPT's primal-dual system error at barrier parameter m (soft restoration): sum of the 1-norms of the dual,
+    // primal and complementarity residuals over the element count
+    const double n_pd = (double)((N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M) +
+                        (double)(NX + nc + N * NX + (N + 1) * M) + nzc;
+    auto pd_error = [&](double m) {
+        double c1 = 0;
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            c1 += fabs(AT(zl, e) * (u - p.umin[e % NU]) - m) + fabs(AT(zu, e) * (p.umax[e % NU] - u) - m);
+        }
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) c1 += fabs(AT(zs, k) * AT(S, k) - m);
+        for (int q = lane; q < (N + 1) * M; q += 64) c1 += fabs(AT(vt, q) * AT(T, q) - m);
+        return (d1_w + p1_w + wsum(c1)) / n_pd;
+    };
+    if (ph == PH_SOFT2) {
+        // the soft restoration's tentatively accepted point (k_accept): accepted if its primal-dual error fell by
+        // the factor, then this is the next iteration's evaluation; else back to the saved point and restoration
+        const double pd_t = pd_error(SC(SC_MUPD));
+        const bool ok = isfinite(pd_t) && pd_t <= o.soft_resto_pderror_reduction_factor * SC(SC_PDC);
+        wsync();
+        if (!ok) {
+            double* buf = &AT(sts, 0);
+            iter_io(ws, b, lane, buf, false);
+            wsync();
+            resto_enter(o, p, dm, ws, b, lane, cnt_next);
+            return;
+        }
+        if (lane == 0) {
+            SC(SC_ITERS) = SC(SC_ITERS) + 1;
+            SC(SC_INSOFT) = 1;
+            SC(SC_TINYLAST) = 0;
+            SC(SC_PHASE) = PH_EVAL;
+        }
+        wsync();
+    }
     const int iters = (int)SC(SC_ITERS);
     wsync();
     auto finish = [&](int status) {
@@ -1959,11 +2489,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
         use_qf = free_;
     }
+    const double mu_pd = (o.mu_strategy == 1 && use_qf) ? 0.0 : mu;  // soft restoration's mu (free mode: 0)
+    const double pd_c = pd_error(mu_pd);
     wsync();
     if (lane == 0) {
         SC(SC_MU) = mu;
         SC(SC_TAU) = tau;
         if (reset_filter) SC(SC_NFILT) = 0;
+        SC(SC_PDC) = pd_c;
+        SC(SC_MUPD) = mu_pd;
     }
     wsync();
     // ---- Newton system (free mode: affine mu = 0 and centering mu = avg right-hand sides): stage
@@ -1991,7 +2525,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
 // and the line-search reference values.
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
-                                               const int* __restrict__ active, int* cnt, float* tp) {
+                                               const int* __restrict__ active, int* cnt, float* tp, int* cnt_next) {
     if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -1999,6 +2533,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     using SV = Solver<DYN>;
     constexpr int NX = SV::NX, NU = SV::NU;
     const int b = active[blockIdx.x], lane = threadIdx.x;
+    if (SC(SC_RESTO) != 0.0) return;  // k_resto_b
     const int ric = (int)SC(SC_RIC);
     if (ric == 4) {  // a second-order correction's solve failed: restore the step, halve the original alpha
         double* rb = &AT(rcs, 0);
@@ -2011,6 +2546,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             step_io(ws, b, lane, buf, save);
         }
         const double na = 0.5 * SC(SC_SOCA);
+        const bool failed = na < SC(SC_AMIN);
         wsync();
         if (lane == 0) {
             SC(SC_RIC) = 0;
@@ -2018,14 +2554,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             SC(SC_AZ) = SC(SC_SOCAZ);
             SC(SC_TRIALS) = 1;
             SC(SC_ALPHA) = na;
-            if (na < SC(SC_AMIN)) {
-                SC(SC_STATUS) = NLOT_LS_FAILED;
-                SC(SC_PHASE) = PH_DONE;
-            } else {
-                SC(SC_PHASE) = PH_LS;
-            }
+            if (!failed) SC(SC_PHASE) = PH_LS;
         }
-        if (!(na < SC(SC_AMIN))) emit_points(*pp_, *dd_, ws, b, lane, cnt, true, tp, 1, na);
+        wsync();
+        if (failed) ls_failed(o, *pp_, *dd_, ws, b, lane, tp, cnt, cnt_next);
+        else emit_points(*pp_, *dd_, ws, b, lane, cnt, true, tp, 1, na);
         return;
     }
     if (ric != 2) return;
@@ -2391,9 +2924,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     amin *= 0.05;
     // IPOPT DetectTinyStep (not while the watchdog runs): primal step tiny relative to the iterate, multiplier
     // step small, nearly feasible -> the full step is taken without a line search
-    const bool in_wd = SC(SC_WD) != 0.0;
+    const bool in_wd = SC(SC_WD) != 0.0, in_soft = SC(SC_INSOFT) != 0.0;
     bool tiny = false;
-    if (o.tiny_step_tol > 0 && !in_wd) {
+    if (o.tiny_step_tol > 0 && !in_wd && !in_soft) {
         double mx = 0, my = 0, ya = 0;
         for (int i = lane; i < (N + 1) * NX; i += 64) mx = fmax(mx, fabs(AT(dX, i)) / (1.0 + fabs(AT(X, i))));
         for (int i = lane; i < N * NU; i += 64) mx = fmax(mx, fabs(AT(dU, i)) / (1.0 + fabs(AT(U, i))));
@@ -2415,7 +2948,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     }
     // IPOPT StartWatchDog: after watchdog_shortened_iter_trigger shortened steps in a row, remember the point,
     // its direction and reference values; the next watchdog_trial_iter_max iterations try full steps only
-    const bool start_wd = !tiny && !in_wd && o.watchdog_shortened_iter_trigger > 0 &&
+    const bool start_wd = !tiny && !in_wd && !in_soft && o.watchdog_shortened_iter_trigger > 0 &&
                           SC(SC_WDSHORT) >= o.watchdog_shortened_iter_trigger;
     if (start_wd) {
         double* buf = &AT(wdi, 0);
@@ -2451,16 +2984,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             SC(SC_WDTAU) = tau;
         }
     }
-    // the first line-search round: alpha_max alone (none for a tiny step)
     wsync();  // dX complete
+    if (in_soft) {
+        // soft restoration phase (IPOPT): no line search; after max_soft_resto_iters soft steps the restoration
+        // phase, else the next soft step (PH_SOFT1, min(alpha_max, alpha_z), this step's trial list)
+        const int sc = (int)SC(SC_SOFTCNT) + 1;
+        wsync();
+        if (lane == 0) SC(SC_SOFTCNT) = sc;
+        if (sc > o.max_soft_resto_iters) {
+            resto_enter(o, p, dm, ws, b, lane, cnt_next);
+        } else {
+            if (lane == 0) {
+                SC(SC_ALPHA) = fmin(amax, az);
+                SC(SC_PHASE) = PH_SOFT1;
+            }
+            wsync();
+            emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, fmin(amax, az));
+        }
+        return;
+    }
+    // the first line-search round: alpha_max alone (none for a tiny step)
     emit_points(p, dm, ws, b, lane, cnt, true, tp, tiny ? 0 : 1, amax);
 }
 
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* __restrict__ next,
-                                               const double* __restrict__ x0, const double* __restrict__ xg, int* cnt,
-                                               int* cnt_next, float* tp_next, const float* tval, int nspec_next) {
+                                               int* __restrict__ nextr, const double* __restrict__ x0,
+                                               const double* __restrict__ xg, int* cnt, int* cnt_next, float* tp_next,
+                                               const float* tval, int nspec_next) {
     if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -2468,7 +3020,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
     constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
     const int b = active[blockIdx.x], lane = threadIdx.x;
     int ph = (int)SC(SC_PHASE);
-    if (ph == PH_LS) {
+    // instances in a restoration phase: k_resto_ls ran their line search; here they only join the next lists
+    if (SC(SC_RESTO) == 0.0 && (ph == PH_LS || ph == PH_SOFT1)) {
         const int N = dm.N, M = dm.M, nc = dm.nc;
         const double a0 = SC(SC_ALPHA), mu = SC(SC_MU);
         const int rank0 = (int)SC(SC_RANK), ncand = (int)SC(SC_NCAND);  // as emitted
@@ -2563,6 +3116,71 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             *fa = ok && ftype && armijo;
             return ok;
         };
+        // accept the trial point x + al d: primal and equality multipliers with al, bound multipliers with az and
+        // IPOPT's kappa_Sigma safeguard
+        auto accept_point = [&](double al, double az) {
+            const double ks = 1e10;
+            auto zupd = [&](double z, double dz, double sl) {
+                const double zn = z + az * dz;
+                return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
+            };
+            for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
+            for (int e = lane; e < N * NU; e += 64) {
+                const double u = AT(U, e) + al * AT(dU, e);
+                AT(U, e) = u;
+                AT(zl, e) = zupd(AT(zl, e), AT(dzl, e), u - p.umin[e % NU]);
+                AT(zu, e) = zupd(AT(zu, e), AT(dzu, e), p.umax[e % NU] - u);
+            }
+            for (int k = lane; k <= N; k += 64)
+                if (dm.ns) {
+                    const double s_ = AT(S, k) + al * AT(dS, k);
+                    AT(S, k) = s_;
+                    AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s_);
+                }
+            for (int q = lane; q < (N + 1) * M; q += 64) {
+                const double t = AT(T, q) + al * AT(dT, q);
+                AT(T, q) = t;
+                AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), t);
+                AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
+            }
+            for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
+            for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
+            for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
+        };
+        if (ph == PH_SOFT1) {
+            // IPOPT TrySoftRestoStep: the step a = min(alpha_max, alpha_z) for primal and dual variables is taken if
+            // the filter accepts it (the switching condition at alpha 0), or if it reduces the primal-dual error by
+            // soft_resto_pderror_reduction_factor (PH_SOFT2: tentatively accepted, evaluated by the next step)
+            double th, pht;
+            int fa = 0;
+            trial(a0, rank0, false, 0.0, &th, &pht);
+            const int sat = acceptable(SC(SC_THETA), SC(SC_PHI), SC(SC_GD), 0.0, th, pht, &fa);
+            wsync();
+            if (!sat) {
+                double* buf = &AT(sts, 0);
+                iter_io(ws, b, lane, buf, true);
+                wsync();
+            }
+            accept_point(a0, a0);
+            wsync();
+            if (lane == 0) {
+                SC(SC_AZ) = a0;
+                SC(SC_ACCSLOT) = (double)rank0;
+                SC(SC_SOCK) = 0;
+                if (sat) {
+                    SC(SC_ITERS) = SC(SC_ITERS) + 1;
+                    SC(SC_INSOFT) = 0;
+                    SC(SC_SOFTCNT) = 0;
+                    SC(SC_TINYLAST) = 0;
+                    SC(SC_PHASE) = PH_EVAL;
+                } else {
+                    SC(SC_PHASE) = PH_SOFT2;
+                }
+            }
+            ph = sat ? PH_EVAL : PH_SOFT2;
+            wsync();
+            emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+        } else {
         const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
         double rth = theta, rph = phi, rgd = gd, at_fix = -1.0;
         if (in_wd) {  // watchdog: the watchdog point's reference values and its alpha_max as the test step
@@ -2683,57 +3301,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     SC(SC_NFREJ) = 0;
                 }
             }
-            if (!tiny && !fa && lane == 0) {
-                const double ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
-                const int nfc = (int)SC(SC_NFILT);
-                int w = 0;
-                for (int i = 0; i < nfc; ++i) {
-                    const double ft = AT(filt, 2 * i), fp = AT(filt, 2 * i + 1);
-                    if (!(ft >= ntv && fp >= npv)) {
-                        AT(filt, 2 * w) = ft;
-                        AT(filt, 2 * w + 1) = fp;
-                        ++w;
-                    }
-                }
-                if (w == FILT_MAX) {
-                    for (int i = 0; i + 1 < FILT_MAX; ++i) {
-                        AT(filt, 2 * i) = AT(filt, 2 * (i + 1));
-                        AT(filt, 2 * i + 1) = AT(filt, 2 * (i + 1) + 1);
-                    }
-                    w--;
-                }
-                AT(filt, 2 * w) = ntv;
-                AT(filt, 2 * w + 1) = npv;
-                SC(SC_NFILT) = w + 1;
-            }
+            if (!tiny && !fa && lane == 0) filter_add(ws, b, &AT(filt, 0), SC_NFILT, theta, phi);
             // accept: primal and multipliers with alpha, bound multipliers with alpha_z + safeguard
-            const double az = SC(SC_AZ), ks = 1e10;
-            auto zupd = [&](double z, double dz, double sl) {
-                const double zn = z + az * dz;
-                return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
-            };
-            for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
-            for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e) + al * AT(dU, e);
-                AT(U, e) = u;
-                AT(zl, e) = zupd(AT(zl, e), AT(dzl, e), u - p.umin[e % NU]);
-                AT(zu, e) = zupd(AT(zu, e), AT(dzu, e), p.umax[e % NU] - u);
-            }
-            for (int k = lane; k <= N; k += 64)
-                if (dm.ns) {
-                    const double s = AT(S, k) + al * AT(dS, k);
-                    AT(S, k) = s;
-                    AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s);
-                }
-            for (int q = lane; q < (N + 1) * M; q += 64) {
-                const double t = AT(T, q) + al * AT(dT, q);
-                AT(T, q) = t;
-                AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), t);
-                AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
-            }
-            for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
-            for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
-            for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
+            accept_point(al, SC(SC_AZ));
             const bool stop_tiny = tiny && SC(SC_TINYLAST) != 0.0;  // IPOPT STOP_AT_TINY_STEP
             ph = stop_tiny ? PH_DONE : PH_EVAL;
             if (lane == 0) {
@@ -2756,17 +3326,766 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
         } else {
             const double na = SC(SC_ALPHA);
             if (na < SC(SC_AMIN)) {
-                ph = PH_DONE;
-                if (lane == 0) {
-                    SC(SC_STATUS) = NLOT_LS_FAILED;
-                    SC(SC_PHASE) = PH_DONE;
-                }
+                ph = ls_failed(o, p, dm, ws, b, lane, tp_next, cnt_next, cnt_next);
             } else {
                 emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
             }
         }
+        }  // PH_LS
     }
-    if (ph != PH_DONE && lane == 0) next[atomicAdd(&cnt_next[2], 1)] = b;  // the next step's active count
+    wsync();
+    ph = (int)SC(SC_PHASE);
+    if (ph != PH_DONE && lane == 0) {  // the next step's active list (and restoration list) and counts
+        next[atomicAdd(&cnt_next[2], 1)] = b;
+        if (SC(SC_RESTO) != 0.0) nextr[atomicAdd(&cnt_next[5], 1)] = b;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Feasibility restoration phase (IPOPT MinC_1NrmRestorationPhase; oracle restoration()): instances with
+// SC_RESTO = 1, list ws.actr.  The restoration problem's iterate lives in the ordinary arrays (X U S T, y, z) plus
+// p, n, z_p, z_n per equality row; the original iterate (x_R and its bound multipliers) is saved in wdi.
+//   k_resto_a  (PH_RINIT: initialisation, then) evaluation, back-to-the-original-problem test, convergence,
+//              monotone mu, restoration stage matrices (k_ric<DYN, true> solves them)
+//   k_resto_b  p, n, t and bound-multiplier steps, fraction to the boundary, line-search reference values
+//   k_resto_ls filter line search of the restoration problem (no second-order correction, watchdog or soft step)
+// ---------------------------------------------------------------------------------------------
+template <int DYN>
+struct Resto {
+    static constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
+    // multiplier of restoration row i (the row's equality multiplier)
+    __device__ static double yrow(const Dims& dm, const Ws& ws, int b, int i) {
+        const int rt = NX + dm.N * NX, rq = rt + dm.nc;
+        return i < NX ? AT(yi, i) : i < rt ? AT(yk, i - NX) : i < rq ? AT(yt, i - rt) : AT(yd, i - rq);
+    }
+    // sum over the rows of p + n, and of log p + log n (wave-reduced)
+    __device__ static void pn_sums(const Dims& dm, const Ws& ws, int b, int lane, double al, double* lin, double* bar) {
+        const int ne = NX + dm.N * NX + dm.nc + (dm.N + 1) * dm.M;
+        double l = 0, g = 0;
+        for (int i = lane; i < ne; i += 64) {
+            const double pp = AT(rp, i) + al * AT(rdp, i), nn = AT(rn, i) + al * AT(rdn, i);
+            l += pp + nn;
+            g += log(pp) + log(nn);
+        }
+        *lin = wsum(l);
+        *bar = wsum(g);
+    }
+    // zeta / 2 ||D_R (x + al dx - x_R)||^2 over x = (X, U, S)
+    __device__ static double proximity(const Dims& dm, const Ws& ws, int b, int lane, double al) {
+        const double* ori = &AT(wdi, 0);
+        const int N = dm.N, oU = ws.L_X, oS = oU + ws.L_U;
+        double q = 0;
+        auto add = [&](double x, double xr) {
+            const double dr = fmin(1.0, 1.0 / fabs(xr)), v = dr * (x - xr);
+            q += v * v;
+        };
+        for (int i = lane; i < (N + 1) * NX; i += 64) add(AT(X, i) + al * AT(dX, i), ori[i]);
+        for (int i = lane; i < N * NU; i += 64) add(AT(U, i) + al * AT(dU, i), ori[oU + i]);
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) add(AT(S, k) + al * AT(dS, k), ori[oS + k]);
+        return 0.5 * SC(SC_ZETA) * wsum(q);
+    }
+};
+
+template <int DYN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_resto_a(
+    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+    const int* __restrict__ actr, const double* __restrict__ x0, const double* __restrict__ xg, int* cnt) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    using SV = Solver<DYN>;
+    using RS = Resto<DYN>;
+    constexpr int NX = SV::NX, NU = SV::NU;
+    const int lane = threadIdx.x, nlist = cnt[5];
+    // grid-stride over the restoration list (the host sizes the grid by a stale bound)
+    auto body = [&](const int b) {
+    if (SC(SC_RESTO) == 0.0) return;
+    const int ph = (int)SC(SC_PHASE);
+    if (ph != PH_RINIT && ph != PH_EVAL) return;
+    const bool init = ph == PH_RINIT;
+    const int N = dm.N, M = dm.M, nc = dm.nc, rank = (int)SC(SC_RANK);
+    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const double kappa_d = 1e-5;
+    const double* x0b = x0 + (size_t)b * NX;
+    const double* xgb = xg + (size_t)b * NX;
+    double* ori = &AT(wdi, 0);
+    const int oU = ws.L_X, oS = oU + ws.L_U, oT = oS + ws.L_S, oyi = oT + ws.L_T, oyk = oyi + ws.L_yi,
+              oyt = oyk + ws.L_yk, oyd = oyt + ws.L_yt, ozl = oyd + ws.L_yd, ozu = ozl + ws.L_zl, ozs = ozu + ws.L_zu,
+              ovt = ozs + ws.L_zs;
+    (void)oyi; (void)oyk; (void)oyt; (void)oyd;
+    // ---- evaluation at X: constraint values and Jacobians; the restoration multipliers weight Hd (0 at PH_RINIT)
+    for (int k = lane; k <= N; k += 64) {
+        double xk[NX], d[MMAX], gk[MMAX][3], w[MMAX], Hw[6];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i);
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) w[j] = (!init && j < M) ? AT(yd, k * M + j) : 0.0;
+        knot_eval(p, dm, ws, rank, k, xk, d, gk, w, Hw);
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) {
+            if (j >= M) break;
+            AT(dv, k * M + j) = d[j] + (dm.sd ? AT(S, k) : 0.0);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) AT(Jd, (k * M + j) * 3 + a) = gk[j][a];
+        }
+        for (int q = 0; q < 6; ++q) AT(Hd, k * 6 + q) = init ? 0.0 : Hw[q];
+    }
+    wsync();
+    // ---- the original constraints c(x) (IPOPT sign): theta_o = ||c||_1, pinf = ||c||_inf
+    for (int i = lane; i < NX; i += 64) AT(rci, i) = AT(X, i) - x0b[i];
+    for (int i = lane; i < nc; i += 64) AT(rct, i) = AT(X, N * NX + dm.tidx[i]) - xgb[dm.tidx[i]];
+    for (int k = lane; k < N; k += 64) {
+        double x[NX], u[NU], f[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+        for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+        Dyn<DYN>::f(x, u, p.wheelbase, f, p.dt);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
+    }
+    for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) = AT(dv, q) - AT(T, q);
+    wsync();
+    auto crow = [&](int i) {  // c of restoration row i
+        return i < NX ? AT(rci, i) : i < rt ? AT(rcd, i - NX) : i < rq ? AT(rct, i - rt) : AT(rcq, i - rq);
+    };
+    double th_o = 0, pinf = 0;
+    for (int i = lane; i < ne; i += 64) {
+        const double c = fabs(crow(i));
+        th_o += c;
+        pinf = fmax(pinf, c);
+    }
+    th_o = wsum(th_o);
+    pinf = wmax(pinf);
+    // the original barrier merit at this point with the original problem's mu: ln of every bound slack, the linear
+    // damping on one-sided ones
+    auto phi_orig = [&](double mu_o) {
+        double bar = 0, lin = 0;
+        for (int q = lane; q < (N + 1) * M; q += 64) {
+            bar += log(AT(T, q));
+            lin += AT(T, q);
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
+        }
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) {
+                bar += log(AT(S, k));
+                lin += AT(S, k);
+            }
+        return objective_w(p, dm, ws, b, lane, 0.0) - mu_o * wsum(bar) + kappa_d * mu_o * wsum(lin);
+    };
+    if (init) {
+        // MinC_1Nrm initialisation: x_R = x, mu = max(mu, ||c||_inf), p / n minimising the barrier problem for fixed
+        // x (IPOPT eq. (33)), bound multipliers capped at rho, equality multipliers 0
+        const double mu_o = SC(SC_MU), ph_R = phi_orig(mu_o);
+        iter_io(ws, b, lane, ori, true);
+        const double mu = fmax(mu_o, pinf), rho = o.resto_penalty_parameter;
+        wsync();
+        for (int i = lane; i < ne; i += 64) {
+            const double c = crow(i);
+            const double a = (mu - rho * c) / (2.0 * rho);
+            const double n = a + sqrt(a * a + mu * c / (2.0 * rho));
+            AT(rn, i) = n;
+            AT(rp, i) = c + n;
+            AT(rzp, i) = mu / (c + n);
+            AT(rzn, i) = mu / n;
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            AT(zl, e) = fmin(rho, AT(zl, e));
+            AT(zu, e) = fmin(rho, AT(zu, e));
+        }
+        for (int k = lane; k <= N; k += 64) AT(zs, k) = fmin(rho, AT(zs, k));
+        for (int q = lane; q < (N + 1) * M; q += 64) {
+            AT(vt, q) = fmin(rho, AT(vt, q));
+            AT(yd, q) = 0.0;
+        }
+        for (int i = lane; i < NX; i += 64) AT(yi, i) = 0.0;
+        for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0.0;
+        for (int i = lane; i < 8; i += 64) AT(yt, i) = 0.0;
+        wsync();
+        // the restoration's theta_max / theta_min from its merit at the start (proximity term 0 at x_R)
+        double th0 = 0;
+        for (int i = lane; i < ne; i += 64) th0 += fabs(crow(i) - AT(rp, i) + AT(rn, i));
+        th0 = wsum(th0);
+        if (lane == 0) {
+            SC(SC_RMUO) = mu_o;
+            SC(SC_RTAUO) = SC(SC_TAU);
+            SC(SC_RDWO) = SC(SC_DWLAST);
+            SC(SC_DWLAST) = 0.0;
+            SC(SC_THR) = th_o;
+            SC(SC_PHR) = ph_R;
+            SC(SC_RHO) = rho;
+            SC(SC_ZETA) = o.resto_proximity_weight * sqrt(mu);
+            SC(SC_RTHMAX) = 1e4 * fmax(1.0, th0);
+            SC(SC_RTHMIN) = 1e-4 * fmax(1.0, th0);
+            SC(SC_RNFILT) = 0;
+            SC(SC_MU) = mu;
+            SC(SC_TAU) = fmax(0.99, 1.0 - mu);
+            SC(SC_RFIRST) = 1;
+            SC(SC_PHASE) = PH_EVAL;
+            SC(SC_NRESTO) = SC(SC_NRESTO) + 1;
+        }
+        wsync();
+    }
+    const bool first = SC(SC_RFIRST) != 0.0;
+    const double rho = SC(SC_RHO), zeta = SC(SC_ZETA), mu0 = SC(SC_MU);
+    // ---- the restoration problem's residuals c(x) - p + n
+    for (int i = lane; i < NX; i += 64) AT(rci, i) += -AT(rp, i) + AT(rn, i);
+    for (int i = lane; i < N * NX; i += 64) AT(rcd, i) += -AT(rp, NX + i) + AT(rn, NX + i);
+    for (int j = lane; j < nc; j += 64) AT(rct, j) += -AT(rp, rt + j) + AT(rn, rt + j);
+    for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) += -AT(rp, rq + q) + AT(rn, rq + q);
+    wsync();
+    // ---- optimality measures of the restoration problem (oracle errors(), resto branch)
+    double dual = 0, primal = 0, c0 = 0, cmu = 0, ysum = 0, zsum = 0, nzc = 0;
+    auto dual_ = [&](double v) { dual = fmax(dual, fabs(v)); };
+    for (int k = lane; k <= N; k += 64) {
+        double r[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double xr = ori[k * NX + i], dr = fmin(1.0, 1.0 / fabs(xr));
+            r[i] = zeta * dr * dr * (AT(X, k * NX + i) - xr);
+        }
+        if (k > 0)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) r[i] += AT(yk, (k - 1) * NX + i);
+        double A[NX][NX], Bu[NX][NU];
+        if (k < N) {
+            double x[NX], u[NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) x[i] = AT(X, k * NX + i);
+#pragma unroll
+            for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i);
+            Dyn<DYN>::jac(x, u, p.dt, p.wheelbase, A, Bu);
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                double t = 0;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) t += A[i][j] * AT(yk, k * NX + i);
+                r[j] -= t;
+            }
+        }
+        if (k == 0)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) r[i] += AT(yi, i);
+        if (k == N)
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+                for (int cc = 0; cc < nc; ++cc)
+                    if (dm.tidx[cc] == i) r[i] += AT(yt, cc);
+        for (int j = 0; j < M; ++j)
+            for (int a = 0; a < 3 && a < NX; ++a) r[a] += AT(Jd, (k * M + j) * 3 + a) * AT(yd, k * M + j);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dual_(r[i]);
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                const double ur = ori[oU + k * NU + i], dr = fmin(1.0, 1.0 / fabs(ur));
+                double t = zeta * dr * dr * (AT(U, k * NU + i) - ur) - AT(zl, k * NU + i) + AT(zu, k * NU + i);
+#pragma unroll
+                for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
+                dual_(t);
+            }
+        if (dm.ns) {
+            const double sr = ori[oS + k], dr = fmin(1.0, 1.0 / fabs(sr));
+            double t = zeta * dr * dr * (AT(S, k) - sr) - AT(zs, k);
+            if (dm.sd)
+                for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
+            dual_(t);
+        }
+        for (int j = 0; j < M; ++j) dual_(-AT(yd, k * M + j) - AT(vt, k * M + j));
+    }
+    auto compl_ = [&](double z, double sl) {
+        c0 = fmax(c0, fabs(z * sl));
+        cmu = fmax(cmu, fabs(z * sl - mu0));
+        zsum += fabs(z);
+        nzc += 1;
+    };
+    for (int i = lane; i < ne; i += 64) {  // p and n rows: rho -+ y - z = 0, z p = mu, z n = mu
+        const double y = RS::yrow(dm, ws, b, i);
+        dual_(rho - y - AT(rzp, i));
+        dual_(rho + y - AT(rzn, i));
+        compl_(AT(rzp, i), AT(rp, i));
+        compl_(AT(rzn, i), AT(rn, i));
+        primal = fmax(primal, fabs(crow(i)));
+        ysum += fabs(y);
+    }
+    for (int e = lane; e < N * NU; e += 64) {
+        const double u = AT(U, e);
+        compl_(AT(zl, e), u - p.umin[e % NU]);
+        compl_(AT(zu, e), p.umax[e % NU] - u);
+    }
+    if (dm.ns)
+        for (int k = lane; k <= N; k += 64) compl_(AT(zs, k), AT(S, k));
+    for (int q = lane; q < (N + 1) * M; q += 64) compl_(AT(vt, q), AT(T, q));
+    dual = wmax(dual);
+    primal = wmax(primal);
+    c0 = wmax(c0);
+    cmu = wmax(cmu);
+    zsum = wsum(zsum);
+    ysum = wsum(ysum);
+    nzc = wsum(nzc);
+    const double sd = fmax(100.0, (ysum + zsum) / ((double)ne + nzc)) / 100.0;
+    const double scc = fmax(100.0, zsum / nzc) / 100.0;
+    const double E0 = fmax(fmax(dual / sd, primal), c0 / scc);
+    const int iters = (int)SC(SC_ITERS);
+    wsync();
+    auto finish = [&](int status) {
+        if (lane == 0) {
+            SC(SC_E0) = E0;
+            SC(SC_STATUS) = status;
+            SC(SC_PHASE) = PH_DONE;
+        }
+    };
+    if (!isfinite(E0)) return finish(NLOT_NUMERIC);
+    if (!first) {
+        // RestoConvergenceCheck: back to the original problem once theta_o <= kappa_resto theta_R and the point is
+        // acceptable to the original filter (sufficient decrease against (theta_R, phi_R))
+        const double mu_o = SC(SC_RMUO), th_R = SC(SC_THR), ph_R = SC(SC_PHR);
+        const double ph_o = phi_orig(mu_o);
+        const double gt = 1e-5, gp = 1e-8;
+        int bad = 0;
+        const int nf = (int)SC(SC_NFILT);
+        for (int i = lane; i < nf; i += 64)
+            if (!(th_o <= AT(filt, 2 * i) || ph_o <= AT(filt, 2 * i + 1))) bad = 1;
+        const bool back = th_o <= o.required_infeasibility_reduction * th_R && wmax((double)bad) == 0.0 &&
+                          (cmp_le(th_o, (1.0 - gt) * th_R, th_R) || cmp_le(ph_o - ph_R, -gp * th_R, ph_R));
+        if (back) {
+            // leave the restoration phase: the bound multipliers of the original problem take one complementarity
+            // Newton step from their saved values over the whole phase (fraction to the boundary with the original
+            // tau), reset to 1 above bound_mult_reset_threshold; the equality multipliers restart at 0
+            const double tau_o = SC(SC_RTAUO);
+            double az = 1.0, zmax = 0;
+            auto dz = [&](double z, double so, double sn) { return (mu_o - z * sn) / so; };
+            for (int e = lane; e < N * NU; e += 64) {
+                const double lo = p.umin[e % NU], hi = p.umax[e % NU], uo = ori[oU + e], un = AT(U, e);
+                AT(dzl, e) = dz(ori[ozl + e], uo - lo, un - lo);
+                AT(dzu, e) = dz(ori[ozu + e], hi - uo, hi - un);
+                az = frac_to_bound(ori[ozl + e], AT(dzl, e), tau_o, az);
+                az = frac_to_bound(ori[ozu + e], AT(dzu, e), tau_o, az);
+            }
+            if (dm.ns)
+                for (int k = lane; k <= N; k += 64) {
+                    AT(dzs, k) = dz(ori[ozs + k], ori[oS + k], AT(S, k));
+                    az = frac_to_bound(ori[ozs + k], AT(dzs, k), tau_o, az);
+                }
+            for (int q = lane; q < (N + 1) * M; q += 64) {
+                AT(dvt, q) = dz(ori[ovt + q], ori[oT + q], AT(T, q));
+                az = frac_to_bound(ori[ovt + q], AT(dvt, q), tau_o, az);
+            }
+            az = wmin(az);
+            for (int e = lane; e < N * NU; e += 64) {
+                AT(zl, e) = ori[ozl + e] + az * AT(dzl, e);
+                AT(zu, e) = ori[ozu + e] + az * AT(dzu, e);
+                zmax = fmax(zmax, fmax(AT(zl, e), AT(zu, e)));
+            }
+            if (dm.ns)
+                for (int k = lane; k <= N; k += 64) {
+                    AT(zs, k) = ori[ozs + k] + az * AT(dzs, k);
+                    zmax = fmax(zmax, AT(zs, k));
+                }
+            for (int q = lane; q < (N + 1) * M; q += 64) {
+                AT(vt, q) = ori[ovt + q] + az * AT(dvt, q);
+                zmax = fmax(zmax, AT(vt, q));
+                AT(yd, q) = 0.0;
+            }
+            zmax = wmax(zmax);
+            if (zmax > o.bound_mult_reset_threshold) {
+                for (int e = lane; e < N * NU; e += 64) AT(zl, e) = AT(zu, e) = 1.0;
+                for (int k = lane; k <= N; k += 64) AT(zs, k) = 1.0;
+                for (int q = lane; q < (N + 1) * M; q += 64) AT(vt, q) = 1.0;
+            }
+            for (int i = lane; i < NX; i += 64) AT(yi, i) = 0.0;
+            for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0.0;
+            for (int i = lane; i < 8; i += 64) AT(yt, i) = 0.0;
+            wsync();
+            if (lane == 0) {  // k_iter_a (launched next) takes the instance's iteration from this evaluation
+                SC(SC_MU) = mu_o;
+                SC(SC_TAU) = tau_o;
+                SC(SC_DWLAST) = SC(SC_RDWO);
+                SC(SC_RESTO) = 0;
+                SC(SC_INSOFT) = 0;
+                SC(SC_SOFTCNT) = 0;
+                SC(SC_WD) = 0;
+                SC(SC_WDSHORT) = 0;
+                SC(SC_TINYLAST) = 0;
+            }
+            return;
+        }
+        if (E0 <= o.tol) {  // the restoration problem converged at a point the original problem does not accept
+            const double thr = o.resto_failure_feasibility_threshold > 0 ? o.resto_failure_feasibility_threshold
+                                                                          : 1e2 * o.tol;
+            return finish(pinf <= thr ? NLOT_RESTO_FAILED : NLOT_INFEASIBLE);
+        }
+    }
+    if (lane == 0) SC(SC_RFIRST) = 0;
+    if (iters >= o.max_iter) return finish(NLOT_MAXITER);
+    // ---- monotone barrier update inside the restoration phase
+    const double kap = o.barrier_tol_factor, mu_floor = fmin(o.tol, o.compl_inf_tol) / (kap + 1.0);
+    double mu = mu0, tau = SC(SC_TAU);
+    bool reset_filter = false;
+    for (;;) {
+        const double Emu = fmax(fmax(dual / sd, primal), cmu / scc);
+        if (Emu > kap * mu) break;
+        const double nm = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_floor);
+        if (nm >= mu) break;
+        mu = nm;
+        tau = fmax(0.99, 1.0 - mu);
+        reset_filter = true;
+        double cm = 0;
+        auto cmx = [&](double z, double sl) { cm = fmax(cm, fabs(z * sl - mu)); };
+        for (int i = lane; i < ne; i += 64) {
+            cmx(AT(rzp, i), AT(rp, i));
+            cmx(AT(rzn, i), AT(rn, i));
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            const double u = AT(U, e);
+            cmx(AT(zl, e), u - p.umin[e % NU]);
+            cmx(AT(zu, e), p.umax[e % NU] - u);
+        }
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) cmx(AT(zs, k), AT(S, k));
+        for (int q = lane; q < (N + 1) * M; q += 64) cmx(AT(vt, q), AT(T, q));
+        cmu = wmax(cm);
+    }
+    wsync();
+    if (lane == 0) {
+        SC(SC_MU) = mu;
+        SC(SC_TAU) = tau;
+        if (reset_filter) SC(SC_RNFILT) = 0;
+    }
+    wsync();
+    SV::build_stages_resto(p, dm, ws, b, lane, 0.0, mu, &AT(stg, 0));
+    if (lane == 0) {
+        SC(SC_E0) = E0;
+        SC(SC_RMU0) = mu;
+        SC(SC_RMU1) = 0.0;
+        SC(SC_RNR) = 1;
+        SC(SC_USEQF) = 0.0;
+        SC(SC_RICFIX) = -1.0;
+        SC(SC_RIC) = 1;
+        atomicAdd(&cnt[4], 1);
+    }
+    };
+    for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
+        body(actr[idx]);
+        wsync();
+    }
+}
+
+template <int DYN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_resto_b(
+    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+    const int* __restrict__ actr, int* cnt, float* tp) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    using RS = Resto<DYN>;
+    constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
+    const int lane = threadIdx.x, nlist = cnt[5];
+    auto body = [&](const int b) {
+    if (SC(SC_RESTO) == 0.0 || (int)SC(SC_RIC) != 2) return;
+    (void)o;
+    const int N = dm.N, M = dm.M, nc = dm.nc;
+    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const double kappa_d = 1e-5, dw = SC(SC_DW), mu = SC(SC_MU), tau = SC(SC_TAU), rho = SC(SC_RHO),
+                 zeta = SC(SC_ZETA);
+    const double* ori = &AT(wdi, 0);
+    const int oU = ws.L_X, oS = oU + ws.L_U;
+    double amax = 1.0, az = 1.0, gd = 0;
+    // p, n and their multipliers' steps of row r given its new multiplier yn (oracle PN_STEP)
+    auto pn_step = [&](int r, double yn) {
+        const double pp = AT(rp, r), nn = AT(rn, r);
+        const double sp = AT(rzp, r) / pp + dw, sn = AT(rzn, r) / nn + dw;
+        const double dp = (yn - rho - kappa_d * mu + mu / pp) / sp, dn = (-yn - rho - kappa_d * mu + mu / nn) / sn;
+        const double dzp = mu / pp - AT(rzp, r) - (AT(rzp, r) / pp) * dp, dzn = mu / nn - AT(rzn, r) - (AT(rzn, r) / nn) * dn;
+        AT(rdp, r) = dp;
+        AT(rdn, r) = dn;
+        AT(rdzp, r) = dzp;
+        AT(rdzn, r) = dzn;
+        amax = frac_to_bound(pp, dp, tau, amax);
+        amax = frac_to_bound(nn, dn, tau, amax);
+        az = frac_to_bound(AT(rzp, r), dzp, tau, az);
+        az = frac_to_bound(AT(rzn, r), dzn, tau, az);
+        gd += (rho + kappa_d * mu - mu / pp) * dp + (rho + kappa_d * mu - mu / nn) * dn;
+    };
+    for (int k = lane; k <= N; k += 64) {
+        for (int j = 0; j < M; ++j) {  // t, p and n of the inequality row from its new multiplier y~
+            const int q = k * M + j, r = rq + q;
+            double Jdz = 0;
+            for (int a = 0; a < 3 && a < NX; ++a) Jdz += AT(Jd, q * 3 + a) * AT(dX, k * NX + a);
+            if (dm.sd) Jdz += AT(dS, k);
+            const double t = AT(T, q), v = AT(vt, q), pp = AT(rp, r), nn = AT(rn, r);
+            const double st = v / t + dw, sp = AT(rzp, r) / pp + dw, sn = AT(rzn, r) / nn + dw;
+            const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+            const double E = (mu / t - kappa_d * mu) / st + (mu / pp - rho - kappa_d * mu) / sp -
+                             (mu / nn - rho - kappa_d * mu) / sn;
+            const double yn = (Jdz + AT(rcq, q) - E) / C;
+            const double dt_ = (yn + mu / t - kappa_d * mu) / st;
+            const double dvt_ = mu / t - v - (v / t) * dt_;
+            AT(yd_n, q) = yn;
+            AT(dT, q) = dt_;
+            AT(dvt, q) = dvt_;
+            pn_step(r, yn);
+            amax = frac_to_bound(t, dt_, tau, amax);
+            az = frac_to_bound(v, dvt_, tau, az);
+            gd += (-mu / t + kappa_d * mu) * dt_;
+        }
+        if (dm.ns) {
+            const double s_ = AT(S, k), ds = AT(dS, k), sr = ori[oS + k], dr = fmin(1.0, 1.0 / fabs(sr));
+            const double dzs_ = mu / s_ - AT(zs, k) - (AT(zs, k) / s_) * ds;
+            AT(dzs, k) = dzs_;
+            amax = frac_to_bound(s_, ds, tau, amax);
+            az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+            gd += (zeta * dr * dr * (s_ - sr) - mu / s_ + kappa_d * mu) * ds;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double xr = ori[k * NX + i], dr = fmin(1.0, 1.0 / fabs(xr));
+            gd += zeta * dr * dr * (AT(X, k * NX + i) - xr) * AT(dX, k * NX + i);
+        }
+    }
+    for (int i = lane; i < NX; i += 64) pn_step(i, AT(yi_n, i));
+    for (int i = lane; i < N * NX; i += 64) pn_step(NX + i, AT(yk_n, i));
+    for (int j = lane; j < nc; j += 64) pn_step(rt + j, AT(yt_n, j));
+    for (int e = lane; e < N * NU; e += 64) {
+        const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = AT(dU, e);
+        const double ur = ori[oU + e], dr = fmin(1.0, 1.0 / fabs(ur));
+        const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * du;
+        const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * du;
+        AT(dzl, e) = dzl_;
+        AT(dzu, e) = dzu_;
+        amax = frac_to_bound(sl, du, tau, amax);
+        amax = frac_to_bound(su, -du, tau, amax);
+        az = frac_to_bound(AT(zl, e), dzl_, tau, az);
+        az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+        gd += (zeta * dr * dr * (u - ur) - mu / sl + mu / su) * du;
+    }
+    amax = wmin(amax);
+    az = wmin(az);
+    gd = wsum(gd);
+    // the restoration merit at the current point: theta = ||c - p + n||_1, phi = its objective - mu sum ln(bound
+    // slacks incl. p, n) + kappa_d mu sum(one-sided slacks)
+    double th = 0, bar = 0, lin = 0;
+    for (int i = lane; i < NX; i += 64) th += fabs(AT(rci, i));
+    for (int i = lane; i < nc; i += 64) th += fabs(AT(rct, i));
+    for (int i = lane; i < N * NX; i += 64) th += fabs(AT(rcd, i));
+    for (int q = lane; q < (N + 1) * M; q += 64) {
+        th += fabs(AT(rcq, q));
+        bar += log(AT(T, q));
+        lin += AT(T, q);
+    }
+    for (int e = lane; e < N * NU; e += 64) {
+        const double u = AT(U, e);
+        bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
+    }
+    if (dm.ns)
+        for (int k = lane; k <= N; k += 64) {
+            bar += log(AT(S, k));
+            lin += AT(S, k);
+        }
+    double pn_lin, pn_bar;
+    RS::pn_sums(dm, ws, b, lane, 0.0, &pn_lin, &pn_bar);
+    const double theta = wsum(th);
+    const double phi = rho * pn_lin + RS::proximity(dm, ws, b, lane, 0.0) - mu * (wsum(bar) + pn_bar) +
+                       kappa_d * mu * (wsum(lin) + pn_lin);
+    const double gt = 1e-5, gp = 1e-8;
+    double amin = gt;
+    if (gd < 0) {
+        amin = fmin(gt, gp * theta / (-gd));
+        if (theta <= SC(SC_RTHMIN)) amin = fmin(amin, pow(theta, 1.1) / pow(-gd, 2.3));
+    }
+    amin *= 0.05;
+    (void)ne;
+    wsync();
+    if (lane == 0) {
+        SC(SC_RIC) = 0;
+        SC(SC_THETA) = theta;
+        SC(SC_PHI) = phi;
+        SC(SC_GD) = gd;
+        SC(SC_AMAX) = amax;
+        SC(SC_AMIN) = amin;
+        SC(SC_AZ) = az;
+        SC(SC_ALPHA) = amax;
+        SC(SC_TRIALS) = 0;
+        SC(SC_TINY) = 0;
+        SC(SC_PHASE) = PH_LS;
+    }
+    wsync();
+    emit_points(p, dm, ws, b, lane, cnt, true, tp, 1, amax);
+    };
+    for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
+        body(actr[idx]);
+        wsync();
+    }
+}
+
+template <int DYN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_resto_ls(
+    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
+    const int* __restrict__ actr, const double* __restrict__ x0, const double* __restrict__ xg, int* cnt,
+    int* cnt_next, float* tp_next, const float* tval, int nspec_next) {
+    const NlotProblem& p = *pp_;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    using RS = Resto<DYN>;
+    constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
+    const int lane = threadIdx.x, nlist = cnt[5];
+    auto body = [&](const int b) {
+    if (SC(SC_RESTO) == 0.0 || (int)SC(SC_PHASE) != PH_LS) return;
+    (void)o;
+    const int N = dm.N, M = dm.M, nc = dm.nc;
+    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const double a0 = SC(SC_ALPHA), mu = SC(SC_MU), rho = SC(SC_RHO), kappa_d = 1e-5;
+    const int rank0 = (int)SC(SC_RANK), ncand = (int)SC(SC_NCAND);
+    const double* x0b = x0 + (size_t)b * NX;
+    const double* xgb = xg + (size_t)b * NX;
+    const double gt = 1e-5, gp = 1e-8, delta = 1.0, sth = 1.1, sph = 2.3, eta = 1e-8;
+    // the restoration merit at x + al d, p + al dp, n + al dn (trial-list slot `rank`)
+    auto trial = [&](double al, int rank, double* th_o, double* ph_o) {
+        double th = 0, bar = 0, lin = 0;
+        auto pr = [&](int r) { return (AT(rp, r) + al * AT(rdp, r)) - (AT(rn, r) + al * AT(rdn, r)); };
+        for (int i = lane; i < NX; i += 64) th += fabs(AT(X, i) + al * AT(dX, i) - x0b[i] - pr(i));
+        for (int cc = lane; cc < nc; cc += 64) {
+            const int ix = N * NX + dm.tidx[cc];
+            th += fabs(AT(X, ix) + al * AT(dX, ix) - xgb[dm.tidx[cc]] - pr(rt + cc));
+        }
+        for (int k = lane; k <= N; k += 64) {
+            double xk[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xk[i] = AT(X, k * NX + i) + al * AT(dX, k * NX + i);
+            if (k < N) {
+                double u[NU], f[NX];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[i] = AT(U, k * NU + i) + al * AT(dU, k * NU + i);
+                Dyn<DYN>::f(xk, u, p.wheelbase, f, p.dt);
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+                    th += fabs(AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]) -
+                               pr(NX + k * NX + i));
+#pragma unroll
+                for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+            }
+            double d[MMAX];
+            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
+            const double sk = AT(S, k) + al * AT(dS, k);
+            for (int j = 0; j < M; ++j) {
+                const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
+                th += fabs(d[j] + (dm.sd ? sk : 0.0) - t - pr(rq + k * M + j));
+                bar += log(t);
+                lin += t;
+            }
+            if (dm.ns) {
+                bar += log(sk);
+                lin += sk;
+            }
+        }
+        double pn_lin, pn_bar;
+        RS::pn_sums(dm, ws, b, lane, al, &pn_lin, &pn_bar);
+        *th_o = wsum(th);
+        *ph_o = rho * pn_lin + RS::proximity(dm, ws, b, lane, al) - mu * (wsum(bar) + pn_bar) +
+                kappa_d * mu * (wsum(lin) + pn_lin);
+    };
+    const double rth = SC(SC_THETA), rph = SC(SC_PHI), rgd = SC(SC_GD);
+    const int nf = (int)SC(SC_RNFILT);
+    auto acceptable = [&](double at, double th, double pht, int* fa) {  // against the restoration's filter
+        int ok = isfinite(th) && isfinite(pht) && th <= SC(SC_RTHMAX);
+        const int ftype = rgd < 0 && at * pow(-rgd, sph) > delta * pow(rth, sth);
+        const int armijo = cmp_le(pht - rph, eta * at * rgd, rph);
+        if (ok) {
+            if (ftype && rth <= SC(SC_RTHMIN)) {
+                ok = armijo;
+            } else {
+                ok = cmp_le(th, (1.0 - gt) * rth, rth) || cmp_le(pht - rph, -gp * rth, rph);
+                if (ok && pht > rph) {
+                    const double bas = fabs(rph) > 10.0 ? log10(fabs(rph)) : 1.0;
+                    if (log10(pht - rph) > 5.0 + bas) ok = 0;
+                }
+            }
+        }
+        if (ok) {
+            int bad = 0;
+            for (int i = lane; i < nf; i += 64)
+                if (!(th <= AT(rfilt, 2 * i) || pht <= AT(rfilt, 2 * i + 1))) bad = 1;
+            ok = wmax((double)bad) == 0.0;
+        }
+        *fa = ok && ftype && armijo;
+        return ok;
+    };
+    int ok = 0, fa = 0, cnd = 0;
+    double al = a0;
+    for (cnd = 0; cnd < ncand && !ok; ++cnd) {
+        al = ldexp(a0, -cnd);
+        double th, pht;
+        trial(al, rank0 + cnd, &th, &pht);
+        ok = acceptable(al, th, pht, &fa);
+    }
+    wsync();
+    if (!ok) {
+        const double na = ldexp(a0, -ncand);
+        if (lane == 0) {
+            SC(SC_ALPHA) = na;
+            SC(SC_TRIALS) = SC(SC_TRIALS) + ncand;
+            if (na < SC(SC_AMIN)) {  // the restoration phase's line search failed: IPOPT Restoration_Failed
+                SC(SC_STATUS) = NLOT_RESTO_FAILED;
+                SC(SC_PHASE) = PH_DONE;
+            }
+        }
+        wsync();
+        if (!(na < SC(SC_AMIN))) emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
+        return;
+    }
+    if (!fa && lane == 0) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph);
+    // accept: primal, p, n and equality multipliers with alpha; bound multipliers (z_p, z_n included) with alpha_z
+    const double az = SC(SC_AZ), ks = 1e10;
+    auto zupd = [&](double z, double dz, double sl) {
+        const double zn = z + az * dz;
+        return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
+    };
+    for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
+    for (int e = lane; e < N * NU; e += 64) {
+        const double u = AT(U, e) + al * AT(dU, e);
+        AT(U, e) = u;
+        AT(zl, e) = zupd(AT(zl, e), AT(dzl, e), u - p.umin[e % NU]);
+        AT(zu, e) = zupd(AT(zu, e), AT(dzu, e), p.umax[e % NU] - u);
+    }
+    if (dm.ns)
+        for (int k = lane; k <= N; k += 64) {
+            const double s_ = AT(S, k) + al * AT(dS, k);
+            AT(S, k) = s_;
+            AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s_);
+        }
+    for (int q = lane; q < (N + 1) * M; q += 64) {
+        const double t = AT(T, q) + al * AT(dT, q);
+        AT(T, q) = t;
+        AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), t);
+        AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
+    }
+    for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
+    for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
+    for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
+    for (int i = lane; i < ne; i += 64) {
+        const double pp = AT(rp, i) + al * AT(rdp, i), nn = AT(rn, i) + al * AT(rdn, i);
+        AT(rp, i) = pp;
+        AT(rn, i) = nn;
+        AT(rzp, i) = zupd(AT(rzp, i), AT(rdzp, i), pp);
+        AT(rzn, i) = zupd(AT(rzn, i), AT(rdzn, i), nn);
+    }
+    wsync();
+    if (lane == 0) {
+        SC(SC_ITERS) = SC(SC_ITERS) + 1;
+        SC(SC_PHASE) = PH_EVAL;
+        SC(SC_ACCSLOT) = (double)(rank0 + cnd - 1);
+    }
+    wsync();
+    emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+    };
+    for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
+        body(actr[idx]);
+        wsync();
+    }
 }
 
 __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
@@ -2837,10 +4156,10 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
     }
     for (int i = 0; i < p->nu; ++i)
         if (!(p->umin[i] < p->umax[i])) { set_error("control bounds must satisfy min < max"); return NLOT_ERR_INVALID; }
-    if (o->resto != 0 || o->soft_resto_pderror_reduction_factor > 0) {
-        set_error("the feasibility restoration phase (resto = 1, soft restoration) runs only in the CPU oracle; the GPU "
-                  "path ends an instance with NLOT_LS_FAILED where IPOPT would restore: pass resto = 0 and "
-                  "soft_resto_pderror_reduction_factor = 0 (DESIGN.md §4)");
+    if (o->max_iter < 0 || o->max_iter > 10000000) { set_error("max_iter must be in [0, 1e7]"); return NLOT_ERR_INVALID; }
+    if (o->resto && (o->resto_penalty_parameter <= 0 || o->required_infeasibility_reduction <= 0 ||
+                     o->required_infeasibility_reduction >= 1 || o->resto_proximity_weight < 0)) {
+        set_error("restoration options: rho > 0, 0 < kappa_resto < 1, proximity weight >= 0");
         return NLOT_ERR_INVALID;
     }
     if (o->max_soc < 0 || o->watchdog_shortened_iter_trigger < 0 || o->watchdog_trial_iter_max < 0) {
@@ -2925,7 +4244,11 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
     int kpipe = KPIPE;
     if (const char* e = getenv("NLOT_PIPE")) kpipe = std::max(1, std::min(KPIPE, atoi(e)));
-    const int max_steps = (o.max_iter + 2) * 64;
+    // a safety net against a phase-machine bug, not an iteration limit (max_iter bounds every instance): at most
+    // 64 global steps per iteration per admission wave
+    const int64_t waves = (B + std::max(1, o.max_active > 0 && o.max_active < Bi ? o.max_active : Bi) - 1) /
+                          std::max(1, o.max_active > 0 && o.max_active < Bi ? o.max_active : Bi);
+    const int64_t max_steps = ((int64_t)o.max_iter + 2) * 64 * (waves + 1);
     // Continuous batching (o.max_active = capacity < B): the first `capacity` instances start; whenever a host
     // synchronisation finds at least capacity / 32 slots free, the next instances (index order) join the active
     // list and run their INIT step (corners, slack push, least-squares multipliers) in the next step.  Every
@@ -2935,73 +4258,22 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     const int min_admit = std::max(1, capacity / 32);
     int next_admit = capacity;
     bool init_step = true;  // this step runs the INIT pass (step 0, and the step after an admission)
-    int rc = NLOT_OK, n_active = capacity, cur = 0;
+    // grid bound of the restoration kernels (they read the exact list count on the device): every active instance
+    // until a synchronisation shows how many are restoring (an instance enters at most one step before)
+    int resto_bound = o.resto ? Bi : 0;
+    int rc = NLOT_OK, n_active = capacity, cur = 0, synced = 0;
+    int64_t step = 0;
     NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 16 * sizeof(int), st));
     res.hcnt[0] = capacity;  // step 0's active count (cnt[2] of counter set 0)
     NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
-    for (int step = 0; step < max_steps && n_active > 0; ++step) {
-        const int* act = ws.act[cur];
-        int* nxt = ws.act[cur ^ 1];
-        const int kq = step % kpipe;
-        hipEvent_t* ev = res.ev[kq];
-        // Point lists are appended to by the kernel that moves an instance into the phase needing them
-        // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
-        // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
-        const int q = step & 1;
-        int* C = ws.cnt + 8 * q;
-        int* Cn = ws.cnt + 8 * (q ^ 1);
-        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, 8 * sizeof(int), st));
-        // speculative backtracking only while the GPU is latency-bound (few active instances); in the
-        // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
-        const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
-        if (use_mlp) {
-            if (init_step) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
-            if (ev[0]) hipEventRecord(ev[0], st);
-            // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
-            MlpReuse ru = reuse[q ^ 1];  // the previous step's trial list
-            ru.nreused = C + 3;          // statistics: points whose forward was reused
-            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, C + 0, (int)P, 0, nullptr, mo, true, st, &ru);
-            if (rc) break;
-            if (ev[0]) hipEventRecord(ev[1], st);
-        }
-        if (ev[4]) hipEventRecord(ev[4], st);
-        if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
-            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C);
-            hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
-                               dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ);
-        }
-        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C);
-        if (ev[6]) hipEventRecord(ev[6], st);
-        hipLaunchKernelGGL(k_ric<DYN>, dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st, dP, dD,
-                           dW, act, n_active, C + 2, (int)MODE_NEWTON);
-        if (ev[6]) hipEventRecord(ev[7], st);
-        hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
-                           use_mlp ? ws.tpts[q] : nullptr);
-        if (ev[4]) hipEventRecord(ev[5], st);
-        if (use_mlp) {
-            if (ev[0]) hipEventRecord(ev[2], st);
-            rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
-                                    mo_t[q], false, st);
-            if (rc) break;
-            if (ev[0]) hipEventRecord(ev[3], st);
-        }
-        // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
-        // starts at most KPIPE steps late; the accepted alpha is the same either way)
-        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, x0, xg, C, Cn,
-                           use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
-        NLOT_HIP_CHECK(hipGetLastError());
-        // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
-        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 16 * kq, ws.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
-        cur ^= 1;
-        init_step = false;
-        if (kq != kpipe - 1) continue;
-        NLOT_HIP_CHECK(hipStreamSynchronize(st));
-        for (int j = 0; j <= kq; ++j) {  // steps step - kq .. step
-            const int sj = step - kq + j, qj = sj & 1;
+    // fold the counters of steps synced .. last into g_stats (after a synchronisation); updates n_active
+    auto fold = [&](int64_t last) {
+        for (int64_t sj = synced; sj <= last; ++sj) {
+            const int j = (int)(sj % kpipe), qj = (int)(sj & 1);
             const int* hc = res.hcnt + 16 * j + 8 * qj;
             const int next_active = res.hcnt[16 * j + 8 * (qj ^ 1) + 2];
-            g_stats.iterations = sj + 1;
+            g_stats.iterations = (int)(sj + 1);
             if (use_mlp) {
                 g_stats.mlp_points_full += (int64_t)hc[0] * P;
                 g_stats.mlp_points_value += (int64_t)hc[1] * P;
@@ -3027,8 +4299,88 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
                 g_stats.ric_ms += r;
             }
             n_active = next_active;
-            if (n_active == 0) break;  // the later steps of this batch found nothing to do
+            if (n_active == 0) break;  // the later steps of this window found nothing to do
         }
+        synced = last + 1;
+    };
+    for (step = 0; step < max_steps && n_active > 0; ++step) {
+        const int* act = ws.act[cur];
+        int* nxt = ws.act[cur ^ 1];
+        const int* actr = ws.actr[cur];
+        int* nxtr = ws.actr[cur ^ 1];
+        const int kq = step % kpipe;
+        hipEvent_t* ev = res.ev[kq];
+        // Point lists are appended to by the kernel that moves an instance into the phase needing them
+        // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
+        // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
+        const int q = step & 1;
+        int* C = ws.cnt + 8 * q;
+        int* Cn = ws.cnt + 8 * (q ^ 1);
+        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, 8 * sizeof(int), st));
+        // speculative backtracking only while the GPU is latency-bound (few active instances); in the
+        // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
+        const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
+        if (use_mlp) {
+            if (init_step) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
+            if (ev[0]) hipEventRecord(ev[0], st);
+            // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
+            MlpReuse ru = reuse[q ^ 1];  // the previous step's trial list
+            ru.nreused = C + 3;          // statistics: points whose forward was reused
+            rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, C + 0, (int)P, 0, nullptr, mo, true, st, &ru);
+            if (rc) break;
+            if (ev[0]) hipEventRecord(ev[1], st);
+        }
+        if (ev[4]) hipEventRecord(ev[4], st);
+        if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C, Cn);
+            hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
+                               st, dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ);
+        }
+        // restoration phases (list actr, count C[5]): before k_iter_a, which continues the iteration of an instance
+        // that k_resto_a returns to the original problem
+        const int n_resto = std::min(n_active, resto_bound);
+        if (n_resto > 0)
+            hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, x0, xg, C);
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C, Cn);
+        if (ev[6]) hipEventRecord(ev[6], st);
+        hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
+                           dP, dD, dW, act, n_active, C + 2, (int)MODE_NEWTON);
+        if (ev[6]) hipEventRecord(ev[7], st);
+        if (n_resto > 0)
+            hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
+                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON);
+        hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
+                           use_mlp ? ws.tpts[q] : nullptr, Cn);
+        if (n_resto > 0)
+            hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, C,
+                               use_mlp ? ws.tpts[q] : nullptr);
+        if (ev[4]) hipEventRecord(ev[5], st);
+        if (use_mlp) {
+            if (ev[0]) hipEventRecord(ev[2], st);
+            rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
+                                    mo_t[q], false, st);
+            if (rc) break;
+            if (ev[0]) hipEventRecord(ev[3], st);
+        }
+        // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
+        // starts at most KPIPE steps late; the accepted alpha is the same either way)
+        if (n_resto > 0)
+            hipLaunchKernelGGL(k_resto_ls<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, x0, xg, C, Cn,
+                               use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
+        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, nxtr, x0, xg, C, Cn,
+                           use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
+        NLOT_HIP_CHECK(hipGetLastError());
+        // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
+        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 16 * kq, ws.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
+        cur ^= 1;
+        init_step = false;
+        if (kq != kpipe - 1) continue;
+        NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        // restoration lists of the window: the next launches' grid bound (their kernels read the exact count)
+        int rmax = 0;
+        for (int j = 0; j <= kq; ++j) rmax = std::max(rmax, res.hcnt[16 * j + 8 * (((step - kq + j) & 1) ^ 1) + 5]);
+        resto_bound = std::min(Bi, 2 * rmax + 256);
+        fold(step);
         if (next_admit < Bi && (capacity - n_active >= min_admit || n_active == 0)) {
             // append instances next_admit .. next_admit + n_new - 1 to the next step's active list and count
             const int n_new = std::min(capacity - n_active, Bi - next_admit);
@@ -3041,6 +4393,14 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         }
     }
     if (rc) return rc;
+    if (synced < step) {  // a window the loop left before its synchronisation point
+        NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        fold(step - 1);
+    }
+    if (n_active > 0 || next_admit < Bi) {
+        set_error("nlot_solve_batch: the global step cap was reached with instances unfinished (phase-machine bug)");
+        return NLOT_ERR_INVALID;
+    }
     hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);
     NLOT_HIP_CHECK(hipGetLastError());
     NLOT_HIP_CHECK(hipStreamSynchronize(st));

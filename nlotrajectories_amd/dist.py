@@ -56,3 +56,15 @@ def sum_over_ranks(n: int, device) -> int:
     t = torch.tensor([n], dtype=torch.int64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def gather_rank_rows(row, device):
+    """Every rank's small float vector (the same length on all ranks) as a [world, len] list on every rank
+    (one all_gather): per-rank status counts and iteration tails, so straggler imbalance is visible."""
+    row = [float(v) for v in row]
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [row]
+    t = torch.tensor(row, dtype=torch.float64, device=_coll_device(device))
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]

@@ -2393,7 +2393,14 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     }
     free(tb);
     (void)lin_resid;
-    if (status) return status;
+    if (status) {
+        /* the instance ends inside the restoration phase: its output is the restoration iterate (the GPU solver's
+         * arrays hold it); IPOPT would report the original problem's last iterate */
+        memcpy(s->X, r->X, sizeof(double) * (N + 1) * nx);
+        memcpy(s->U, r->U, sizeof(double) * N * nu);
+        memcpy(s->S, r->S, sizeof(double) * (N + 1));
+        return status;
+    }
     /* back to the regular problem */
     double* zold = (double*)malloc(sizeof(double) * 4 * (2 * N * nu + (N + 1) + (N + 1) * M));
     const double mu0 = s->mu;
@@ -2445,7 +2452,8 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
 
 /* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
  * seen, [4] = final mu, [5] = E_0 (scaled overall error), [6] = restoration phases, [7] = watchdog /
- * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny) */
+ * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny),
+ * [8] = theta (1-norm) at the last line-search failure, -1 if none.  info holds >= 9 doubles. */
 int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
                      const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
                      int* iters_out, double* info) {
@@ -2528,6 +2536,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
     double* wd_dir = wd_it + nit;
     int in_wd = 0, wd_short = 0, wd_trial = 0, in_soft = 0, soft_cnt = 0, tiny_last = 0;
     int n_resto = 0, n_wd = 0, n_soft = 0, n_tiny = 0;
+    double theta_fail = -1.0; /* theta of the last iterate whose line search failed (diagnostic) */
     LsRef wd_ref = {0, 0, 0, 0, 1};
     double wd_amax = 1, wd_az = 1, wd_amin = 0, wd_mu = 0, wd_tau = 0;
     for (;;) {
@@ -2785,12 +2794,23 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                     iter, s->mu, s->f, theta, E0, e.dual, dw, amax, alpha, azz, s->nfilt, in_wd ? " W" : "",
                     in_soft ? " s" : "", is_tiny ? " T" : "");
         if (!accepted) {
+            theta_fail = ref.theta;
             if (!o->resto) {
                 status = NLOT_LS_FAILED;
                 break;
             }
+            /* IPOPT BacktrackingLineSearch::FindAcceptableTrialPoint: the restoration phase is not entered at
+             * an almost feasible point (theta <= 1e-2 tol); without an acceptable iterate to fall back to
+             * (acceptable_tol 1e-6 < tol here, so none) IPOPT stops with Restoration_Failed. */
+            if (ref.theta <= 1e-2 * o->tol) {
+                status = NLOT_RESTO_FAILED;
+                break;
+            }
             /* ---- feasibility restoration phase ---- */
-            filter_add(s, theta, phi); /* the current point enters the filter first */
+            /* the current point enters the filter first: FilterLSAcceptor::PrepareRestoPhaseStart augments it with
+             * the line search's reference values (the watchdog point's after StopWatchDog, where s is back at
+             * that point) */
+            filter_add(s, ref.theta, ref.phi);
             if (!r_alloc) {
                 sol_setup(r, p, o, m, x0, xg);
                 r->resto = 1;
@@ -2832,6 +2852,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         info[4] = s->mu;
         info[6] = n_resto;
         info[7] = 1e6 * n_wd + 1e4 * n_soft + 1e2 * (s->n_soc_tried > 99 ? 99 : s->n_soc_tried) + n_tiny;
+        info[8] = theta_fail;
     }
     if (r_alloc) free(r->arena);
     free(s->arena);

@@ -117,7 +117,7 @@ def test_restoration_rescues_infeasible_start():
                 slack_penalty=10, use_smooth=True, smooth_weight=0.5, control_bounds=((-1, 1), (-2, 2)),
                 obstacles=[_circle((0.5, 0.45), 0.12, 0.01)])
     x0, xg = [0, 0.4, 0, 0, 0, 0, 0], [1, 0.4, 0, 0, 0, 0, 0]
-    r = O.solve_one(p, x0, xg, opt=_abi.gpu_options())
+    r = O.solve_one(p, x0, xg, opt=_abi.default_options(**_abi.NO_RESTO))
     assert r["status"] == _abi.NLOT_LS_FAILED and r["iters"] <= 3
     r = O.solve_one(p, x0, xg)
     assert r["status"] == 0 and r["resto_phases"] >= 1 and r["constr_viol"] < 1e-4
