@@ -2439,11 +2439,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                 if (f_c + m >= AT(afilt, 2 * i) && th_c + m >= AT(afilt, 2 * i + 1)) return false;
             return true;
         };
+        // fixed mode (IPOPT AdaptiveMuUpdate): back to free mode as soon as the point makes sufficient progress
+        // w.r.t. the progress filter (checked every iteration; remembered below), else one Fiacco-McCormick
+        // decrease once the barrier problem is solved
         if (!free_) {
-            const double Emu = fmax(fmax(dual / sd, primal), cmu / scc);
-            if (Emu <= kap * mu) {
-                if (af_ok()) free_ = true;
-                else barrier_decrease(cmu);
+            if (af_ok()) {
+                free_ = true;
+            } else if (fmax(fmax(dual / sd, primal), cmu / scc) <= kap * mu) {
+                const double nm = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_floor);
+                if (nm < mu) {
+                    mu = nm;
+                    tau = fmax(0.99, 1.0 - mu);
+                    reset_filter = true;
+                }
             }
         }
         int naf_new = naf;
@@ -2495,7 +2503,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     if (lane == 0) {
         SC(SC_MU) = mu;
         SC(SC_TAU) = tau;
-        if (reset_filter) SC(SC_NFILT) = 0;
+        if (reset_filter) {  // a new barrier problem: BacktrackingLineSearch::Reset (filter, soft restoration, watchdog)
+            SC(SC_NFILT) = 0;
+            SC(SC_INSOFT) = 0;
+            SC(SC_SOFTCNT) = 0;
+            SC(SC_WD) = 0;
+            SC(SC_WDSHORT) = 0;
+        }
         SC(SC_PDC) = pd_c;
         SC(SC_MUPD) = mu_pd;
     }
@@ -2839,10 +2853,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         for (int i = lane; i < N * NX; i += 64) AT(yk_n, i) = qa_[oyk + i] + sig * qc_[oyk + i];
         for (int i = lane; i < 8; i += 64) AT(yt_n, i) = qa_[oyt + i] + sig * qc_[oyt + i];
         wsync();
-        if (lane == 0) {
+        if (lane == 0) {  // a new barrier problem: BacktrackingLineSearch::Reset (filter, soft restoration, watchdog)
             SC(SC_MU) = mu;
             SC(SC_TAU) = tau;
-            SC(SC_NFILT) = 0;  // the line-search filter belongs to one barrier problem
+            SC(SC_NFILT) = 0;
+            SC(SC_INSOFT) = 0;
+            SC(SC_SOFTCNT) = 0;
+            SC(SC_WD) = 0;
+            SC(SC_WDSHORT) = 0;
         }
         wsync();
         }

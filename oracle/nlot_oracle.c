@@ -2560,7 +2560,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         /* ---- barrier parameter ---- */
         const double kap = o->barrier_tol_factor;
         const double mu_floor = fmin(o->tol, o->compl_inf_tol) / (kap + 1.0);
-        int use_qf = 0;
+        int use_qf = 0, ls_reset = 0;
         if (o->mu_strategy == 0) { /* IPOPT MonotoneMuUpdate, fast decrease allowed */
             if (iter > 0) {
                 for (;;) {
@@ -2572,6 +2572,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                     s->mu = nm;
                     s->tau = fmax(0.99, 1.0 - s->mu);
                     s->nfilt = 0;
+                    ls_reset = 1;
                     errors(s, &e); /* complmu depends on mu */
                     tiny_last = 0;
                 }
@@ -2585,21 +2586,22 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             double th_c, ph_c;
             merit(s, s->X, s->U, s->S, s->T, s->mu, &th_c, &ph_c, NULL);
             const double f_c = s->f;
+            /* fixed mode: back to free mode as soon as the point makes sufficient progress w.r.t. the progress
+             * filter ("Switching back to free mu mode", checked every iteration); otherwise one Fiacco-McCormick
+             * decrease once the barrier problem is solved ("Reducing mu ... in fixed mu mode") */
             if (!s->free_mode) {
-                double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
-                if (Emu <= kap * s->mu) { /* barrier problem solved: back to free mode, or decrease */
-                    if (afilt_acceptable(s, f_c, th_c)) {
-                        s->free_mode = 1;
-                    } else {
-                        for (;;) {
-                            double nm = fmax(fmin(0.2 * s->mu, pow(s->mu, 1.5)), mu_floor);
-                            if (nm >= s->mu) break;
+                if (afilt_acceptable(s, f_c, th_c)) {
+                    s->free_mode = 1; /* RememberCurrentPointAsAccepted below */
+                } else {
+                    double Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
+                    if (Emu <= kap * s->mu) {
+                        double nm = fmax(fmin(0.2 * s->mu, pow(s->mu, 1.5)), mu_floor);
+                        if (nm < s->mu) {
                             s->mu = nm;
                             s->tau = fmax(0.99, 1.0 - s->mu);
                             s->nfilt = 0;
+                            ls_reset = 1;
                             errors(s, &e);
-                            Emu = fmax(fmax(e.dual / e.sd, e.primal), e.complmu / e.sc);
-                            if (Emu > kap * s->mu) break;
                         }
                     }
                 }
@@ -2612,6 +2614,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                     s->mu = fmin(fmax(0.8 * e.avg_compl, AMU_MU_MIN), s->mu_max);
                     s->tau = fmax(0.99, 1.0 - s->mu);
                     s->nfilt = 0;
+                    ls_reset = 1;
                     errors(s, &e);
                 }
             }
@@ -2646,8 +2649,14 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             s->mu = mu;
             s->tau = fmax(0.99, 1.0 - mu);
             s->nfilt = 0; /* the line-search filter belongs to one barrier problem */
+            ls_reset = 1;
         } else {
             s->mu = mu_it;
+        }
+        if (ls_reset) { /* a new barrier problem: BacktrackingLineSearch::Reset ends the soft restoration and the
+                         * watchdog (and clears the filter, above) */
+            in_soft = soft_cnt = 0;
+            in_wd = wd_short = 0;
         }
         /* ---- step sizes: fraction to the boundary; line-search reference values ---- */
         const double tau = s->tau;
@@ -2910,3 +2919,25 @@ int oracle_sizeof_problem(void) { return (int)sizeof(NlotProblem); }
 int oracle_sizeof_options(void) { return (int)sizeof(NlotSolverOptions); }
 int oracle_sizeof_mlpdesc(void) { return (int)sizeof(NlotMlpDesc); }
 int oracle_sizeof_stats(void) { return (int)sizeof(NlotSolveStats); }
+
+/* NLP pieces for an independent solver (scripts/crosscheck_scipy.py): the knot inequalities with their pose
+ * gradients and the w-weighted pose Hessian sum_j w_j d2 d_j / dpose2 (3x3 row-major) ... */
+int oracle_knot_constraints_h(const NlotProblem* p, const NlotMlpDesc* m, const double* xk, double sk, const double* w,
+                              double* d, double* grad3, double* hess9) {
+    jet dj[NLOT_MAX_BODY];
+    int mm = knot_ineq(p, m, xk, 1, dj);
+    for (int a = 0; a < 9; ++a) hess9[a] = 0.0;
+    for (int j = 0; j < mm; ++j) {
+        d[j] = dj[j].v + ((p->use_slack && p->shape != NLOT_SHAPE_DOT) ? sk : 0.0);
+        for (int i = 0; i < 3; ++i) grad3[3 * j + i] = dj[j].g[i];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) hess9[a * 3 + b] += w[j] * dj[j].h[hix(a, b)];
+    }
+    return mm;
+}
+/* ... and the defect map F(x, u) (Euler or RK4) with its Jacobians and the lambda-weighted Hessian
+ * sum_i lambda_i d2 F_i / d(x, u)2 ((nx + nu)^2 row-major). */
+void oracle_dyn_hess(const NlotProblem* p, const double* x, const double* u, const double* lam, double* F, double* A,
+                     double* B, double* H) {
+    dyn_eval(p, x, u, lam, F, A, B, H);
+}

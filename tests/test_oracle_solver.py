@@ -45,9 +45,9 @@ def test_b2_tight_tolerance_reaches_trust_constr_cost():
 def test_b2_adaptive_mu_reaches_a_kkt_point():
     """The reference's IPOPT setting (mu_strategy adaptive, quality-function oracle, barrier_tol_factor 0.05,
     runner.py:118-120) from the same start converges to a local minimum of b2; tightening the tolerance
-    confirms it is a KKT point.  The YAML's diagonal start is path-sensitive (1e-13 perturbations of the start
-    switch the outcome), so the point reached is one of b2's two local minima: the robot holds near
-    the start then drives (cost 1.632809), or the monotone run's (1.656058, reached at tol 1e-8 within 2e-4)."""
+    confirms it is a KKT point (dual infeasibility 9e-9 at cost 1.631531, next to SLSQP's 1.631863 of SURVEY.md
+    §6: b2 has several local minima close in cost), and the tol 1e-4 stop lies within 1e-4 of it (north_star's
+    cost tolerance)."""
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
@@ -58,9 +58,7 @@ def test_b2_adaptive_mu_reaches_a_kkt_point():
     t = O.solve_one(b["problem"], b["start"], b["goal"], opt=_abi.default_options(tol=1e-8, constr_viol_tol=1e-8,
                                                                                   compl_inf_tol=1e-8))
     assert t["status"] == 0 and t["dual_inf"] < 1e-7 and t["constr_viol"] < 1e-10
-    # at tol 1e-4 the run stops where the scaled KKT error first drops below 1e-4: with IPOPT's safeguards that
-    # point lies 4e-3 above the KKT cost (the complementarity gap sum z s ~ n mu allows it)
-    assert min(abs(t["cost"] - 1.632809), abs(t["cost"] - 1.656058)) < 2e-4 and abs(r["cost"] - t["cost"]) < 1e-2
+    assert abs(r["cost"] - t["cost"]) < 1e-4 * t["cost"] and 1.60 < t["cost"] < 1.66
 
 
 def test_b3_analytic_and_batch_equals_single():

@@ -77,3 +77,45 @@ def test_gpu_rrt_matches_oracle(fn):
         print(fn, b, "ok", okc, bool(okg[b]), "max |dX|", err, flush=True)
         assert bool(okg[b]) == okc
         assert err < 1e-9, (fn, b, err)
+
+
+# ---- reference-pinned fixtures (tests/golden/make_rrt_golden.py: the REFERENCE's RRTInitializer driven like
+# run_benchmark.py:116-127, its `random` replaced by the counter-based stream; circle / square scenes) ----
+RRT_GOLD = json.load(open(os.path.join(HERE, "golden", "rrt_golden.json")))["cases"]
+
+
+def _gold_problem(c):
+    from nlotrajectories_amd.config import Config
+
+    return Config.model_validate(GOLD["configs"][c["yaml"]]).to_problem().with_(sdf="analytic")
+
+
+@pytest.mark.parametrize("i", range(len(RRT_GOLD)))
+def test_oracle_rrt_matches_reference_rrt(i):
+    """The restatement reproduces the reference's X_init (tree, intermediate points, shortcuts, CubicSpline)."""
+    import rrt_oracle as R
+
+    c = RRT_GOLD[i]
+    X, ok = R.rrt_one(_gold_problem(c), np.array(c["x0"]), np.array(c["xg"]), c["bounds"], step_size=c["step_size"],
+                      max_iter=c["max_iter"], margin=c["margin"], seed=c["seed"], instance=c["instance"])
+    assert ok == c["ok"]
+    np.testing.assert_allclose(X, np.array(c["X_init"]), atol=1e-12, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("yaml", sorted({c["yaml"] for c in RRT_GOLD}))
+def test_gpu_rrt_matches_reference_rrt(yaml):
+    """nlot_rrt_init on the scene's 4 instances (batch index = the fixture's instance) against the reference's X_init:
+    1e-9 (the kernel's Thomas spline solve vs scipy's LAPACK)."""
+    from nlotrajectories_amd.rrt import rrt_initial_guess
+
+    cs = sorted([c for c in RRT_GOLD if c["yaml"] == yaml], key=lambda c: c["instance"])
+    c0 = cs[0]
+    Xg, okg = rrt_initial_guess(_gold_problem(c0), np.array([c["x0"] for c in cs]), np.array([c["xg"] for c in cs]),
+                                c0["bounds"], step_size=c0["step_size"], max_iter=c0["max_iter"], margin=c0["margin"],
+                                seed=c0["seed"])
+    Xg, okg = Xg.cpu().numpy(), okg.cpu().numpy()
+    for b, c in enumerate(cs):
+        err = float(np.abs(Xg[b] - np.array(c["X_init"])).max())
+        print(yaml, b, "max |dX| vs reference", err, flush=True)
+        assert bool(okg[b]) == c["ok"] and err < 1e-9

@@ -117,3 +117,39 @@ def test_solver_iterates_smooth_sdf(artefact, act):
         assert rg["iters"][0].item() == rc["iters"]
         np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-4)
         np.testing.assert_allclose(rg["U"][0].cpu().numpy(), rc["U"], atol=1e-4)
+
+
+# ---- reference-pinned fixtures (tests/golden/make_smooth_golden.py: the REFERENCE's FourierMLP(tanh | sigmoid |
+# leaky_relu) and SIREN modules, core/nn_architectures.py:8-100, seeded, fp64 autograd) ----
+REF_CASES = ["fourier_tanh", "fourier_sigmoid_2x", "fourier_leaky", "siren", "siren_w5_3x"]
+
+
+def _golden_net(name):
+    import os
+
+    from nlotrajectories_amd.nn import MlpWeights
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "smooth_golden.npz"))
+    g = lambda k: z[f"{name}/{k}"]
+    w = MlpWeights(int(g("in_kind")), int(g("hidden")), int(g("n_hidden")), float(g("fourier_scale")),
+                   float(g("b_out")), {k: g(k).astype(np.float32) for k in ("A", "b0", "W", "b", "w_out")}, int(g("act")))
+    return w, z["p"], (g("f"), g("grad"), g("hess"))
+
+
+@pytest.mark.parametrize("name", REF_CASES)
+def test_oracle_smooth_matches_reference_golden(name):
+    import oracle as O
+
+    w, pts, ref = _golden_net(name)
+    v, g, h = O.mlp_eval(O.HostMlp(w), pts)
+    _check(v, g, h.reshape(-1, 2, 2), ref, 5e-5 if "siren" in name else 2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", REF_CASES)
+def test_kernel_smooth_matches_reference_golden(name):
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    w, pts, ref = _golden_net(name)
+    v, g, h = (t.cpu().numpy() for t in sdf_mlp_eval(DeviceMlp(w), torch.tensor(pts, device="cuda:0")))
+    _check(v, g, h.reshape(-1, 2, 2), ref, 5e-5 if "siren" in name else 2e-5)
