@@ -183,7 +183,7 @@ def main():
     opt_cont.max_active = slots
     agg_keys = ("mlp_full_ms", "mlp_full_launches", "mlp_points_full", "mlp_value_ms", "mlp_value_launches",
                 "mlp_points_value", "iterations", "iterate_ms", "mlp_points_full_reused", "ric_ms", "ric_launches",
-                "ric_solves")
+                "ric_solves", "ric_soc_solves", "ric_resto_solves")
     agg = {k: 0 for k in agg_keys}
     timing = {"on": False}
 
@@ -307,8 +307,13 @@ def main():
             "solves_per_launch": ric_solves_per_launch,
             "avg_launch_ms": ric_avg_ms,
             "launches": agg["ric_launches"],
+            "side_stream_solves": {"second_order_corrections": agg["ric_soc_solves"],
+                                   "restoration": agg["ric_resto_solves"],
+                                   "factorisations_main": agg["ric_solves"]},
             "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
-                    "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline",
+                    "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline.  The "
+                    "second-order corrections (substitution with the stored factors, k_ric<DYN, false, true>) and the "
+                    "restoration solves run on a side stream and are not counted in this launch's solves",
             "pmc_note": "profiles/r02/kric_sq.json (B = 16384): 25.5 % of wave cycles issue (15.4 % VALU), 50.4 % "
                         "wait on s_waitcnt (LDS hand-offs, DMA ring), 24.0 % issue-stalled (fp64 VALU pipe)",
         }

@@ -159,6 +159,10 @@ typedef struct NlotSolverOptions {
     double resto_proximity_weight;           /* zeta = weight * sqrt(mu), weight 1 */
     double bound_mult_reset_threshold;       /* 1000 */
     double resto_failure_feasibility_threshold; /* 0 means 1e2 * tol (IPOPT default) */
+    int32_t general_bounds;      /* 1: the control bounds and slack >= 0 as constraint rows g(x) = U, g(x) = S with
+                                    bounded IPOPT slacks (CasADi Opti's form, runner.py:67-69,100-104); 0: variable
+                                    bounds.  CPU restatement only so far (oracle/); the GPU solver refuses 1 */
+    int32_t pad_gb_;
 } NlotSolverOptions;
 
 /* Learned SDF: an l4casadi-wrappable torch model, flattened.
@@ -251,7 +255,9 @@ typedef struct NlotSolveStats {
     double ric_ms;             /* summed device time of the Newton-solve (k_ric) launches (hipEvents) */
     int32_t ric_launches;
     int32_t pad2_;
-    int64_t ric_solves;        /* instance Newton solves those launches performed */
+    int64_t ric_solves;        /* instance Newton solves (factorisations) those launches performed */
+    int64_t ric_soc_solves;    /* second-order corrections: substitutions with the stored factors (side stream) */
+    int64_t ric_resto_solves;  /* restoration-phase Newton solves (side stream) */
 } NlotSolveStats;
 /* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
 void nlot_set_timing(int32_t enabled);

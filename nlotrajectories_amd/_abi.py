@@ -53,6 +53,7 @@ class NlotSolverOptions(C.Structure):
         ("soft_resto_pderror_reduction_factor", C.c_double), ("required_infeasibility_reduction", C.c_double),
         ("resto_penalty_parameter", C.c_double), ("resto_proximity_weight", C.c_double),
         ("bound_mult_reset_threshold", C.c_double), ("resto_failure_feasibility_threshold", C.c_double),
+        ("general_bounds", C.c_int32), ("pad_gb_", C.c_int32),
     ]
 
 
@@ -72,7 +73,8 @@ class NlotSolveStats(C.Structure):
         ("mlp_full_launches", C.c_int32), ("mlp_value_launches", C.c_int32),
         ("iterate_ms", C.c_double), ("slots_in_lds", C.c_int32), ("pad_", C.c_int32),
         ("mlp_points_full_reused", C.c_int64), ("ric_ms", C.c_double), ("ric_launches", C.c_int32),
-        ("pad2_", C.c_int32), ("ric_solves", C.c_int64),
+        ("pad2_", C.c_int32), ("ric_solves", C.c_int64), ("ric_soc_solves", C.c_int64),
+        ("ric_resto_solves", C.c_int64),
     ]
 
 

@@ -153,6 +153,10 @@ __host__ __device__ constexpr int it_len(int N, int nx, int nu, int M) {
 // allocated with the terminal block padded to 8
 __host__ __device__ constexpr int ne_len(int N, int nx, int M) { return nx + N * nx + 8 + (N + 1) * M; }
 
+// a stored pivoted LDL^T factor of an n x n block (ldl_factor's in-place form, then the permutation): the Q_vv
+// factor of every stage and the terminal block's, kept by each Newton solve for the second-order corrections
+__host__ __device__ constexpr int ldl_len(int n) { return n * n + n; }
+
 // instance-major arrays: (name, per-instance length)
 #define NLOT_WS_ARRAYS(X_)                                                                             \
     X_(X, (N + 1) * nx) X_(U, N * nu) X_(S, N + 1) X_(T, (N + 1) * M) X_(yi, nx) X_(yk, N * nx) X_(yt, 8) \
@@ -167,7 +171,8 @@ __host__ __device__ constexpr int ne_len(int N, int nx, int M) { return nx + N *
     X_(sts, it_len(N, nx, nu, M)) X_(rcs, nx + N * nx + 8 + (N + 1) * M) X_(wdi, it_len(N, nx, nu, M))       \
     X_(wdd, it_len(N, nx, nu, M)) X_(rp, ne_len(N, nx, M)) X_(rn, ne_len(N, nx, M)) X_(rzp, ne_len(N, nx, M))     \
     X_(rzn, ne_len(N, nx, M)) X_(rdp, ne_len(N, nx, M)) X_(rdn, ne_len(N, nx, M)) X_(rdzp, ne_len(N, nx, M))      \
-    X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)
+    X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)   \
+    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx))
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -184,7 +189,8 @@ struct Ws {
     uint32_t* tmask[2];  // its hidden-layer ReLU patterns [4][slot][P]
     int* tsrc;           // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
     int* cnt;  // counters of step parity q at cnt + 8 q: [0] evaluation ranks, [1] trial slots, [2] next active
-               // count, [3] full-launch points whose forward was reused, [4] Newton solves, [5] restoration list count
+               // count, [3] full-launch points whose forward was reused, [4] Newton solves, [5] restoration list count,
+               // [6] second-order corrections, [7] restoration Newton solves
     int* act[2]; // active instance lists (ping-pong)
     int* actr[2]; // the instances of act in a restoration phase (count: counter [5] of the step's set)
     int64_t cap;
@@ -472,6 +478,8 @@ struct Solver {
     // of registers.
     // Two right-hand sides: g_r = g(mu_r) for r < nr, written as o = [H | g_0 g_1] (NZ x (NZ+2)); g is
     // affine in mu, accumulated as base + mu * coefficient.
+    // GONLY: only the g columns are written (a second-order correction: H is the iteration's, already factorised)
+    template <bool GONLY = false>
     __device__ __forceinline__ static void stage(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int k, int mode,
                                                  double dw, double mu0, double mu1, int nr, double* o) {
         const int N = dm.N, M = dm.M;
@@ -607,7 +615,7 @@ struct Solver {
                         if (j == is && i < 3) h += ps[i];
                     }
                     if (i == j && i < nz) h += dg;
-                    o[i * (NZ + 2) + j] = h;
+                    if constexpr (!GONLY) o[i * (NZ + 2) + j] = h;
                 }
                 double gi = 0, gm = 0;
                 if (i < NX) {
@@ -655,13 +663,14 @@ struct Solver {
     __host__ __device__ static constexpr int qe_col(int c) { return c < NX ? c : NZ + (c - NX); }
 
     // Build every stage's matrices in parallel (lane = knot): [H | g] -> hg (HBM); [A B 0 | c], M -> slot.
-    template <bool LDS>
+    // GONLY: hg's g columns only (second-order correction; the slot is rebuilt: the forward sweep overwrote it)
+    template <bool LDS, bool GONLY = false>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
                                         double dw, double mu0, double mu1, int nr, double* SL, int stride = 64) {
         const int N = dm.N;
         for (int k = lane; k <= N; k += stride) {
             double* o = SL + (size_t)k * SLOT;
-            stage(p, dm, ws, b, k, mode, dw, mu0, mu1, nr, &AT(hg, k * HG));
+            stage<GONLY>(p, dm, ws, b, k, mode, dw, mu0, mu1, nr, &AT(hg, k * HG));
             double A[NX][NX], Bu[NX][NU];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -943,17 +952,19 @@ __device__ __forceinline__ void ric_sync_reads() {
 // with IPOPT's inertia correction: on a wrong inertia the group rebuilds its stages with the next
 // delta_w and factorises again.  Outputs: dX dU dS yi_n yk_n yt_n (and the second right-hand side).
 // waves per SIMD of k_ric: NLOT_WPE_RIC, except ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
-template <int DYN>
+template <int DYN, bool SOC = false>
 struct RicWpe {
-    static constexpr int value = DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
+    static constexpr int value = SOC ? 2 : DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
 };
 // RESTO = true: the restoration problem's Newton solve (instances with SC_RESTO = 1, list ws.actr): every
 // equality row is soft (p, n eliminated, oracle soft_transform): before stage k uses the value function of
 // x_{k+1} it becomes that of y = x_{k+1} - w (P <- (I + P D)^-1 P, [p | G] likewise, Psi / psi corrected), the
 // initial state likewise after the sweep, the terminal rows get (-Psi + D_t) nu = ..., and the forward sweep
 // maps x_{k+1} = (I + D P)^-1 (y - D (p + G nu)); every stage block must be positive definite.
-template <int DYN, bool RESTO>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+// SOC = true: the second-order corrections (SC_RICFIX >= 0) by substitution with the stored factors; the SOC = false
+// launch skips them (separate instantiations: the substitution's registers stay out of the factorising sweep's).
+template <int DYN, bool RESTO, bool SOC = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, SOC>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
                                             const int* __restrict__ nact, int mode) {
     using R = RicG<DYN>;
@@ -975,6 +986,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     const int b = active[si];
     if ((int)SC(SC_RIC) != 1) return;
     if ((SC(SC_RESTO) != 0.0) != RESTO) return;
+    if (!RESTO && (SC(SC_RICFIX) >= 0.0) != SOC) return;
     typename R::Sh& sh = shg[grp];
     const int N = dm.N, nc = dm.nc, ns = dm.ns;
     const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
@@ -986,6 +998,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     const bool own_pe = a_pe >= 0 && a_pe < NC;
     double nu_[2][NC], dx0[NX];
     const int neg_lim = RESTO ? 0 : nc;  // negative stage pivots the terminal block can absorb (none: all rows soft)
+    // a Newton solve keeps its factors (Q_vv per stage, the terminal block) for the second-order corrections
+    constexpr int QFL = ldl_len(NV);
+    const bool keep_fac = !RESTO && mode == MODE_NEWTON;
     const int q0r = NX + N * NX + nc;   // restoration rows: first inequality row (terminal rows at q0r - nc)
 
     // backward sweep + terminal multipliers; 0, or 1 on a wrong inertia (uniform within the group)
@@ -1219,6 +1234,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
                 const double i2 = 1.0 / d2;
                 negsum += (d0 < 0) + (d1 < 0) + (d2 < 0);
                 if (negsum > neg_lim) return 1;
+                if (keep_fac && l == 0) {  // ldl_factor's form: L below the diagonal, D on it, then the permutation
+                    const double f[QFL] = {d0, 0.0, 0.0, l10, d1, 0.0, l20, l21, d2, (double)o0, (double)o1, (double)o2};
+                    double* qf = &AT(qfac, k * QFL);
+#pragma unroll
+                    for (int e = 0; e < QFL; ++e) qf[e] = f[e];
+                }
                 if (gc >= 0) {
                     const double x0 = q[NX], x1 = q[NX + 1], x2 = q[NX + 2];
                     // permutations as exact 0/1 blends (selects by a run-time index become scratch arrays)
@@ -1247,6 +1268,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
                 if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
                 negsum += nneg;
                 if (negsum > neg_lim) return 1;
+                if (keep_fac && l == 0) {
+                    double* qf = &AT(qfac, k * QFL);
+#pragma unroll
+                    for (int a = 0; a < NV; ++a) {
+#pragma unroll
+                        for (int c = 0; c < NV; ++c) qf[a * NV + c] = L[a][c];
+                        qf[NV * NV + a] = (double)perm[a];
+                    }
+                }
                 if (gc >= 0) {
                     double col[NV];
 #pragma unroll
@@ -1396,6 +1426,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
                 if (nneg != negsum) return 1;
                 if (l == 0) SC(SC_DC) = dc;
             }
+            if (keep_fac && l == 0) {
+                double* tf = &AT(tfac, 0);
+#pragma unroll
+                for (int a = 0; a < NC; ++a) {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) tf[a * NC + c] = L[a][c];
+                    tf[NC * NC + a] = (double)perm[a];
+                }
+            }
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
                 if (rr >= nr) break;
@@ -1415,6 +1454,136 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
             return 1;
         }
         return 0;
+    };
+
+    // Second-order correction (SC_RICFIX >= 0): the matrix is the iteration's (same iterate, multipliers and
+    // delta_w), only the right-hand side changed (g and c from the corrected residuals, k_iter_a).  So no
+    // factorisation: a backward substitution with the stored Q_vv factors and gains, the value function's P and
+    // Gamma kept from the iteration's sweep, and the recursion of the right-hand-side terms alone:
+    //   w = P' c + p',  q = g + M c + AB' w,  k = -Q_vv^-1 q_v,  p = q_x + K' q_v,  psi += Gamma'(c + B k)
+    // (p = q_x + Q_xv k = q_x + K' q_v since K = -Q_vv^-1 Q_vx).  Lanes i < NX carry w, p and the open-loop
+    // offset e = c + B k; lanes i < NZ carry q; every lane solves the NV x NV system; lanes a < NC carry psi.
+    // Writes k_0 into the gains and p_0 into vf (the forward sweep's inputs), nu_[0] and dx0.
+    auto backward_rhs = [&]() {
+        const int li = l < NZ ? l : 0, lx = l < NX ? l : 0, lm = l < 2 ? l : 0, la = l < NC ? l : 0;
+        // one stage's inputs of this lane (row lx / column li / terminal column la), loaded a stage ahead
+        struct In {
+            double cl, g, m0, m1, P[NX], ab[NX], gam[NX], qf[QFL], kt[NV], bu[NU];
+        };
+        auto load = [&](int k, In& d) {
+            const double* slot = SL + (size_t)k * SLOT;
+            const double* vn = &AT(vf, (k < N ? k + 1 : N) * VF);  // the stage after (k < N; clamped, unused at N)
+            d.cl = slot[sAB + lx * NAB + NZ];
+            d.g = AT(hg, k * HG + li * (NZ + 2) + NZ);
+            d.m0 = slot[sM + 2 * lm];
+            d.m1 = slot[sM + 2 * lm + 1];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                d.P[r] = vn[lx * NCOL + r];
+                d.ab[r] = slot[sAB + r * NAB + li];
+                d.gam[r] = vn[r * NCOL + NX + 2 + la];
+            }
+            const double* f = &AT(qfac, k * QFL);
+#pragma unroll
+            for (int e = 0; e < QFL; ++e) d.qf[e] = f[e];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) d.kt[v] = slot[sGN + lx * NV + v];
+#pragma unroll
+            for (int v = 0; v < NU; ++v) d.bu[v] = slot[sAB + lx * NAB + NX + v];
+        };
+        double pn = 0.0, psi = 0.0;
+        In cur, nxt;
+        load(N, cur);
+        for (int k = N; k >= 0; --k) {
+            if (k > 0) load(k - 1, nxt);
+            const int nv = (k < N ? NU : 0) + ns;
+            const bool kn = k < N;
+            const double cl = kn && l < NX ? cur.cl : 0.0;
+            double c[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) c[r] = __shfl(cl, gb + r);
+            double wl = pn;
+#pragma unroll
+            for (int qq = 0; qq < NX; ++qq) wl += cur.P[qq] * c[qq];
+            double w[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) w[r] = __shfl(kn ? wl : 0.0, gb + r);
+            double ql = cur.g;
+            if (kn) {
+                if (l < 2) ql += cur.m0 * c[0] + cur.m1 * c[1];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) ql += cur.ab[r] * w[r];
+            }
+            double qvv[NV], kv[NV];  // q_v, then k = -Q_vv^-1 q_v
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                qvv[v] = __shfl(ql, gb + NX + v);
+                kv[v] = v < nv ? -qvv[v] : 0.0;
+            }
+            if (nv > 0) {
+                double L[NV][NV];
+                int perm[NV];
+#pragma unroll
+                for (int a = 0; a < NV; ++a) {
+#pragma unroll
+                    for (int cc = 0; cc < NV; ++cc) L[a][cc] = cur.qf[a * NV + cc];
+                    perm[a] = (int)cur.qf[NV * NV + a];
+                }
+                ldl_solve1<NV>(L, nv, perm, kv);
+            }
+            double* GN = SL + (size_t)k * SLOT + sGN;
+            if (l < NV) {
+                double v = 0;
+#pragma unroll
+                for (int vv = 0; vv < NV; ++vv) v = vv == l ? kv[vv] : v;
+                GN[NX * NV + l] = v;  // k_0
+            }
+            double pl = ql, el = cl;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) pl += cur.kt[v] * qvv[v];
+#pragma unroll
+            for (int v = 0; v < NU; ++v) el += cur.bu[v] * kv[v];
+            if (l < NX) AT(vf, k * VF + lx * NCOL + NX) = pl;  // p_0
+            if (!kn) {
+                psi = l < nc ? AT(rct, la) : 0.0;
+            } else {
+                double e[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) e[r] = __shfl(el, gb + r);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) psi += cur.gam[r] * e[r];
+            }
+            pn = pl;
+            cur = nxt;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx0[i] = -AT(rci, i);
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) nu_[rr][cc] = 0.0;
+        if (nc) {  // (-Psi + delta_c) nu = psi + Gamma_0' dx0 with the stored factor
+            double t = psi;
+            if (l < nc)
+#pragma unroll
+                for (int r = 0; r < NX; ++r) t += AT(vf, r * NCOL + NX + 2 + li) * dx0[r];
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) {
+                const double v = __shfl(t, gb + cc);
+                nu_[0][cc] = cc < nc ? v : 0.0;
+            }
+            double L[NC][NC];
+            int perm[NC];
+            const double* f = &AT(tfac, 0);
+#pragma unroll
+            for (int a = 0; a < NC; ++a) {
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) L[a][cc] = f[a * NC + cc];
+                perm[a] = (int)f[NC * NC + a];
+            }
+            ldl_solve1<NC>(L, nc, perm, nu_[0]);
+        }
+        __syncthreads();  // k_0 and p_0 in HBM are read across lanes by the forward sweep
     };
 
     // delta_w enters the stage matrices linearly: H(dw) = H(0) + dw (I_nz + sum_q Jx_q Jx_q'),
@@ -1514,7 +1683,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN>:
     int n_att = 0;
     PROF_T(tr0);
 #endif
-    for (int attempt = 0;; ++attempt) {
+    if constexpr (SOC) backward_rhs();
+    for (int attempt = 0; !SOC; ++attempt) {
 #ifdef NLOT_PHASE_PROF
         PROF_T(ta);
         ++n_att;
@@ -2074,7 +2244,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         // second-order correction: the same Newton matrix (the iteration's delta_w, no inertia loop) with the
         // corrected constraint residuals c_soc in rci/rcd/rct/rcq (written by k_accept)
         const double dw = SC(SC_DW), mu = SC(SC_MU);
-        SV::template build_stages<false>(p, dm, ws, b, lane, MODE_NEWTON, dw, mu, 0.0, 1, SL);
+        SV::template build_stages<false, true>(p, dm, ws, b, lane, MODE_NEWTON, dw, mu, 0.0, 1, SL);
         if (lane == 0) {
             SC(SC_RMU0) = mu;
             SC(SC_RMU1) = 0.0;
@@ -2082,7 +2252,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
             SC(SC_USEQF) = 0.0;
             SC(SC_RICFIX) = dw;
             SC(SC_RIC) = 1;
-            atomicAdd(&cnt[4], 1);
+            atomicAdd(&cnt[6], 1);  // statistics: second-order corrections (k_ric<DYN, false, true>)
         }
         return;
     }
@@ -3784,7 +3954,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         SC(SC_USEQF) = 0.0;
         SC(SC_RICFIX) = -1.0;
         SC(SC_RIC) = 1;
-        atomicAdd(&cnt[4], 1);
+        atomicAdd(&cnt[7], 1);  // statistics: restoration Newton solves (k_ric<DYN, true>)
     }
     };
     for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
@@ -4148,6 +4318,10 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
         return NLOT_ERR_INVALID;
     }
     if (p->N < 2 || p->N > 4096 || p->dt <= 0) { set_error("N must be in [2, 4096], dt > 0"); return NLOT_ERR_INVALID; }
+    if (o->general_bounds) {
+        set_error("general_bounds = 1 (bounds as constraint rows) is implemented in the CPU restatement only");
+        return NLOT_ERR_INVALID;
+    }
     if (p->integrator != NLOT_INTEG_EULER && p->integrator != NLOT_INTEG_RK4) {
         set_error("integrator must be NLOT_INTEG_EULER or NLOT_INTEG_RK4"); return NLOT_ERR_INVALID;
     }
@@ -4219,14 +4393,28 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     struct Res {
         int* hcnt = nullptr;
         hipEvent_t ev[KPIPE][8] = {};
+        hipStream_t s2 = nullptr;                                   // side stream: SOC and restoration solves
+        hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr;  // fork after k_iter_a, joins
         ~Res() {
             for (auto& r : ev)
                 for (auto& e : r)
-                    if (e) hipEventDestroy(e);
-            if (hcnt) hipHostFree(hcnt);
+                    if (e) (void)hipEventDestroy(e);
+            for (hipEvent_t e : {e_a, e_soc, e_r})
+                if (e) (void)hipEventDestroy(e);
+            if (s2) (void)hipStreamDestroy(s2);
+            if (hcnt) (void)hipHostFree(hcnt);
         }
     } res;
     NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, KPIPE * 16 * sizeof(int), hipHostMallocDefault));
+    // The second-order corrections (substitution, short) and the restoration instances' Newton solves (a longer
+    // sequential sweep, few instances) touch disjoint instances from the main Newton solve: they run on a side
+    // stream, forked after k_iter_a, so their latency hides under k_ric's; k_iter_b joins the corrections, the
+    // value-MLP launch joins the restoration chain (k_resto_b appends to the same trial list).
+    NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s2, hipStreamNonBlocking));
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_a, hipEventDisableTiming));
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_soc, hipEventDisableTiming));
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_r, hipEventDisableTiming));
+    hipStream_t s2 = res.s2;
     if (g_timing)
         for (int k = 0; k < KPIPE; ++k)
             for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
@@ -4301,18 +4489,20 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
             }
             g_stats.ric_launches++;
             g_stats.ric_solves += hc[4];
+            g_stats.ric_soc_solves += hc[6];
+            g_stats.ric_resto_solves += hc[7];
             hipEvent_t* e = res.ev[j];
             if (e[0] && use_mlp) {
                 float a = 0, c = 0;
-                hipEventElapsedTime(&a, e[0], e[1]);
-                hipEventElapsedTime(&c, e[2], e[3]);
+                (void)hipEventElapsedTime(&a, e[0], e[1]);
+                (void)hipEventElapsedTime(&c, e[2], e[3]);
                 g_stats.mlp_full_ms += a;
                 g_stats.mlp_value_ms += c;
             }
             if (e[4]) {
                 float a = 0, r = 0;
-                hipEventElapsedTime(&a, e[4], e[5]);
-                hipEventElapsedTime(&r, e[6], e[7]);
+                (void)hipEventElapsedTime(&a, e[4], e[5]);
+                (void)hipEventElapsedTime(&r, e[6], e[7]);
                 g_stats.iterate_ms += a;
                 g_stats.ric_ms += r;
             }
@@ -4340,15 +4530,15 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
         if (use_mlp) {
             if (init_step) hipLaunchKernelGGL(k_points, dim3(n_active), dim3(64), 0, st, dP, dD, dW, act, C);
-            if (ev[0]) hipEventRecord(ev[0], st);
+            if (ev[0]) (void)hipEventRecord(ev[0], st);
             // contiguous rank-major list: P_per = 1, count = (#instances) * P read on the device
             MlpReuse ru = reuse[q ^ 1];  // the previous step's trial list
             ru.nreused = C + 3;          // statistics: points whose forward was reused
             rc = launch_mlp_strided(mlp->dev, ws.pts, n_active, C + 0, (int)P, 0, nullptr, mo, true, st, &ru);
             if (rc) break;
-            if (ev[0]) hipEventRecord(ev[1], st);
+            if (ev[0]) (void)hipEventRecord(ev[1], st);
         }
-        if (ev[4]) hipEventRecord(ev[4], st);
+        if (ev[4]) (void)hipEventRecord(ev[4], st);
         if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
             hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C, Cn);
             hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
@@ -4360,25 +4550,33 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         if (n_resto > 0)
             hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, x0, xg, C);
         hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C, Cn);
-        if (ev[6]) hipEventRecord(ev[6], st);
+        NLOT_HIP_CHECK(hipEventRecord(res.e_a, st));
+        NLOT_HIP_CHECK(hipStreamWaitEvent(s2, res.e_a, 0));
+        hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
+                           s2, dP, dD, dW, act, n_active, C + 2, (int)MODE_NEWTON);
+        NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
+        if (n_resto > 0) {
+            hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s2,
+                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON);
+            hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, s2, dP, dD, o, dW, actr, C,
+                               use_mlp ? ws.tpts[q] : nullptr);
+        }
+        NLOT_HIP_CHECK(hipEventRecord(res.e_r, s2));
+        if (ev[6]) (void)hipEventRecord(ev[6], st);
         hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
                            dP, dD, dW, act, n_active, C + 2, (int)MODE_NEWTON);
-        if (ev[6]) hipEventRecord(ev[7], st);
-        if (n_resto > 0)
-            hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
-                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON);
+        if (ev[6]) (void)hipEventRecord(ev[7], st);
+        NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_soc, 0));
         hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
                            use_mlp ? ws.tpts[q] : nullptr, Cn);
-        if (n_resto > 0)
-            hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, C,
-                               use_mlp ? ws.tpts[q] : nullptr);
-        if (ev[4]) hipEventRecord(ev[5], st);
+        NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_r, 0));
+        if (ev[4]) (void)hipEventRecord(ev[5], st);
         if (use_mlp) {
-            if (ev[0]) hipEventRecord(ev[2], st);
+            if (ev[0]) (void)hipEventRecord(ev[2], st);
             rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
                                     mo_t[q], false, st);
             if (rc) break;
-            if (ev[0]) hipEventRecord(ev[3], st);
+            if (ev[0]) (void)hipEventRecord(ev[3], st);
         }
         // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
         // starts at most KPIPE steps late; the accepted alpha is the same either way)
@@ -4450,7 +4648,14 @@ extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOption
     }
     hipStream_t st = (hipStream_t)stream;
     // the dynamics model and the integrator select the instantiation (Euler: DYN; RK4: DYN + NLOT_RK4_BIAS)
+#ifdef NLOT_ONLY_DYN  // kernel-tuning builds (make tune): the one instantiation
+    if (p->dynamics + (p->integrator == NLOT_INTEG_RK4 ? NLOT_RK4_BIAS : 0) == NLOT_ONLY_DYN)
+        return run<NLOT_ONLY_DYN>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st);
+    set_error("tuning build (NLOT_ONLY_DYN): this dynamics model is not compiled in");
+    return NLOT_ERR_INVALID;
+#endif
 #define NLOT_RUN(D) return run<D>(*p, *o, mlp, x0, xg, Xinit, X, U, S, cost, status, iters, B, workspace, st)
+#ifndef NLOT_ONLY_DYN
     switch (p->dynamics + (p->integrator == NLOT_INTEG_RK4 ? NLOT_RK4_BIAS : 0)) {
     case NLOT_POINT_1ST: NLOT_RUN(NLOT_POINT_1ST);
     case NLOT_POINT_2ND: NLOT_RUN(NLOT_POINT_2ND);
@@ -4465,6 +4670,7 @@ extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOption
     case NLOT_ACKERMANN + NLOT_RK4_BIAS: NLOT_RUN(NLOT_ACKERMANN + NLOT_RK4_BIAS);
     case NLOT_ACKERMANN_2ND + NLOT_RK4_BIAS: NLOT_RUN(NLOT_ACKERMANN_2ND + NLOT_RK4_BIAS);
     }
+#endif
 #undef NLOT_RUN
     set_error("unknown dynamics");
     return NLOT_ERR_INVALID;

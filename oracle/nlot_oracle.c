@@ -760,11 +760,26 @@ typedef struct {
     double *rp, *rn, *rzp, *rzn;            /* p, n and their bound multipliers */
     double *rdp, *rdn, *rdzp, *rdzn;        /* their steps */
     double *Dsoft, *esoft;                  /* per row: compliance and offset of the soft equality */
+    /* ---- general-constraint bounds (o->general_bounds = 1): CasADi Opti hands the reference's control bounds
+     * (opti.bounded(umin, U, umax), runner.py:100-104) and slack >= 0 (runner.py:67-69) to IPOPT as constraint
+     * rows g(x) = U_ki, g(x) = S_k, so IPOPT sees d(x) - sigma = 0 with the bounds on its slack sigma, and U, S
+     * free.  Bound row b: control b = k nu + i (umin_i <= sigma <= umax_i), then slack rows N nu + k (sigma >= 0);
+     * zbl / zbu are sigma's bound multipliers, yb the row multiplier, rcb = U - sigma (or S - sigma). */
+    int gcb, nb;
+    double *sb, *yb, *zbl, *zbu, *rcb, *dsb, *yb_n, *dzbl, *dzbu;
     double *arena;
 } Sol;
 static int row_d(const Sol* s, int k, int i) { return s->nx + k * s->nx + i; }
 static int row_t(const Sol* s, int j) { return s->nx + s->N * s->nx + j; }
 static int row_q(const Sol* s, int q) { return s->nx + s->N * s->nx + s->nc + q; }
+static int row_b(const Sol* s, int b) { return row_q(s, (s->N + 1) * s->M) + b; } /* restoration row of bound row b */
+/* bound row b: its variable, bounds (one-sided rows have no upper bound) */
+static double bvar(const Sol* s, const double* U, const double* S, int b) {
+    return b < s->N * s->nu ? U[b] : S[b - s->N * s->nu];
+}
+static double blo(const Sol* s, int b) { return b < s->N * s->nu ? s->p->umin[b % s->nu] : 0.0; }
+static int bhi_on(const Sol* s, int b) { return b < s->N * s->nu; }
+static double bhi(const Sol* s, int b) { return b < s->N * s->nu ? s->p->umax[b % s->nu] : 0.0; }
 
 static int nv_of(const Sol* s, int k) { return (k < s->N ? s->nu : 0) + s->ns; }
 
@@ -787,8 +802,10 @@ static int sol_alloc(Sol* s) {
     TAKE(dvt, (N + 1) * M) TAKE(rci, XMAX) TAKE(rcd, N * nx) TAKE(rct, CMAX) TAKE(rcq, (N + 1) * M)         \
     TAKE(XR, (N + 1) * nx) TAKE(UR, N * nu) TAKE(SR, N + 1) TAKE(DRX, (N + 1) * nx) TAKE(DRU, N * nu)           \
     TAKE(DRS, N + 1) TAKE(rp, NE) TAKE(rn, NE) TAKE(rzp, NE) TAKE(rzn, NE) TAKE(rdp, NE) TAKE(rdn, NE)          \
-    TAKE(rdzp, NE) TAKE(rdzn, NE) TAKE(Dsoft, NE) TAKE(esoft, NE)
-    const int NE = nx + N * nx + CMAX + (N + 1) * M;
+    TAKE(rdzp, NE) TAKE(rdzn, NE) TAKE(Dsoft, NE) TAKE(esoft, NE) TAKE(sb, NB) TAKE(yb, NB) TAKE(zbl, NB)           \
+    TAKE(zbu, NB) TAKE(rcb, NB) TAKE(dsb, NB) TAKE(yb_n, NB) TAKE(dzbl, NB) TAKE(dzbu, NB)
+    const int NB = N * nu + N + 1;
+    const int NE = nx + N * nx + CMAX + (N + 1) * M + NB;
     ALLOCS
 #undef TAKE
     s->arena = (double*)calloc(n, sizeof(double));
@@ -839,9 +856,10 @@ static double objective_resto(const Sol* s, const double* X, const double* U, co
     return s->rho * a + 0.5 * s->zeta * q;
 }
 
-/* Equality residuals c(x) (IPOPT sign) at a point; any output may be NULL. */
-static void residuals(const Sol* s, const double* X, const double* U, const double* S, const double* T, double* rci,
-                      double* rcd, double* rct, double* rcq) {
+/* Equality residuals c(x) (IPOPT sign) at a point; any output may be NULL.  rcb (bound rows, general_bounds)
+ * = U - sigma / S - sigma at the slacks SB. */
+static void residuals(const Sol* s, const double* X, const double* U, const double* S, const double* T,
+                      const double* SB, double* rci, double* rcd, double* rct, double* rcq, double* rcb) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     for (int i = 0; i < nx; ++i) rci[i] = X[i] - s->x0[i];
@@ -856,80 +874,98 @@ static void residuals(const Sol* s, const double* X, const double* U, const doub
         knot_ineq(p, s->m, X + k * nx, 0, d);
         for (int j = 0; j < M; ++j) rcq[k * M + j] = d[j].v + (s->sd ? S[k] : 0.0) - T[k * M + j];
     }
+    if (rcb)
+        for (int q = 0; q < s->nb; ++q) rcb[q] = bvar(s, U, S, q) - SB[q];
 }
 
-/* Constraint violation theta = ||c||_1 (incl. d - t) and barrier value phi_mu at a point;
- * the residual arrays (may be NULL) receive c(x). */
-static void merit_r(const Sol* s, const double* X, const double* U, const double* S, const double* T, double mu,
-                    double* theta, double* phi, double* rci, double* rcd, double* rct, double* rcq) {
+/* barrier terms of the bounded quantities: variable bounds of U, S, or (general_bounds) the bound rows' slacks;
+ * the inequality slacks T.  bar = sum of logs, lin = sum of the one-sided slacks (kappa_d damping) */
+static void barrier_terms(const Sol* s, const double* U, const double* S, const double* T, const double* SB,
+                          double* bar_out, double* lin_out) {
     const NlotProblem* p = s->p;
-    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    int nu = s->nu, N = s->N, M = s->M;
+    double bar = 0, lin = 0;
+    for (int q = 0; q < (N + 1) * M; ++q) {
+        bar += log(T[q]);
+        lin += T[q];
+    }
+    if (s->gcb) {
+        for (int q = 0; q < s->nb; ++q) {
+            bar += log(SB[q] - blo(s, q));
+            if (bhi_on(s, q)) bar += log(bhi(s, q) - SB[q]);
+            else lin += SB[q];
+        }
+    } else {
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
+        if (s->ns)
+            for (int k = 0; k <= N; ++k) {
+                bar += log(S[k]);
+                lin += S[k];
+            }
+    }
+    *bar_out = bar;
+    *lin_out = lin;
+}
+
+/* Constraint violation theta = ||c||_1 (incl. d - t and the bound rows) and barrier value phi_mu at a point;
+ * the residual arrays (may be NULL) receive c(x). */
+static void merit_r(const Sol* s, const double* X, const double* U, const double* S, const double* T, const double* SB,
+                    double mu, double* theta, double* phi, double* rci, double* rcd, double* rct, double* rcq,
+                    double* rcb) {
+    int nx = s->nx, N = s->N, M = s->M;
     double bi[XMAX], bt[CMAX];
-    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M + s->nb + 1));
     double* bq = bd + N * nx;
+    double* bb = bq + (N + 1) * M;
     if (!rci) rci = bi;
     if (!rct) rct = bt;
     if (!rcd) rcd = bd;
     if (!rcq) rcq = bq;
-    residuals(s, X, U, S, T, rci, rcd, rct, rcq);
-    double th = 0, bar = 0, lin = 0;
+    if (!rcb) rcb = bb;
+    residuals(s, X, U, S, T, SB, rci, rcd, rct, rcq, rcb);
+    double th = 0, bar, lin;
     for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
     for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
     for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
-    for (int q = 0; q < (N + 1) * M; ++q) {
-        th += fabs(rcq[q]);
-        bar += log(T[q]);
-        lin += T[q];
-    }
+    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[q]);
+    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[q]);
     free(bd);
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
-    if (s->ns)
-        for (int k = 0; k <= N; ++k) {
-            bar += log(S[k]);
-            lin += S[k];
-        }
+    barrier_terms(s, U, S, T, SB, &bar, &lin);
     const double kappa_d = 1e-5;
     *theta = th;
     *phi = objective(s, X, U, S) - mu * bar + kappa_d * mu * lin;
 }
-/* Restoration merit at (x, t, p, n): theta_R = ||c(x) - p + n||_1 over every row (d - t included),
+/* Restoration merit at (x, t, p, n): theta_R = ||c(x) - p + n||_1 over every row (d - t and bound rows included),
  * phi_R = restoration objective - mu sum ln(bound slacks incl. p, n) + kappa_d mu sum(one-sided slacks). */
 static void merit_resto(const Sol* s, const double* X, const double* U, const double* S, const double* T,
-                        const double* pp, const double* nn, double mu, double* theta, double* phi, double* rci,
-                        double* rcd, double* rct, double* rcq) {
-    const NlotProblem* p = s->p;
-    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+                        const double* SB, const double* pp, const double* nn, double mu, double* theta, double* phi,
+                        double* rci, double* rcd, double* rct, double* rcq, double* rcb) {
+    int nx = s->nx, N = s->N, M = s->M;
     double bi[XMAX], bt[CMAX];
-    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* bd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M + s->nb + 1));
     double* bq = bd + N * nx;
+    double* bb = bq + (N + 1) * M;
     if (!rci) rci = bi;
     if (!rct) rct = bt;
     if (!rcd) rcd = bd;
     if (!rcq) rcq = bq;
-    residuals(s, X, U, S, T, rci, rcd, rct, rcq);
+    if (!rcb) rcb = bb;
+    residuals(s, X, U, S, T, SB, rci, rcd, rct, rcq, rcb);
     for (int i = 0; i < nx; ++i) rci[i] += -pp[i] + nn[i];
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nx; ++i) rcd[k * nx + i] += -pp[row_d(s, k, i)] + nn[row_d(s, k, i)];
     for (int j = 0; j < s->nc; ++j) rct[j] += -pp[row_t(s, j)] + nn[row_t(s, j)];
     for (int q = 0; q < (N + 1) * M; ++q) rcq[q] += -pp[row_q(s, q)] + nn[row_q(s, q)];
-    double th = 0, bar = 0, lin = 0;
+    for (int q = 0; q < s->nb; ++q) rcb[q] += -pp[row_b(s, q)] + nn[row_b(s, q)];
+    double th = 0, bar, lin;
     for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
     for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
     for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
-    for (int q = 0; q < (N + 1) * M; ++q) {
-        th += fabs(rcq[q]);
-        bar += log(T[q]);
-        lin += T[q];
-    }
+    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[q]);
+    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[q]);
     free(bd);
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
-    if (s->ns)
-        for (int k = 0; k <= N; ++k) {
-            bar += log(S[k]);
-            lin += S[k];
-        }
+    barrier_terms(s, U, S, T, SB, &bar, &lin);
     for (int i = 0; i < s->ne; ++i) {
         bar += log(pp[i]) + log(nn[i]);
         lin += pp[i] + nn[i];
@@ -938,9 +974,9 @@ static void merit_resto(const Sol* s, const double* X, const double* U, const do
     *phi = objective_resto(s, X, U, S, pp, nn) - mu * bar + 1e-5 * mu * lin;
 }
 
-static void merit(const Sol* s, const double* X, const double* U, const double* S, const double* T, double mu,
-                  double* theta, double* phi, double* fout) {
-    merit_r(s, X, U, S, T, mu, theta, phi, NULL, NULL, NULL, NULL);
+static void merit(const Sol* s, const double* X, const double* U, const double* S, const double* T, const double* SB,
+                  double mu, double* theta, double* phi, double* fout) {
+    merit_r(s, X, U, S, T, SB, mu, theta, phi, NULL, NULL, NULL, NULL, NULL);
     if (fout) *fout = objective(s, X, U, S);
 }
 
@@ -980,8 +1016,10 @@ static void eval_full(Sol* s) {
     }
     for (int i = 0; i < nx; ++i) s->rci[i] = s->X[i] - s->x0[i];
     for (int j = 0; j < s->nc; ++j) s->rct[j] = s->X[N * nx + s->tidx[j]] - s->xg[s->tidx[j]];
+    for (int q = 0; q < s->nb; ++q) s->rcb[q] = bvar(s, s->U, s->S, q) - s->sb[q];
     if (s->resto) { /* c(x) - p + n, and the restoration objective's gradient (no path-length terms) */
         for (int i = 0; i < nx; ++i) s->rci[i] += -s->rp[i] + s->rn[i];
+        for (int q = 0; q < s->nb; ++q) s->rcb[q] += -s->rp[row_b(s, q)] + s->rn[row_b(s, q)];
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < nx; ++i) s->rcd[k * nx + i] += -s->rp[row_d(s, k, i)] + s->rn[row_d(s, k, i)];
         for (int j = 0; j < s->nc; ++j) s->rct[j] += -s->rp[row_t(s, j)] + s->rn[row_t(s, j)];
@@ -1055,18 +1093,21 @@ static void errors(const Sol* s, Errs* e) {
         for (int i = 0; i < nx; ++i) DUAL(r[i]);
         if (k < N)
             for (int i = 0; i < nu; ++i) {
-                double t = s->gU[k * nu + i] - s->zl[k * nu + i] + s->zu[k * nu + i];
+                double t = s->gcb ? s->gU[k * nu + i] + s->yb[k * nu + i]
+                                  : s->gU[k * nu + i] - s->zl[k * nu + i] + s->zu[k * nu + i];
                 for (int a = 0; a < nx; ++a) t -= s->B[k * nx * nu + a * nu + i] * s->yk[k * nx + a];
                 DUAL(t);
             }
         if (s->ns) {
-            double t = s->gS[k] - s->zs[k];
+            double t = s->gcb ? s->gS[k] + s->yb[N * nu + k] : s->gS[k] - s->zs[k];
             if (s->sd)
                 for (int j = 0; j < M; ++j) t += s->yd[k * M + j];
             DUAL(t);
         }
         for (int j = 0; j < M; ++j) DUAL(-s->yd[k * M + j] - s->vt[k * M + j]);
     }
+    for (int q = 0; q < s->nb; ++q) /* bound-row slacks: -y - z_L + z_U */
+        DUAL(-s->yb[q] - s->zbl[q] + (bhi_on(s, q) ? s->zbu[q] : 0.0));
     /* primal infeasibility (c, d - t) and unscaled constraint violation */
 #define PRI(v)                                                                                   \
     do {                                                                                         \
@@ -1084,6 +1125,12 @@ static void errors(const Sol* s, Errs* e) {
         PRI(s->rcq[q]);
         cviol = fmax(cviol, fmax(0.0, -s->dv[q]));
     }
+    for (int q = 0; q < s->nb; ++q) { /* bound rows: d(x) = U or S against [d_L, d_U] */
+        PRI(s->rcb[q]);
+        const double v = bvar(s, s->U, s->S, q);
+        cviol = fmax(cviol, fmax(0.0, blo(s, q) - v));
+        if (bhi_on(s, q)) cviol = fmax(cviol, fmax(0.0, v - bhi(s, q)));
+    }
 #undef PRI
     /* complementarity */
 #define COMPL(z, sl)                                                                             \
@@ -1096,13 +1143,20 @@ static void errors(const Sol* s, Errs* e) {
         zsum += fabs(zz);                                                                        \
         nzc++;                                                                                   \
     } while (0)
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nu; ++i) {
-            COMPL(s->zl[k * nu + i], s->U[k * nu + i] - p->umin[i]);
-            COMPL(s->zu[k * nu + i], p->umax[i] - s->U[k * nu + i]);
+    if (s->gcb) {
+        for (int q = 0; q < s->nb; ++q) {
+            COMPL(s->zbl[q], s->sb[q] - blo(s, q));
+            if (bhi_on(s, q)) COMPL(s->zbu[q], bhi(s, q) - s->sb[q]);
         }
-    if (s->ns)
-        for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k]);
+    } else {
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i) {
+                COMPL(s->zl[k * nu + i], s->U[k * nu + i] - p->umin[i]);
+                COMPL(s->zu[k * nu + i], p->umax[i] - s->U[k * nu + i]);
+            }
+        if (s->ns)
+            for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k]);
+    }
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < M; ++j) COMPL(s->vt[k * M + j], s->T[k * M + j]);
     if (s->resto) /* p and n rows: rho -+ y - z = 0, z p = mu, z n = mu */
@@ -1110,7 +1164,8 @@ static void errors(const Sol* s, Errs* e) {
             double y = i < nx ? s->yi[i]
                        : i < row_t(s, 0) ? s->yk[i - nx]
                        : i < row_q(s, 0) ? s->yt[i - row_t(s, 0)]
-                                         : s->yd[i - row_q(s, 0)];
+                       : i < row_b(s, 0) ? s->yd[i - row_q(s, 0)]
+                                         : s->yb[i - row_b(s, 0)];
             DUAL(s->rho - y - s->rzp[i]);
             DUAL(s->rho + y - s->rzn[i]);
             COMPL(s->rzp[i], s->rp[i]);
@@ -1122,7 +1177,8 @@ static void errors(const Sol* s, Errs* e) {
     for (int i = 0; i < N * nx; ++i) ysum += fabs(s->yk[i]);
     for (int j = 0; j < s->nc; ++j) ysum += fabs(s->yt[j]);
     for (int i = 0; i < (N + 1) * M; ++i) ysum += fabs(s->yd[i]);
-    ny = nx + N * nx + s->nc + (N + 1) * M;
+    for (int i = 0; i < s->nb; ++i) ysum += fabs(s->yb[i]);
+    ny = nx + N * nx + s->nc + (N + 1) * M + s->nb;
     const double smax = 100.0;
     e->sd = fmax(smax, (ysum + zsum) / (double)(ny + nzc)) / smax;
     e->sc = fmax(smax, zsum / (double)nzc) / smax;
@@ -1158,6 +1214,45 @@ enum { MODE_NEWTON = 0, MODE_LSQ = 1 };
  *   min sum_k 1/2 z_k' H_k z_k + g_k' z_k + sum_k dx_k' M_k dx_{k+1}
  *   s.t. dx_0 = dx0, dx_{k+1} = A_k dx_k + B_k dv_k + c_k, C dx_N = rN
  * H_k includes W_kk + Sigma + dw I + J_d' D J_d (IPOPT slacks t and their duals eliminated). */
+/* bound row q (general_bounds) in the condensed stage system: sigma (and in the restoration problem p, n) eliminated.
+ * bg = sigma's barrier gradient, Sig = its barrier Hessian; Newton: D = Sig + dw, rhs = D r + bg (r = U - sigma);
+ * restoration: D = 1 / C, rhs = (r - E) / C as for the inequality rows; least squares: D = 1, rhs = -(z_L - z_U). */
+static void bound_sig(const Sol* s, int q, double* Sig, double* bg) {
+    const double mu = s->mu, kappa_d = 1e-5, sl = s->sb[q] - blo(s, q);
+    *Sig = s->zbl[q] / sl;
+    *bg = -mu / sl;
+    if (bhi_on(s, q)) {
+        const double su = bhi(s, q) - s->sb[q];
+        *Sig += s->zbu[q] / su;
+        *bg += mu / su;
+    } else {
+        *bg += kappa_d * mu;
+    }
+}
+static void bound_row(const Sol* s, int q, int mode, double dw, double* D, double* rhs) {
+    const double kappa_d = 1e-5, mu = s->mu;
+    if (mode != MODE_NEWTON) {
+        *D = 1.0;
+        *rhs = -(s->zbl[q] - (bhi_on(s, q) ? s->zbu[q] : 0.0));
+        return;
+    }
+    double Sig, bg;
+    bound_sig(s, q, &Sig, &bg);
+    const double st = Sig + dw;
+    if (s->resto) {
+        const int r = row_b(s, q);
+        const double pp = s->rp[r], nn = s->rn[r];
+        const double sp = s->rzp[r] / pp + dw, sn = s->rzn[r] / nn + dw;
+        const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+        const double E = -bg / st + (mu / pp - s->rho - kappa_d * mu) / sp - (mu / nn - s->rho - kappa_d * mu) / sn;
+        *D = 1.0 / C;
+        *rhs = (s->rcb[q] - E) / C;
+    } else {
+        *D = st;
+        *rhs = st * s->rcb[q] + bg;
+    }
+}
+
 static void build(Sol* s, int mode, double dw) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M, nzd = nx + nu;
@@ -1199,23 +1294,32 @@ static void build(Sol* s, int mode, double dw) {
             for (int a = 0; a < 3; ++a)
                 for (int b = 0; b < 3; ++b)
                     if (a < nx && b < nx) HH(a, b) += s->Hd[9 * k + a * 3 + b];
-            /* bound barriers Sigma and barrier gradient */
-            if (k < N)
+            /* bound barriers Sigma and barrier gradient (variable bounds; general_bounds: the bound rows below) */
+            if (k < N && !s->gcb)
                 for (int i = 0; i < nu; ++i) {
                     double sl = s->U[k * nu + i] - p->umin[i], su = p->umax[i] - s->U[k * nu + i];
                     HH(iu + i, iu + i) += s->zl[k * nu + i] / sl + s->zu[k * nu + i] / su;
                     g[iu + i] += -mu / sl + mu / su;
                 }
-            if (s->ns) {
+            if (s->ns && !s->gcb) {
                 HH(is, is) += s->zs[k] / s->S[k];
                 g[is] += -mu / s->S[k] + kappa_d * mu;
             }
             for (int i = 0; i < nzk; ++i) HH(i, i) += dw;
         } else {
             for (int i = 0; i < nzk; ++i) HH(i, i) = 1.0;
-            if (k < N)
+            if (k < N && !s->gcb)
                 for (int i = 0; i < nu; ++i) g[iu + i] += -s->zl[k * nu + i] + s->zu[k * nu + i];
-            if (s->ns) g[is] += -s->zs[k];
+            if (s->ns && !s->gcb) g[is] += -s->zs[k];
+        }
+        /* general_bounds: bound rows U_ki - sigma = 0 / S_k - sigma = 0 with sigma's barrier eliminated like t below
+         * (J = the unit vector of the variable) */
+        for (int c = 0; c < (s->gcb ? nvk : 0); ++c) {
+            const int q = c < nvk - s->ns ? k * nu + c : N * nu + k; /* stage column iu + c: controls, then slack */
+            double D, rhs;
+            bound_row(s, q, mode, dw, &D, &rhs);
+            HH(iu + c, iu + c) += D;
+            g[iu + c] += rhs;
         }
         /* eliminated inequality slacks t (IPOPT d(x) - t = 0, t >= 0) */
         for (int j = 0; j < M; ++j) {
@@ -1695,7 +1799,34 @@ static void recover(Sol* s, double dw) {
             for (int i = 0; i < nx; ++i) PN_STEP(row_d(s, k, i), s->yk_n[k * nx + i]);
         for (int j = 0; j < s->nc; ++j) PN_STEP(row_t(s, j), s->yt_n[j]);
     }
+    /* general_bounds: the bound rows' slack step, row multiplier and slack bound multipliers */
+    for (int q = 0; q < s->nb; ++q) {
+        const double dvar = bvar(s, s->dU, s->dS, q);
+        double Sig, bg;
+        bound_sig(s, q, &Sig, &bg);
+        const double st = Sig + dw;
+        if (s->resto) {
+            double D, rhs;
+            bound_row(s, q, MODE_NEWTON, dw, &D, &rhs);
+            const double yn = D * dvar + rhs; /* (J dz + r - E) / C */
+            s->yb_n[q] = yn;
+            s->dsb[q] = (yn - bg) / st;
+            PN_STEP(row_b(s, q), yn);
+        } else {
+            s->dsb[q] = dvar + s->rcb[q];
+            s->yb_n[q] = st * s->dsb[q] + bg;
+        }
+        const double sl = s->sb[q] - blo(s, q);
+        s->dzbl[q] = mu / sl - s->zbl[q] - (s->zbl[q] / sl) * s->dsb[q];
+        if (bhi_on(s, q)) {
+            const double su = bhi(s, q) - s->sb[q];
+            s->dzbu[q] = mu / su - s->zbu[q] + (s->zbu[q] / su) * s->dsb[q];
+        } else {
+            s->dzbu[q] = 0.0;
+        }
+    }
     #undef PN_STEP
+    if (s->gcb) return;
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
@@ -1779,14 +1910,18 @@ static double primal_frac(const Sol* s, double tau) {
     const NlotProblem* p = s->p;
     int nu = s->nu, N = s->N, M = s->M;
     double a = 1.0;
-    for (int k = 0; k < N; ++k)
+    for (int k = 0; k < (s->gcb ? 0 : N); ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
             a = frac_to_bound(s->U[q] - p->umin[i], s->dU[q], tau, a);
             a = frac_to_bound(p->umax[i] - s->U[q], -s->dU[q], tau, a);
         }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) a = frac_to_bound(s->S[k], s->dS[k], tau, a);
+    for (int q = 0; q < s->nb; ++q) {
+        a = frac_to_bound(s->sb[q] - blo(s, q), s->dsb[q], tau, a);
+        if (bhi_on(s, q)) a = frac_to_bound(bhi(s, q) - s->sb[q], -s->dsb[q], tau, a);
+    }
     for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->T[q], s->dT[q], tau, a);
     if (s->resto)
         for (int i = 0; i < s->ne; ++i) {
@@ -1798,12 +1933,16 @@ static double primal_frac(const Sol* s, double tau) {
 static double dual_frac(const Sol* s, double tau) {
     int nu = s->nu, N = s->N, M = s->M;
     double a = 1.0;
-    for (int q = 0; q < N * nu; ++q) {
+    for (int q = 0; q < (s->gcb ? 0 : N * nu); ++q) {
         a = frac_to_bound(s->zl[q], s->dzl[q], tau, a);
         a = frac_to_bound(s->zu[q], s->dzu[q], tau, a);
     }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) a = frac_to_bound(s->zs[k], s->dzs[k], tau, a);
+    for (int q = 0; q < s->nb; ++q) {
+        a = frac_to_bound(s->zbl[q], s->dzbl[q], tau, a);
+        if (bhi_on(s, q)) a = frac_to_bound(s->zbu[q], s->dzbu[q], tau, a);
+    }
     for (int q = 0; q < (N + 1) * M; ++q) a = frac_to_bound(s->vt[q], s->dvt[q], tau, a);
     if (s->resto)
         for (int i = 0; i < s->ne; ++i) {
@@ -1812,12 +1951,21 @@ static double dual_frac(const Sol* s, double tau) {
         }
     return a;
 }
+/* the full step: its arrays and their lengths (step_len doubles in all) */
+#define STEP_ARRAYS(s_)                                                                                            \
+    double* arrs[] = {s_->dX,  s_->dU,  s_->dS,  s_->dT,  s_->yi_n, s_->yk_n, s_->yt_n, s_->yd_n,                  \
+                      s_->dzl, s_->dzu, s_->dzs, s_->dvt, s_->dsb,  s_->yb_n, s_->dzbl, s_->dzbu};                 \
+    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1,   \
+                  (N + 1) * M, s_->nb, s_->nb, s_->nb, s_->nb};
+static int step_len(const Sol* s) {
+    int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
+    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX + 4 * s->nb;
+}
 /* save (dir=0) / restore (dir=1) the full step */
 static void step_save(Sol* s, double* buf, int dir) {
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
-    double* arrs[] = {s->dX, s->dU, s->dS, s->dT, s->yi_n, s->yk_n, s->yt_n, s->yd_n, s->dzl, s->dzu, s->dzs, s->dvt};
-    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1, (N + 1) * M};
-    for (int i = 0; i < 12; ++i) {
+    STEP_ARRAYS(s)
+    for (int i = 0; i < 16; ++i) {
         if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
         else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
         buf += lens[i];
@@ -1825,9 +1973,9 @@ static void step_save(Sol* s, double* buf, int dir) {
 }
 static void res_save(Sol* s, double* buf, int dir) {
     int nx = s->nx, N = s->N, M = s->M;
-    double* arrs[] = {s->rci, s->rcd, s->rct, s->rcq};
-    int lens[] = {XMAX, N * nx, CMAX, (N + 1) * M};
-    for (int i = 0; i < 4; ++i) {
+    double* arrs[] = {s->rci, s->rcd, s->rct, s->rcq, s->rcb};
+    int lens[] = {XMAX, N * nx, CMAX, (N + 1) * M, s->nb};
+    for (int i = 0; i < 5; ++i) {
         if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
         else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
         buf += lens[i];
@@ -1875,9 +2023,8 @@ static void afilt_add(Sol* s, double f, double th) {
 /* step = aff + sigma * cen over every step array (layout of step_save) */
 static void step_combine(Sol* s, const double* aff, const double* cen, double sigma) {
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
-    double* arrs[] = {s->dX, s->dU, s->dS, s->dT, s->yi_n, s->yk_n, s->yt_n, s->yd_n, s->dzl, s->dzu, s->dzs, s->dvt};
-    int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1, (N + 1) * M};
-    for (int a = 0; a < 12; ++a) {
+    STEP_ARRAYS(s)
+    for (int a = 0; a < 16; ++a) {
         for (int i = 0; i < lens[a]; ++i) arrs[a][i] = aff[i] + sigma * cen[i];
         aff += lens[a];
         cen += lens[a];
@@ -1903,14 +2050,18 @@ static double qf_eval(Sol* s, const QfCtx* q, double sigma) {
         double c_ = ((sl) + ap * (dsl)) * ((z) + ad * (dz));                                     \
         csq += c_ * c_;                                                                          \
     } while (0)
-    for (int k = 0; k < N; ++k)
+    for (int k = 0; k < (s->gcb ? 0 : N); ++k)
         for (int i = 0; i < nu; ++i) {
             int j = k * nu + i;
             CQ(s->U[j] - p->umin[i], s->dU[j], s->zl[j], s->dzl[j]);
             CQ(p->umax[i] - s->U[j], -s->dU[j], s->zu[j], s->dzu[j]);
         }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) CQ(s->S[k], s->dS[k], s->zs[k], s->dzs[k]);
+    for (int q = 0; q < s->nb; ++q) {
+        CQ(s->sb[q] - blo(s, q), s->dsb[q], s->zbl[q], s->dzbl[q]);
+        if (bhi_on(s, q)) CQ(bhi(s, q) - s->sb[q], -s->dsb[q], s->zbu[q], s->dzbu[q]);
+    }
     for (int j = 0; j < (N + 1) * M; ++j) CQ(s->T[j], s->dT[j], s->vt[j], s->dvt[j]);
 #undef CQ
     const Errs* e = q->e;
@@ -1988,15 +2139,15 @@ static double qf_sigma(Sol* s, const QfCtx* q, double mu_min, double mu_max) {
 /* iterate (primal + equality/bound multipliers; restoration p, n, zp, zn) save (dir 0) / load (dir 1) */
 static int iter_len(const Sol* s) {
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
-    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX + 4 * s->ne;
+    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX + 4 * s->ne + 4 * s->nb;
 }
 static void iter_io(Sol* s, double* buf, int dir) {
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     double* arrs[] = {s->X, s->U, s->S, s->T, s->yi, s->yk, s->yt, s->yd, s->zl, s->zu, s->zs, s->vt,
-                      s->rp, s->rn, s->rzp, s->rzn};
+                      s->rp, s->rn, s->rzp, s->rzn, s->sb, s->yb, s->zbl, s->zbu};
     int lens[] = {(N + 1) * nx, N * nu, N + 1, (N + 1) * M, nx, N * nx, CMAX, (N + 1) * M, N * nu, N * nu, N + 1,
-                  (N + 1) * M, s->ne, s->ne, s->ne, s->ne};
-    for (int i = 0; i < 16; ++i) {
+                  (N + 1) * M, s->ne, s->ne, s->ne, s->ne, s->nb, s->nb, s->nb, s->nb};
+    for (int i = 0; i < 20; ++i) {
         if (dir == 0) memcpy(buf, arrs[i], sizeof(double) * lens[i]);
         else memcpy(arrs[i], buf, sizeof(double) * lens[i]);
         buf += lens[i];
@@ -2004,7 +2155,7 @@ static void iter_io(Sol* s, double* buf, int dir) {
 }
 
 typedef struct { /* trial point buffers */
-    double *X, *U, *S, *T, *P, *N;
+    double *X, *U, *S, *T, *P, *N, *SB;
 } Trial;
 
 static void trial_primal(const Sol* s, double a, Trial* t) {
@@ -2013,6 +2164,7 @@ static void trial_primal(const Sol* s, double a, Trial* t) {
     for (int i = 0; i < N * nu; ++i) t->U[i] = s->U[i] + a * s->dU[i];
     for (int k = 0; k <= N; ++k) t->S[k] = s->S[k] + a * s->dS[k];
     for (int q = 0; q < (N + 1) * M; ++q) t->T[q] = s->T[q] + a * s->dT[q];
+    for (int q = 0; q < s->nb; ++q) t->SB[q] = s->sb[q] + a * s->dsb[q];
     if (s->resto)
         for (int i = 0; i < s->ne; ++i) {
             t->P[i] = s->rp[i] + a * s->rdp[i];
@@ -2020,9 +2172,9 @@ static void trial_primal(const Sol* s, double a, Trial* t) {
         }
 }
 static void trial_merit(const Sol* s, const Trial* t, double mu, double* th, double* ph, double* rci, double* rcd,
-                        double* rct, double* rcq) {
-    if (s->resto) merit_resto(s, t->X, t->U, t->S, t->T, t->P, t->N, mu, th, ph, rci, rcd, rct, rcq);
-    else merit_r(s, t->X, t->U, t->S, t->T, mu, th, ph, rci, rcd, rct, rcq);
+                        double* rct, double* rcq, double* rcb) {
+    if (s->resto) merit_resto(s, t->X, t->U, t->S, t->T, t->SB, t->P, t->N, mu, th, ph, rci, rcd, rct, rcq, rcb);
+    else merit_r(s, t->X, t->U, t->S, t->T, t->SB, mu, th, ph, rci, rcd, rct, rcq, rcb);
 }
 
 /* accept the trial point: primal (and equality multipliers, IPOPT alpha_for_y = primal) with alpha, bound
@@ -2039,20 +2191,26 @@ static void accept_step(Sol* s, double al, double az, const Trial* t) {
     for (int i = 0; i < N * nx; ++i) s->yk[i] += al * (s->yk_n[i] - s->yk[i]);
     for (int i = 0; i < s->nc; ++i) s->yt[i] += al * (s->yt_n[i] - s->yt[i]);
     for (int i = 0; i < (N + 1) * M; ++i) s->yd[i] += al * (s->yd_n[i] - s->yd[i]);
+    memcpy(s->sb, t->SB, sizeof(double) * s->nb);
+    for (int i = 0; i < s->nb; ++i) s->yb[i] += al * (s->yb_n[i] - s->yb[i]);
 #define ZUPD(z, dz, sl)                                                                          \
     do {                                                                                         \
         double zn = (z) + az * (dz), sv = (sl);                                                  \
         zn = fmax(fmin(zn, ks * mu / sv), mu / (ks * sv));                                       \
         (z) = zn;                                                                                \
     } while (0)
-    for (int k = 0; k < N; ++k)
+    for (int k = 0; k < (s->gcb ? 0 : N); ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
             ZUPD(s->zl[q], s->dzl[q], s->U[q] - p->umin[i]);
             ZUPD(s->zu[q], s->dzu[q], p->umax[i] - s->U[q]);
         }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k]);
+    for (int q = 0; q < s->nb; ++q) {
+        ZUPD(s->zbl[q], s->dzbl[q], s->sb[q] - blo(s, q));
+        if (bhi_on(s, q)) ZUPD(s->zbu[q], s->dzbu[q], bhi(s, q) - s->sb[q]);
+    }
     for (int q = 0; q < (N + 1) * M; ++q) ZUPD(s->vt[q], s->dvt[q], s->T[q]);
     if (s->resto) {
         memcpy(s->rp, t->P, sizeof(double) * s->ne);
@@ -2075,10 +2233,15 @@ static double barrier_gd(const Sol* s) {
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
-            gd += (s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
+            gd += (s->gcb ? s->gU[q] : s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
         }
     if (s->ns)
-        for (int k = 0; k <= N; ++k) gd += (s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
+        for (int k = 0; k <= N; ++k) gd += (s->gcb ? s->gS[k] : s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
+    for (int q = 0; q < s->nb; ++q) {
+        double Sig, bg;
+        bound_sig(s, q, &Sig, &bg);
+        gd += bg * s->dsb[q];
+    }
     for (int q = 0; q < (N + 1) * M; ++q) gd += (-mu / s->T[q] + kappa_d * mu) * s->dT[q];
     if (s->resto)
         for (int i = 0; i < s->ne; ++i)
@@ -2116,11 +2279,12 @@ static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double a
                      int only_full, double dw, Trial* t, double* alpha_out, double* az_out, int* ftype_armijo) {
     const NlotSolverOptions* o = s->o;
     int nx = s->nx, N = s->N, M = s->M;
-    const int nsave = (N + 1) * nx + 3 * N * s->nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX;
-    const int nres = XMAX + N * nx + CMAX + (N + 1) * M;
+    const int nsave = step_len(s);
+    const int nres = XMAX + N * nx + CMAX + (N + 1) * M + s->nb;
     double tri[XMAX], trt[CMAX];
-    double* trd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M));
+    double* trd = (double*)malloc(sizeof(double) * (N * nx + (N + 1) * M + s->nb + 1));
     double* trq = trd + N * nx;
+    double* trb = trq + (N + 1) * M;
     double alpha = skip_first ? 0.5 * amax : amax, az = az0;
     int accepted = 0, ntr = skip_first ? 1 : 0;
     s->last_rej_filter = 0;
@@ -2128,7 +2292,7 @@ static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double a
         ++ntr;
         trial_primal(s, alpha, t);
         double tht, pht;
-        trial_merit(s, t, s->mu, &tht, &pht, tri, trd, trt, trq);
+        trial_merit(s, t, s->mu, &tht, &pht, tri, trd, trt, trq, trb);
         const double at = ref->fixed_test ? ref->alpha_test : alpha;
         if (ls_accept(s, ref->theta, ref->phi, ref->gd, at, tht, pht, ftype_armijo)) {
             accepted = 1;
@@ -2144,11 +2308,12 @@ static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double a
             double* c0 = save + nsave;
             step_save(s, save, 0);
             res_save(s, c0, 0);
-            double *ci = s->rci, *cd = s->rcd, *ct = s->rct, *cq = s->rcq;
+            double *ci = s->rci, *cd = s->rcd, *ct = s->rct, *cq = s->rcq, *cb = s->rcb;
             for (int i = 0; i < nx; ++i) ci[i] = alpha * ci[i] + tri[i];
             for (int i = 0; i < N * nx; ++i) cd[i] = alpha * cd[i] + trd[i];
             for (int i = 0; i < s->nc; ++i) ct[i] = alpha * ct[i] + trt[i];
             for (int i = 0; i < (N + 1) * M; ++i) cq[i] = alpha * cq[i] + trq[i];
+            for (int i = 0; i < s->nb; ++i) cb[i] = alpha * cb[i] + trb[i];
             double th_old = tht;
             for (int pc = 0; pc < o->max_soc; ++pc) {
                 build(s, MODE_NEWTON, dw);
@@ -2157,7 +2322,7 @@ static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double a
                 const double asoc = primal_frac(s, tau);
                 trial_primal(s, asoc, t);
                 double ths, phs;
-                trial_merit(s, t, s->mu, &ths, &phs, tri, trd, trt, trq);
+                trial_merit(s, t, s->mu, &ths, &phs, tri, trd, trt, trq, trb);
                 if (ls_accept(s, ref->theta, ref->phi, ref->gd, alpha, ths, phs, ftype_armijo)) {
                     soc_ok = 1;
                     alpha = asoc;
@@ -2170,6 +2335,7 @@ static int backtrack(Sol* s, const LsRef* ref, double amax, double az0, double a
                 for (int i = 0; i < N * nx; ++i) cd[i] = asoc * cd[i] + trd[i];
                 for (int i = 0; i < s->nc; ++i) ct[i] = asoc * ct[i] + trt[i];
                 for (int i = 0; i < (N + 1) * M; ++i) cq[i] = asoc * cq[i] + trq[i];
+                for (int i = 0; i < s->nb; ++i) cb[i] = asoc * cb[i] + trb[i];
             }
             res_save(s, c0, 1);
             if (!soc_ok) step_save(s, save, 1);
@@ -2200,6 +2366,7 @@ static int tiny_step(const Sol* s, const Errs* e) {
     if (s->ns)
         for (int k = 0; k <= N; ++k) mx = fmax(mx, fabs(s->dS[k]) / (1.0 + fabs(s->S[k])));
     for (int q = 0; q < (N + 1) * M; ++q) mx = fmax(mx, fabs(s->dT[q]) / (1.0 + fabs(s->T[q])));
+    for (int q = 0; q < s->nb; ++q) mx = fmax(mx, fabs(s->dsb[q]) / (1.0 + fabs(s->sb[q])));
     if (mx > o->tiny_step_tol) return 0;
     for (int i = 0; i < nx; ++i) {
         my = fmax(my, fabs(s->yi_n[i] - s->yi[i]));
@@ -2216,6 +2383,10 @@ static int tiny_step(const Sol* s, const Errs* e) {
     for (int q = 0; q < (N + 1) * M; ++q) {
         my = fmax(my, fabs(s->yd_n[q] - s->yd[q]));
         ya = fmax(ya, fabs(s->yd[q]));
+    }
+    for (int q = 0; q < s->nb; ++q) {
+        my = fmax(my, fabs(s->yb_n[q] - s->yb[q]));
+        ya = fmax(ya, fabs(s->yb[q]));
     }
     if (my / (1.0 + ya) > o->tiny_step_y_tol) return 0;
     return e->primal < 1e-4;
@@ -2238,7 +2409,9 @@ static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, 
         if (p->enforce_heading || i != 2) s->tidx[s->nc++] = i;
     memcpy(s->x0, x0, sizeof(double) * p->nx);
     memcpy(s->xg, xg, sizeof(double) * p->nx);
-    s->ne = s->nx + s->N * s->nx + s->nc + (s->N + 1) * s->M;
+    s->gcb = o->general_bounds ? 1 : 0;
+    s->nb = s->gcb ? s->N * s->nu + s->ns * (s->N + 1) : 0;
+    s->ne = s->nx + s->N * s->nx + s->nc + (s->N + 1) * s->M + s->nb;
 }
 
 /* IPOPT MinC_1NrmRestorationPhase (Waechter & Biegler 2006 §3.3, IPOPT's documented defaults), run on the
@@ -2253,17 +2426,19 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     const double kappa_d = 1e-5, gt = 1e-5, gp = 1e-8;
     /* reference point x_R and the original merit there */
     double th_R, ph_R;
-    merit(s, s->X, s->U, s->S, s->T, s->mu, &th_R, &ph_R, NULL);
-    residuals(s, s->X, s->U, s->S, s->T, s->rci, s->rcd, s->rct, s->rcq);
+    merit(s, s->X, s->U, s->S, s->T, s->sb, s->mu, &th_R, &ph_R, NULL);
+    residuals(s, s->X, s->U, s->S, s->T, s->sb, s->rci, s->rcd, s->rct, s->rcq, s->rcb);
     double cmax = 0;
     for (int i = 0; i < nx; ++i) cmax = fmax(cmax, fabs(s->rci[i]));
     for (int i = 0; i < N * nx; ++i) cmax = fmax(cmax, fabs(s->rcd[i]));
     for (int j = 0; j < s->nc; ++j) cmax = fmax(cmax, fabs(s->rct[j]));
     for (int q = 0; q < (N + 1) * M; ++q) cmax = fmax(cmax, fabs(s->rcq[q]));
+    for (int q = 0; q < s->nb; ++q) cmax = fmax(cmax, fabs(s->rcb[q]));
     memcpy(r->X, s->X, sizeof(double) * (N + 1) * nx);
     memcpy(r->U, s->U, sizeof(double) * N * nu);
     memcpy(r->S, s->S, sizeof(double) * (N + 1));
     memcpy(r->T, s->T, sizeof(double) * (N + 1) * M);
+    memcpy(r->sb, s->sb, sizeof(double) * s->nb);
     memcpy(r->XR, s->X, sizeof(double) * (N + 1) * nx);
     memcpy(r->UR, s->U, sizeof(double) * N * nu);
     memcpy(r->SR, s->S, sizeof(double) * (N + 1));
@@ -2281,7 +2456,8 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
         const double c = i < nx ? s->rci[i]
                          : i < row_t(s, 0) ? s->rcd[i - nx]
                          : i < row_q(s, 0) ? s->rct[i - row_t(s, 0)]
-                                           : s->rcq[i - row_q(s, 0)];
+                         : i < row_b(s, 0) ? s->rcq[i - row_q(s, 0)]
+                                           : s->rcb[i - row_b(s, 0)];
         const double a = (mu - r->rho * c) / (2.0 * r->rho);
         const double n = a + sqrt(a * a + mu * c / (2.0 * r->rho));
         r->rn[i] = n;
@@ -2295,6 +2471,11 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     }
     for (int k = 0; k <= N; ++k) r->zs[k] = fmin(r->rho, s->zs[k]);
     for (int q = 0; q < (N + 1) * M; ++q) r->vt[q] = fmin(r->rho, s->vt[q]);
+    for (int q = 0; q < s->nb; ++q) {
+        r->zbl[q] = fmin(r->rho, s->zbl[q]);
+        r->zbu[q] = fmin(r->rho, s->zbu[q]);
+    }
+    memset(r->yb, 0, sizeof(double) * s->nb);
     memset(r->yi, 0, sizeof(double) * nx);
     memset(r->yk, 0, sizeof(double) * N * nx);
     memset(r->yt, 0, sizeof(double) * CMAX);
@@ -2303,14 +2484,15 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     r->dw_last = 0;
     {
         double th0, ph0;
-        merit_resto(r, r->X, r->U, r->S, r->T, r->rp, r->rn, r->mu, &th0, &ph0, NULL, NULL, NULL, NULL);
+        merit_resto(r, r->X, r->U, r->S, r->T, r->sb, r->rp, r->rn, r->mu, &th0, &ph0, NULL, NULL, NULL, NULL, NULL);
         r->theta_max = 1e4 * fmax(1.0, th0);
         r->theta_min = 1e-4 * fmax(1.0, th0);
     }
-    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M + 2 * r->ne;
+    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M + 2 * r->ne + r->nb;
     double* tb = (double*)malloc(sizeof(double) * ntr);
     Trial t = {tb, tb + (N + 1) * nx, tb + (N + 1) * nx + N * nu, tb + (N + 1) * nx + N * nu + N + 1,
-               tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M, tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M + r->ne};
+               tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M, tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M + r->ne,
+               tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M + 2 * r->ne};
     const double kap = o->barrier_tol_factor;
     const double mu_floor = fmin(o->tol, o->compl_inf_tol) / (kap + 1.0);
     int status = NLOT_RESTO_FAILED, first = 1;
@@ -2325,7 +2507,7 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
         }
         if (!first) { /* RestoConvergenceCheck: back to the regular iteration? */
             double th_o, ph_o;
-            merit(s, r->X, r->U, r->S, r->T, s->mu, &th_o, &ph_o, NULL);
+            merit(s, r->X, r->U, r->S, r->T, r->sb, s->mu, &th_o, &ph_o, NULL);
             if (th_o <= o->required_infeasibility_reduction * th_R && filter_ok(s, th_o, ph_o) &&
                 (cmp_le(th_o, (1.0 - gt) * th_R, th_R) || cmp_le(ph_o - ph_R, -gp * th_R, ph_R))) {
                 status = 0;
@@ -2335,11 +2517,12 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
                 const double thr = o->resto_failure_feasibility_threshold > 0 ? o->resto_failure_feasibility_threshold
                                                                               : 1e2 * o->tol;
                 double pinf = 0;
-                residuals(s, r->X, r->U, r->S, r->T, s->rci, s->rcd, s->rct, s->rcq);
+                residuals(s, r->X, r->U, r->S, r->T, r->sb, s->rci, s->rcd, s->rct, s->rcq, s->rcb);
                 for (int i = 0; i < nx; ++i) pinf = fmax(pinf, fabs(s->rci[i]));
                 for (int i = 0; i < N * nx; ++i) pinf = fmax(pinf, fabs(s->rcd[i]));
                 for (int j = 0; j < s->nc; ++j) pinf = fmax(pinf, fabs(s->rct[j]));
                 for (int q = 0; q < (N + 1) * M; ++q) pinf = fmax(pinf, fabs(s->rcq[q]));
+                for (int q = 0; q < s->nb; ++q) pinf = fmax(pinf, fabs(s->rcb[q]));
                 status = pinf <= thr ? NLOT_RESTO_FAILED : NLOT_INFEASIBLE;
                 break;
             }
@@ -2369,7 +2552,7 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
         recover(r, dw);
         const double tau = r->tau, amax = primal_frac(r, tau), az = dual_frac(r, tau);
         double theta, phi;
-        merit_resto(r, r->X, r->U, r->S, r->T, r->rp, r->rn, r->mu, &theta, &phi, NULL, NULL, NULL, NULL);
+        merit_resto(r, r->X, r->U, r->S, r->T, r->sb, r->rp, r->rn, r->mu, &theta, &phi, NULL, NULL, NULL, NULL, NULL);
         const double gd = barrier_gd(r);
         double amin = 1e-5;
         if (gd < 0) {
@@ -2406,24 +2589,36 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     const double mu0 = s->mu;
     double az = 1.0;
 #define DZ(z, so, sn) ((mu0 - (z) * (sn)) / (so))
-    for (int k = 0; k < N; ++k)
+    for (int q = 0; q < s->nb; ++q) {
+        s->dzbl[q] = DZ(s->zbl[q], s->sb[q] - blo(s, q), r->sb[q] - blo(s, q));
+        s->dzbu[q] = bhi_on(s, q) ? DZ(s->zbu[q], bhi(s, q) - s->sb[q], bhi(s, q) - r->sb[q]) : 0.0;
+    }
+    for (int k = 0; k < (s->gcb ? 0 : N); ++k)
         for (int i = 0; i < nu; ++i) {
             int q = k * nu + i;
             s->dzl[q] = DZ(s->zl[q], s->U[q] - p->umin[i], r->U[q] - p->umin[i]);
             s->dzu[q] = DZ(s->zu[q], p->umax[i] - s->U[q], p->umax[i] - r->U[q]);
         }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) s->dzs[k] = DZ(s->zs[k], s->S[k], r->S[k]);
     for (int q = 0; q < (N + 1) * M; ++q) s->dvt[q] = DZ(s->vt[q], s->T[q], r->T[q]);
 #undef DZ
     az = dual_frac(s, s->tau);
     double zmax = 0;
-    for (int i = 0; i < N * nu; ++i) {
+    for (int q = 0; q < s->nb; ++q) {
+        s->zbl[q] += az * s->dzbl[q];
+        zmax = fmax(zmax, s->zbl[q]);
+        if (bhi_on(s, q)) {
+            s->zbu[q] += az * s->dzbu[q];
+            zmax = fmax(zmax, s->zbu[q]);
+        }
+    }
+    for (int i = 0; i < (s->gcb ? 0 : N * nu); ++i) {
         s->zl[i] += az * s->dzl[i];
         s->zu[i] += az * s->dzu[i];
         zmax = fmax(zmax, fmax(s->zl[i], s->zu[i]));
     }
-    if (s->ns)
+    if (s->ns && !s->gcb)
         for (int k = 0; k <= N; ++k) {
             s->zs[k] += az * s->dzs[k];
             zmax = fmax(zmax, s->zs[k]);
@@ -2436,16 +2631,19 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
         for (int i = 0; i < N * nu; ++i) s->zl[i] = s->zu[i] = 1.0;
         for (int k = 0; k <= N; ++k) s->zs[k] = 1.0;
         for (int q = 0; q < (N + 1) * M; ++q) s->vt[q] = 1.0;
+        for (int q = 0; q < s->nb; ++q) s->zbl[q] = s->zbu[q] = 1.0;
     }
     free(zold);
     memcpy(s->X, r->X, sizeof(double) * (N + 1) * nx);
     memcpy(s->U, r->U, sizeof(double) * N * nu);
     memcpy(s->S, r->S, sizeof(double) * (N + 1));
     memcpy(s->T, r->T, sizeof(double) * (N + 1) * M);
+    memcpy(s->sb, r->sb, sizeof(double) * s->nb);
     memset(s->yi, 0, sizeof(double) * nx);
     memset(s->yk, 0, sizeof(double) * N * nx);
     memset(s->yt, 0, sizeof(double) * CMAX);
     memset(s->yd, 0, sizeof(double) * (N + 1) * M);
+    memset(s->yb, 0, sizeof(double) * s->nb);
     (void)kappa_d;
     return 0;
 }
@@ -2454,16 +2652,27 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
  * seen, [4] = final mu, [5] = E_0 (scaled overall error), [6] = restoration phases, [7] = watchdog /
  * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny),
  * [8] = theta (1-norm) at the last line-search failure, -1 if none.  info holds >= 9 doubles. */
+/* oracle_solve_one with an initial guess for the controls and slacks too (Uinit / Sinit, NULL = the reference's
+ * U = S = 0), pushed into their bounds as IPOPT pushes a starting point; test infrastructure (warm starts from a
+ * returned solution: is it a local optimum of the same NLP). */
+int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                      const double* xg, const double* Xinit, const double* Uinit, const double* Sinit, double* Xout,
+                      double* Uout, double* Sout, double* cost, int* iters_out, double* info);
 int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
                      const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
                      int* iters_out, double* info) {
+    return oracle_solve_warm(p, o, m, x0, xg, Xinit, NULL, NULL, Xout, Uout, Sout, cost, iters_out, info);
+}
+int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                      const double* xg, const double* Xinit, const double* Uinit, const double* Sinit, double* Xout,
+                      double* Uout, double* Sout, double* cost, int* iters_out, double* info) {
     Sol sol, *s = &sol, rsol, *r = &rsol;
     sol_setup(s, p, o, m, x0, xg);
     if (sol_alloc(s)) return NLOT_NUMERIC;
     int r_alloc = 0;
     int nx = s->nx, nu = s->nu, N = s->N, M = s->M;
     const double k1 = o->bound_push, k2 = o->bound_frac;
-    const int nsave = (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + CMAX;
+    const int nsave = step_len(s);
     double lin_resid = 0;
     double* qf_aff = (double*)malloc(sizeof(double) * 2 * nsave);
     double* qf_cen = qf_aff + nsave;
@@ -2476,9 +2685,17 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             double lo = p->umin[i], hi = p->umax[i];
             double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
             double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
-            s->U[k * nu + i] = fmin(fmax(0.0, lo + pl), hi - pu);
+            const double pushed = fmin(fmax(Uinit ? Uinit[k * nu + i] : 0.0, lo + pl), hi - pu);
+            /* general_bounds: U is free (Opti's initial value 0) and its row slack starts pushed into the bounds */
+            s->U[k * nu + i] = s->gcb ? (Uinit ? Uinit[k * nu + i] : 0.0) : pushed;
+            if (s->gcb) s->sb[k * nu + i] = pushed;
         }
-    for (int k = 0; k <= N; ++k) s->S[k] = s->ns ? fmax(0.0, k1) : 0.0;
+    for (int k = 0; k <= N; ++k) {
+        const double s0 = Sinit ? Sinit[k] : 0.0;
+        s->S[k] = (s->ns && !s->gcb) ? fmax(s0, k1) : (s->ns ? s0 : 0.0);
+        if (s->gcb && s->ns) s->sb[N * nu + k] = fmax(s0, k1); /* slack_bound_push of d(x0) = S_k */
+    }
+    for (int q = 0; q < s->nb; ++q) s->zbl[q] = s->zbu[q] = 1.0;
     for (int k = 0; k <= N; ++k) {
         jet d[NLOT_MAX_BODY];
         knot_ineq(p, m, s->X + k * nx, 0, d);
@@ -2504,6 +2721,10 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                 s->yd[q] = w - s->vt[q];
                 ymax = fmax(ymax, fabs(s->yd[q]));
             }
+        for (int q = 0; q < s->nb; ++q) { /* bound rows: y = J dz - (z_L - z_U), J the unit vector */
+            s->yb[q] = bvar(s, s->dU, s->dS, q) - (s->zbl[q] - (bhi_on(s, q) ? s->zbu[q] : 0.0));
+            ymax = fmax(ymax, fabs(s->yb[q]));
+        }
         memcpy(s->yi, s->yi_n, sizeof(double) * nx);
         memcpy(s->yk, s->yk_n, sizeof(double) * N * nx);
         memcpy(s->yt, s->yt_n, sizeof(double) * s->nc);
@@ -2515,11 +2736,12 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
             memset(s->yk, 0, sizeof(double) * N * nx);
             memset(s->yt, 0, sizeof(double) * CMAX);
             memset(s->yd, 0, sizeof(double) * (N + 1) * M);
+            memset(s->yb, 0, sizeof(double) * s->nb);
         }
     }
     {
         double th0, ph0;
-        merit(s, s->X, s->U, s->S, s->T, s->mu, &th0, &ph0, NULL);
+        merit(s, s->X, s->U, s->S, s->T, s->sb, s->mu, &th0, &ph0, NULL);
         s->theta_max = 1e4 * fmax(1.0, th0);
         s->theta_min = 1e-4 * fmax(1.0, th0);
     }
@@ -2527,9 +2749,10 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
     s->dw_last = 0;
     int status = NLOT_MAXITER, iter = 0;
     Errs e;
-    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M;
+    const int ntr = (N + 1) * nx + N * nu + (N + 1) + (N + 1) * M + s->nb;
     double* tb = (double*)malloc(sizeof(double) * ntr);
-    Trial t = {tb, tb + (N + 1) * nx, tb + (N + 1) * nx + N * nu, tb + (N + 1) * nx + N * nu + N + 1, NULL, NULL};
+    Trial t = {tb, tb + (N + 1) * nx, tb + (N + 1) * nx + N * nu, tb + (N + 1) * nx + N * nu + N + 1, NULL, NULL,
+               tb + (N + 1) * nx + N * nu + N + 1 + (N + 1) * M};
     /* watchdog (IPOPT StartWatchDog / StopWatchDog): saved iterate, direction and reference values */
     const int nit = iter_len(s);
     double* wd_it = (double*)malloc(sizeof(double) * (nit + nsave));
@@ -2584,7 +2807,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                 s->nafilt = 0;
             }
             double th_c, ph_c;
-            merit(s, s->X, s->U, s->S, s->T, s->mu, &th_c, &ph_c, NULL);
+            merit(s, s->X, s->U, s->S, s->T, s->sb, s->mu, &th_c, &ph_c, NULL);
             const double f_c = s->f;
             /* fixed mode: back to free mode as soon as the point makes sufficient progress w.r.t. the progress
              * filter ("Switching back to free mu mode", checked every iteration); otherwise one Fiacco-McCormick
@@ -2662,7 +2885,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
         const double tau = s->tau;
         double amax = primal_frac(s, tau), az = dual_frac(s, tau);
         double theta, phi;
-        merit(s, s->X, s->U, s->S, s->T, s->mu, &theta, &phi, NULL);
+        merit(s, s->X, s->U, s->S, s->T, s->sb, s->mu, &theta, &phi, NULL);
         const double gd = barrier_gd(s);
         double amin = 1e-5;
         if (gd < 0) {
@@ -2756,7 +2979,7 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                 const double a = fmin(amax, az);
                 trial_primal(s, a, &t);
                 double tht, pht;
-                trial_merit(s, &t, s->mu, &tht, &pht, NULL, NULL, NULL, NULL);
+                trial_merit(s, &t, s->mu, &tht, &pht, NULL, NULL, NULL, NULL, NULL);
                 int ft = 0, sat = ls_accept(s, ref.theta, ref.phi, ref.gd, 0.0, tht, pht, &ft);
                 int ok = sat;
                 if (!ok) {

@@ -41,6 +41,8 @@ def lib():
                                               C.c_double, dp, dp]
         L.oracle_solve_one.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
                                        C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, dp]
+        L.oracle_solve_warm.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
+                                         C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, dp, dp, ip, dp]
         L.oracle_solve_batch.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
                                          C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, ip,
                                          C.c_long, C.c_int]
@@ -135,7 +137,7 @@ def knot_constraints(problem, xk, sk=0.0, hm: HostMlp = None):
     return d[:m], g[:m]
 
 
-def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None):
+def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init=None, S_init=None):
     pc = problem.to_c()
     opt = opt or _abi.default_options()
     N, nx, nu = problem.N, problem.nx, problem.nu
@@ -148,8 +150,10 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None):
     x0 = np.ascontiguousarray(x0, np.float64)
     xg = np.ascontiguousarray(xg, np.float64)
     Xi = None if X_init is None else np.ascontiguousarray(X_init, np.float64)
-    st = lib().oracle_solve_one(C.byref(pc), C.byref(opt), C.byref(hm.desc) if hm else None, _dp(x0), _dp(xg),
-                                _dp(Xi), _dp(X), _dp(U), _dp(S), _dp(cost), it, _dp(info))
+    Ui = None if U_init is None else np.ascontiguousarray(U_init, np.float64)
+    Si = None if S_init is None else np.ascontiguousarray(S_init, np.float64)
+    st = lib().oracle_solve_warm(C.byref(pc), C.byref(opt), C.byref(hm.desc) if hm else None, _dp(x0), _dp(xg),
+                                 _dp(Xi), _dp(Ui), _dp(Si), _dp(X), _dp(U), _dp(S), _dp(cost), it, _dp(info))
     ev = int(info[7])
     return dict(status=st, X=X, U=U, S=S, cost=float(cost[0]), iters=int(it[0]), dual_inf=info[1],
                 constr_viol=info[2], lin_resid=info[3], mu=info[4], E0=info[5], resto_phases=int(info[6]),

