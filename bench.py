@@ -253,12 +253,13 @@ def main():
     ric_bytes = ric_bytes_per_solve(prob)
     ric_achieved = ric_solves_per_launch * ric_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     ric_traffic = None
-    tf = os.path.join(ROOT, "profiles", "r02", "kric_traffic.json")  # PMC, scripts/pmc_r02.sh
+    # PMC at bench size (B = 65536): scripts/pmc_r03.sh -> profiles/r03/pmc_traffic_r03m_B65536.json
+    tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_r03m_B65536.json")
+    pmc = None
     if os.path.exists(tf):
         with open(tf) as f:
-            per_solve = json.load(f).get("hbm_bytes_per_solve")
-        if per_solve is not None:
-            ric_traffic = per_solve * ric_solves_per_launch
+            pmc = json.load(f)
+        ric_traffic = pmc["k_ric"]["hbm_bytes_per_solve"] * ric_solves_per_launch
 
     flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1, 789,504 for 2-256x4-1
     flop_fwd = w.flops_per_point_fwd      # 33,536 / 394,752
@@ -269,11 +270,8 @@ def main():
     flop_launch = (agg["mlp_points_full"] * flop_pt - reused * flop_fwd) / n_l
     achieved = flop_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "r02", "mlp_traffic_in_solve.json")  # PMC inside the solve, pmc_r02.sh
-    if os.path.exists(tf):
-        with open(tf) as f:
-            t = json.load(f)
-        traffic = (t["full_fetch_bytes_per_point_corrected"] + t["full_write_bytes_per_point"]) * agg["mlp_points_full"] / n_l
+    if pmc is not None:  # HBM bytes per point of the full launch inside the solve at bench size
+        traffic = pmc["mlp_full"]["hbm_bytes_per_point"] * agg["mlp_points_full"] / n_l
     n_v = max(agg["mlp_value_launches"], 1)
     v_avg_ms = agg["mlp_value_ms"] / n_v
     v_achieved = agg["mlp_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
@@ -314,8 +312,10 @@ def main():
                     "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline.  The "
                     "second-order corrections (substitution with the stored factors, k_ric<DYN, false, true>) and the "
                     "restoration solves run on a side stream and are not counted in this launch's solves",
-            "pmc_note": "profiles/r02/kric_sq.json (B = 16384): 25.5 % of wave cycles issue (15.4 % VALU), 50.4 % "
-                        "wait on s_waitcnt (LDS hand-offs, DMA ring), 24.0 % issue-stalled (fp64 VALU pipe)",
+            "pmc_note": "traffic = HBM bytes per solve from profiles/r03/pmc_traffic_r03m_B65536.json (FETCH_SIZE x2 + "
+                        "WRITE_SIZE at B = 65536: 1.85x the algorithmic bytes) x solves per launch; phase timers "
+                        "(profiles/r03/kric_phase_timers_r03n.log): one solve takes ~160 us alone, ~400 us at B = 65536 "
+                        "(the forward sweep's memory passes 4x slower under load)",
         }
         mlp_full = {
             "kernel": kname % "full" + ": SDF-MLP value + gradient + Hessian",
@@ -335,6 +335,10 @@ def main():
             "points_per_launch": agg["mlp_points_full"] / n_l,
             "avg_launch_ms": avg_ms,
             "launches": agg["mlp_full_launches"],
+            "traffic_note": "HBM bytes per point in the solve at B = 65536 (profiles/r03/pmc_traffic_r03m_B65536.json): "
+                            "53.2 B/point = 1.07x the algorithmic 49.8 B/point with forward reuse (coordinates, the "
+                            "trial's value and ReLU pattern in, value + gradient + Hessian out), 1.66x the 32 B/point "
+                            "of a launch without reuse",
         }
         mlp_value = {
             "kernel": kname % "value" + ": line-search trial points, value only",

@@ -103,8 +103,17 @@ def test_restoration_full_solves_match_oracle(name):
     else:
         assert (sg == rc["status"]).mean() >= min(0.75, self_agree - 2 / B)
     if both.any():
-        assert (rel[both] <= 1e-4).mean() >= 0.8 or (rel[both] <= 1e-4).mean() >= (
-            np.abs(rp["cost"] - rc["cost"])[both] / np.abs(rc["cost"][both]) <= 1e-4).mean() - 2 / B
+        # final costs at tol 1e-4 are loose where the NLP is flat (b2 without slack: the oracle restarted at its own
+        # solution moves the cost by up to 1.5e-3): 1e-4 on 80 % of the jointly solved instances, or the GPU's
+        # differences within 3x the oracle's own run-to-run envelope (1e-13 start perturbation), quartile and max
+        selfb = both & (rp["status"] == 0)
+        rel_self = np.abs(rp["cost"] - rc["cost"])[selfb] / np.abs(rc["cost"][selfb])
+        q_self = np.quantile(rel_self, 0.75) if len(rel_self) else 0.0
+        m_self = rel_self.max() if len(rel_self) else 0.0
+        print(name, "cost envelope: gpu q75 / max", np.quantile(rel[both], 0.75), rel[both].max(), "oracle self",
+              q_self, m_self, flush=True)
+        assert (rel[both] <= 1e-4).mean() >= 0.8 or (
+            np.quantile(rel[both], 0.75) <= 3 * max(1e-4, q_self) and rel[both].max() <= 3 * max(1e-4, m_self))
     if name in ("b2_no_slack", "b6_settings_N100"):
         assert (sg == 0).sum() >= B // 2
 
@@ -127,7 +136,7 @@ def test_restoration_statuses_on_metric(artefact):
     x0, xg = sample_start_goal(METRIC_PROBLEM, 64, seed=0, sdf=sdf)
     opt = _abi.default_options()
     rg = solve_batch(METRIC_PROBLEM, x0, xg, mlp=DeviceMlp(artefact), options=opt)
-    rc = O.solve_batch(METRIC_PROBLEM, x0, xg, O.HostMlp(artefact), opt=opt, threads=8)
+    rc = O.solve_batch(METRIC_PROBLEM, x0, xg, O.HostMlp(artefact), opt=opt, threads=16)  # the box's CPU share
     sg = rg["status"].cpu().numpy()
     print("metric gpu", np.bincount(sg, minlength=7).tolist(), "oracle", np.bincount(rc["status"], minlength=7).tolist(),
           "agree", (sg == rc["status"]).mean(), flush=True)
