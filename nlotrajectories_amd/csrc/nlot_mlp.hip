@@ -462,31 +462,65 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     const float scale = w.scale;
     constexpr int TP = bf16_threads(FULL) / 2;  // points per block tile (32 per wave)
 
-    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += gridDim.x) {
+    // A block's tiles are tile0, tile0 + G, ...: each tile's inputs (point, the reuse source and, one tile later,
+    // the source's trial point / value / ReLU pattern) are loaded ahead, so the dependent global round trips of a
+    // tile overlap the previous tile's MFMA work (one wave per SIMD: nothing else hides their latency)
+    struct TileIn {
+        float px, py;
+        int src;
+    };
+    struct ReuseIn {
+        float tx, ty, tv;
+        uint32_t m0, m1;
+    };
+    const bool reuse_on = FULL && ru.src && ld == 0;
+    auto load_in = [&](int64_t tile, TileIn& a) {
+        const int64_t gi = tile * TP + wave * 32 + il;
+        a.px = a.py = 0.f;
+        a.src = -1;
+        if (gi < npts) {
+            const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
+            a.px = pts[2 * pi];
+            a.py = pts[2 * pi + 1];
+            if (reuse_on) a.src = ru.src[gi / P_per];
+        }
+    };
+    auto load_reuse = [&](int64_t tile, const TileIn& a, ReuseIn& r) {
+        r.tx = r.ty = r.tv = 0.f;
+        r.m0 = r.m1 = 0u;
+        if (reuse_on && a.src >= 0) {
+            const int64_t gi = tile * TP + wave * 32 + il;
+            const int64_t q = (int64_t)a.src * P_per + (gi - (gi / P_per) * P_per);
+            r.tx = ru.tpts[2 * q];
+            r.ty = ru.tpts[2 * q + 1];
+            r.tv = ru.tval[q];
+            r.m0 = ru.tmask[(2 * hl) * ru.plane + q];
+            r.m1 = ru.tmask[(2 * hl + 1) * ru.plane + q];
+        }
+    };
+    const int64_t G = gridDim.x;
+    TileIn in0, in1;
+    ReuseIn re0;
+    load_in(blockIdx.x, in0);
+    load_reuse(blockIdx.x, in0, re0);
+    load_in(blockIdx.x + G, in1);
+    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += G) {
+        TileIn in2;
+        ReuseIn re1;
+        load_in(tile + 2 * G, in2);
+        load_reuse(tile + G, in1, re1);
         const int64_t gi = tile * TP + wave * 32 + il;
         const bool valid = gi < npts;
         const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
-        float px = 0.f, py = 0.f;
-        if (valid) {
-            px = pts[2 * pi];
-            py = pts[2 * pi + 1];
-        }
+        const float px = in0.px, py = in0.py;
         // ---------------- forward reuse (full launches after an accepted trial point) ----------------
         float f = 0.f;
         uint64_t mask = 0;
         bool have = false;
-        if (FULL && ru.src && ld == 0) {
-            const int64_t rk = gi / P_per;
-            const int src = valid ? ru.src[rk] : -1;
-            if (src >= 0) {
-                const int64_t q = (int64_t)src * P_per + (gi - rk * P_per);
-                if (ru.tpts[2 * q] == px && ru.tpts[2 * q + 1] == py) {
-                    f = ru.tval[q];
-                    mask = (uint64_t)ru.tmask[(2 * hl) * ru.plane + q] |
-                           ((uint64_t)ru.tmask[(2 * hl + 1) * ru.plane + q] << 32);
-                    have = true;
-                }
-            }
+        if (reuse_on && valid && in0.src >= 0 && re0.tx == px && re0.ty == py) {
+            f = re0.tv;
+            mask = (uint64_t)re0.m0 | ((uint64_t)re0.m1 << 32);
+            have = true;
         }
         const bool skip = __all(have || !valid);  // wave-uniform
         if (FULL && skip && ru.nreused) {
@@ -641,6 +675,9 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 }
             }
         }
+        in0 = in1;  // the next tile's inputs (loaded during this tile)
+        in1 = in2;
+        re0 = re1;
     }
     if (FULL && ru.nreused) {  // statistics: full-launch points whose forward was reused
         __syncthreads();
