@@ -3,9 +3,10 @@
 
 One step = one batch of B synthetic start/goal instances per GPU of the metric NLP solved to completion:
 benchmark_3's body/bounds/slack penalty, N = 50 knots, learned SDF = the reference artefact FourierMLP
-(2-128-128-1, scale 10), linear initial guess.  By default (--continuous on) the K timed batches stream
-through the solver with B instances in flight (continuous batching, NlotSolverOptions.max_active; up to 4
-batches per nlot_solve_batch call), so one batch's latency-bound tail overlaps the next batch's bulk; every
+(2-128-128-1, scale 10), linear initial guess; B = 32,768 by default (so that `--steps 20 --warmup 5` fits
+600 s; `--batch 65536` measures ~7 % more).  By default (--continuous on) the K timed batches stream through the
+solver with B instances in flight (continuous batching, NlotSolverOptions.max_active; up to 8 batches, ~120 GB
+of workspace, per nlot_solve_batch call), so one batch's latency-bound tail overlaps the next batch's bulk; every
 instance's result is the same as in a call of its own.  Instances are independent, so each rank solves its
 own seeded batches (weak scaling) and the solved trajectories are gathered to rank 0 over RCCL after every
 solve call (the only collective).
@@ -60,7 +61,8 @@ def parse():
                     help="metric = BASELINE.json's headline config; stress = configs[4] (2-256x4-1 SDF MLP, N = 256); "
                          "b6 = configs[3] (benchmark 6 Ackermann + ring corridor, N = 100, trained SDF)")
     ap.add_argument("--batch", type=int, default=None,
-                    help="instances per GPU per step (metric default 65536, SURVEY.md §8d config 3; stress default "
+                    help="instances per GPU per step (metric default 32768, within SURVEY.md §8d config 3's range: the "
+                         "driver's --steps 20 --warmup 5 run fits its 600 s budget; 65536 measures ~7 %% more; stress default "
                          "8192 = 65536 over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=None,
@@ -137,11 +139,11 @@ def main():
     dev = torch.device("cuda", local)
     stress, b6 = a.workload == "stress", a.workload == "b6"
     if a.batch is None:
-        a.batch = 8192 if stress else 16384 if b6 else 65536
+        a.batch = 8192 if stress else 16384 if b6 else 32768
     if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
-        a.cpu_sample = 16 if stress else 32 if b6 else 256
+        a.cpu_sample = 16 if stress else 32 if b6 else 48
     if a.cpu_sample_1core is None:
-        a.cpu_sample_1core = 1 if stress else 2 if b6 else 16
+        a.cpu_sample_1core = 1 if stress else 2 if b6 else 3
     prob = STRESS_PROBLEM if stress else B6_PROBLEM if b6 else METRIC_PROBLEM
     if b6:
         wpath = os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")
@@ -176,7 +178,10 @@ def main():
     # continuous batching: the K timed batches go through ceil(K / G) solve calls of G <= 4 batches each, with
     # a.batch concurrent slots (the per-instance iterations are the same as in one call per batch)
     cont = a.continuous == "on" and not b6 and a.steps > 1
-    G, calls = batch_calls(a.steps, cont)
+    # batches per continuous-batching call: as many as ~120 GB of workspace holds, at most 8 (fewer calls, fewer
+    # latency-bound tails)
+    per_call = int(max(1, min(8, 120e9 // workspace_bytes(prob, a.batch))))
+    G, calls = batch_calls(a.steps, cont, per_call)
     ws = torch.empty(workspace_bytes(prob, a.batch * G), dtype=torch.uint8, device=dev)
     opt_cont = _abi.gpu_options(**{f: getattr(opt, f) for f, _ in opt._fields_})
     slots = a.slots or a.batch

@@ -244,7 +244,7 @@ def test_solution_satisfies_constraints():
         assert (U[b] >= -2 - 1e-9).all() and (U[b] <= 2 + 1e-9).all() and (S[b] >= 0).all()
 
 
-@pytest.mark.parametrize("case", ["metric", "b2"])
+@pytest.mark.parametrize("case", ["metric", "b2", "b2_many_waves"])
 def test_continuous_batching_same_results(artefact, case):
     """NlotSolverOptions.max_active < B (continuous batching: at most max_active instances in flight, the next
     ones admitted as others finish) gives every instance the same status, iterations, cost and trajectory as
@@ -264,10 +264,15 @@ def test_continuous_batching_same_results(artefact, case):
     else:
         p, mlp = BENCHMARKS["b2"]["problem"], None
         sdf = lambda P: np.sqrt(((np.asarray(P) - 0.5) ** 2).sum(1)) - 0.25
-        x0, xg = sample_start_goal(p, 48, seed=4, sdf=sdf, lo=(0, 0), hi=(1, 1))
-        slots = 7
-    ra = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options())
-    rc = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options(max_active=slots))
+        x0, xg = sample_start_goal(p, 64 if case == "b2_many_waves" else 48, seed=4, sdf=sdf, lo=(0, 0), hi=(1, 1))
+        slots = 2 if case == "b2_many_waves" else 7
+    # b2_many_waves: 32 admission waves of 2 instances at max_iter 5: the global step cap is per
+    # admission wave, so no instance is left unadmitted
+    kw = dict(max_iter=5) if case == "b2_many_waves" else {}
+    ra = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options(**kw))
+    rc = solve_batch(p, x0, xg, mlp=mlp, options=_abi.gpu_options(max_active=slots, **kw))
+    if case == "b2_many_waves":
+        assert (rc["iters"] > 0).all()
     print(case, "statuses", np.bincount(ra["status"].cpu().numpy(), minlength=7).tolist())
     for k in ("status", "iters", "cost", "X", "U", "S"):
         assert torch.equal(ra[k], rc[k]), k
