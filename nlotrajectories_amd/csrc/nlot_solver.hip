@@ -29,6 +29,7 @@
 #include <type_traits>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -1963,7 +1964,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 // ---------------------------------------------------------------------------------------------
 // kernels (one 64-lane workgroup = one instance; grid = active instances)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
+static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
                                                    const double* __restrict__ x0, const double* __restrict__ xg,
                                                    const double* __restrict__ Xinit) {
     const NlotProblem& p = *pp_;
@@ -2027,7 +2028,7 @@ __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict
 }
 
 // continuous batching: instances first .. first + n - 1 join the active list of the next step (its count cnt[2])
-__global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, int* __restrict__ cnt, int first, int n) {
+static __global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, int* __restrict__ cnt, int first, int n) {
     const int base = cnt[2];
     for (int t = threadIdx.x; t < n; t += blockDim.x) act[base + t] = first + t;
     __syncthreads();
@@ -2094,7 +2095,7 @@ __device__ void emit_points(const NlotProblem& p, const Dims& dm, const Ws& ws, 
 }
 
 // first global step: the corners of every instance (phase INIT)
-__global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+static __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                                const Ws* __restrict__ ws_, const int* __restrict__ active, int* cnt) {
     const Ws& ws = *ws_;
     const int b = active[blockIdx.x];
@@ -4276,7 +4277,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
     }
 }
 
-__global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
+static __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
                                                  double* cost, int32_t* status, int32_t* iters) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -4307,8 +4308,19 @@ __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
+// Per-dynamics compile units (Makefile): NLOT_UNIT = D >= 0 instantiates run<D> and run<D + NLOT_RK4_BIAS> only;
+// NLOT_UNIT = -1 holds the C ABI, the statistics and the dispatch; without NLOT_UNIT (tuning builds) one unit does all.
+#ifndef NLOT_UNIT
 static thread_local NlotSolveStats g_stats;
 static bool g_timing = false;
+#else
+extern thread_local NlotSolveStats g_stats;
+extern bool g_timing;
+#if NLOT_UNIT < 0
+thread_local NlotSolveStats g_stats;
+bool g_timing = false;
+#endif
+#endif
 
 static int validate(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlp* mlp, int64_t B) {
     if (!p || !o) { set_error("null problem/options"); return NLOT_ERR_INVALID; }
@@ -4364,7 +4376,7 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
 }
 
 template <int DYN>
-static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, const double* x0, const double* xg,
+int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, const double* x0, const double* xg,
                const double* Xinit, double* X, double* U, double* S, double* cost, int32_t* status, int32_t* iters,
                int64_t B, void* workspace, hipStream_t st) {
     const Dims dm = make_dims(p);
@@ -4474,11 +4486,22 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
     NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
     // fold the counters of steps synced .. last into g_stats (after a synchronisation); updates n_active
+    // NLOT_STEP_LOG=path (diagnostics, scripts/step_trace.py): one line per global step appended to path —
+    // step, active, full-eval instances, trial slots, reused points, Newton solves, restoration count, corrections,
+    // restoration solves, next active
+    static const char* step_log = getenv("NLOT_STEP_LOG");
+    std::vector<int> slog;
     auto fold = [&](int64_t last) {
         for (int64_t sj = synced; sj <= last; ++sj) {
             const int j = (int)(sj % kpipe), qj = (int)(sj & 1);
             const int* hc = res.hcnt + 16 * j + 8 * qj;
             const int next_active = res.hcnt[16 * j + 8 * (qj ^ 1) + 2];
+            if (step_log) {
+                slog.push_back((int)sj);
+                slog.push_back(n_active);
+                for (int c = 0; c < 8; ++c) slog.push_back(c == 2 ? 0 : hc[c]);
+                slog.push_back(next_active);
+            }
             g_stats.iterations = (int)(sj + 1);
             if (use_mlp) {
                 g_stats.mlp_points_full += (int64_t)hc[0] * P;
@@ -4617,14 +4640,37 @@ static int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* 
         set_error("nlot_solve_batch: the global step cap was reached with instances unfinished (phase-machine bug)");
         return NLOT_ERR_INVALID;
     }
+    if (step_log && !slog.empty()) {
+        if (FILE* f = fopen(step_log, "a")) {
+            for (size_t i = 0; i < slog.size(); i += 11) {
+                for (int c = 0; c < 11; ++c) fprintf(f, c ? " %d" : "%d", slog[i + c]);
+                fputc('\n', f);
+            }
+            fclose(f);
+        }
+    }
     hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);
     NLOT_HIP_CHECK(hipGetLastError());
     NLOT_HIP_CHECK(hipStreamSynchronize(st));
     return NLOT_OK;
 }
 
+#define NLOT_RUN_SIG(D)                                                                                            \
+    int run<D>(const NlotProblem&, const NlotSolverOptions&, const NlotMlp*, const double*, const double*,          \
+               const double*, double*, double*, double*, double*, int32_t*, int32_t*, int64_t, void*, hipStream_t)
+#if defined(NLOT_UNIT) && NLOT_UNIT >= 0
+template NLOT_RUN_SIG(NLOT_UNIT);
+template NLOT_RUN_SIG(NLOT_UNIT + NLOT_RK4_BIAS);
+#elif defined(NLOT_UNIT)
+#define NLOT_EXTERN_RUN(D) extern template NLOT_RUN_SIG(D); extern template NLOT_RUN_SIG(D + NLOT_RK4_BIAS);
+NLOT_EXTERN_RUN(0) NLOT_EXTERN_RUN(1) NLOT_EXTERN_RUN(2) NLOT_EXTERN_RUN(3) NLOT_EXTERN_RUN(4) NLOT_EXTERN_RUN(5)
+#undef NLOT_EXTERN_RUN
+#endif
+#undef NLOT_RUN_SIG
+
 }  // namespace nlot
 
+#if !defined(NLOT_UNIT) || NLOT_UNIT < 0
 extern "C" size_t nlot_solve_workspace_size(const NlotProblem* p, int64_t B) {
     if (!p) return 0;
     nlot::Dims d = nlot::make_dims(*p);
@@ -4680,3 +4726,4 @@ extern "C" void nlot_set_timing(int32_t en) { nlot::g_timing = en != 0; }
 extern "C" void nlot_last_stats(NlotSolveStats* out) {
     if (out) *out = nlot::g_stats;
 }
+#endif  // C ABI unit
