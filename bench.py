@@ -30,6 +30,8 @@ import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# a progress line on stderr every 30 s from inside the long continuous-batching solve calls
+os.environ.setdefault("NLOT_PROGRESS", "30")
 sys.path.insert(0, ROOT)
 
 from nlotrajectories_amd import _abi  # noqa: E402
@@ -76,7 +78,8 @@ def parse():
                          "(continuous batching, NlotSolverOptions.max_active; up to 4 batches per solve call), so one "
                          "batch's latency-bound tail overlaps the next batch's bulk; off: one solve call per batch")
     ap.add_argument("--slots", type=int, default=None,
-                    help="continuous batching: instances in flight (default --batch)")
+                    help="continuous batching: instances in flight (default 65536 metric, --batch otherwise; the "
+                         "workspace holds the slots' state only, ABI v10)")
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
     return ap.parse_args()
@@ -175,16 +178,15 @@ def main():
 
     from nlotrajectories_amd.solver import workspace_bytes
 
-    # continuous batching: the K timed batches go through ceil(K / G) solve calls of G <= 4 batches each, with
-    # a.batch concurrent slots (the per-instance iterations are the same as in one call per batch)
+    # continuous batching: the K timed batches stream through ONE solve call with `slots` concurrent slots (the
+    # workspace holds the slots' state, not the instances': ABI v10), so the latency-bound tail is paid once; the
+    # per-instance iterations are the same as in one call per batch
     cont = a.continuous == "on" and not b6 and a.steps > 1
-    # batches per continuous-batching call: as many as ~120 GB of workspace holds, at most 8 (fewer calls, fewer
-    # latency-bound tails)
-    per_call = int(max(1, min(8, 120e9 // workspace_bytes(prob, a.batch))))
-    G, calls = batch_calls(a.steps, cont, per_call)
-    ws = torch.empty(workspace_bytes(prob, a.batch * G), dtype=torch.uint8, device=dev)
+    slots = a.slots or (65536 if not (stress or b6) else a.batch)
+    G, calls = batch_calls(a.steps, cont, a.steps)
+    ws = torch.empty(max(workspace_bytes(prob, a.batch * G, slots if cont else 0),
+                         workspace_bytes(prob, a.batch * max(a.warmup, 1), slots)), dtype=torch.uint8, device=dev)
     opt_cont = _abi.gpu_options(**{f: getattr(opt, f) for f, _ in opt._fields_})
-    slots = a.slots or a.batch
     opt_cont.max_active = slots
     agg_keys = ("mlp_full_ms", "mlp_full_launches", "mlp_points_full", "mlp_value_ms", "mlp_value_launches",
                 "mlp_points_value", "iterations", "iterate_ms", "mlp_points_full_reused", "ric_ms", "ric_launches",
@@ -229,8 +231,11 @@ def main():
 
     warm_i = {"i": 0}
 
-    def timed_call():  # the timed region's i-th solve call (warm-up calls: one batch each)
+    def timed_call():  # the timed region's i-th solve call (the warm-up: its W batches in one call, untimed)
         if not timing["on"]:
+            if warm_i["i"] == 0 and cont and a.warmup > 1:
+                warm_i["i"] = a.warmup
+                return step(0, a.warmup)
             warm_i["i"] += 1
             return step(warm_i["i"] - 1, 1)
         i = call_iter["i"]
@@ -238,7 +243,8 @@ def main():
         call_iter["i"] += 1
         return step(a.warmup + sum(calls[:i]), g)
 
-    results, elapsed = timed_loop(timed_call, len(calls), a.warmup, world, sync, dev)
+    warm_calls = 1 if (cont and a.warmup > 1) else a.warmup  # the W warm-up batches: one continuous call
+    results, elapsed = timed_loop(timed_call, len(calls), warm_calls, world, sync, dev)
     set_timing(False)
     st_all = torch.cat([x["status"] for x in results]).long()
     it_all = torch.cat([x["iters"] for x in results]).double()
@@ -398,8 +404,9 @@ def main():
                 "knots": prob.N + 1,
                 "parallelism": f"instances sharded over {world} GPU(s); RCCL gather of solutions to rank 0",
                 "scheduling": (f"continuous batching: the {a.steps} timed batches of {a.batch} instances in "
-                               f"{len(calls)} solve call(s) of up to {G} batches through {slots} concurrent slots "
-                               "(NlotSolverOptions.max_active); each instance runs the same iterations as alone"
+                               f"{len(calls)} solve call(s) through {slots} concurrent slots (NlotSolverOptions.max_active; "
+                               "slot-indexed state, a finished instance's slot goes to the next one); each instance runs "
+                               "the same iterations as alone"
                                if cont else "one solve call per batch"),
                 "batches": f"{a.steps} distinct seeded draws per rank (seed + k, rank offset), resident in HBM "
                            "before the timed region",

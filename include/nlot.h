@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 9
+#define NLOT_ABI_VERSION 10
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -223,6 +223,9 @@ int32_t nlot_sdf_mlp_eval(const NlotMlp* mlp, const float* pts, int64_t P, float
 /* ---- batched trajectory optimisation ------------------------------------------------------ */
 /* Bytes of device workspace nlot_solve_batch needs for B instances. */
 size_t nlot_solve_workspace_size(const NlotProblem* prob, int64_t B);
+/* Bytes for B instances streamed through max_active slots (continuous batching, ABI v10): the workspace holds the
+ * slots' state only, so it depends on min(B, max_active), not on B (max_active <= 0: all B at once). */
+size_t nlot_solve_workspace_size_slots(const NlotProblem* prob, int64_t B, int32_t max_active);
 
 /* Solve B independent instances of `prob` (start x0[b], goal xg[b]) on the device.
  *   x0, xg    [B][nx] fp64 device
@@ -231,7 +234,8 @@ size_t nlot_solve_workspace_size(const NlotProblem* prob, int64_t B);
  *   cost      [B] fp64 (out: objective value, runner.py:80-98 / run_benchmark.py:166)
  *   status    [B] int32 (out: NLOT_SOLVED ...)   iters [B] int32 (out)
  *   mlp       required iff prob->sdf_kind == NLOT_SDF_MLP
- *   workspace >= nlot_solve_workspace_size(prob, B) bytes of device memory.
+ *   workspace >= nlot_solve_workspace_size_slots(prob, B, opt->max_active) bytes of device memory (per-slot state;
+ *             an instance writes its outputs when it finishes, and its slot goes to the next instance).
  * Returns when all instances finished (the host drives the iteration loop on `stream`). */
 int32_t nlot_solve_batch(const NlotProblem* prob, const NlotSolverOptions* opt, const NlotMlp* mlp,
                          const double* x0, const double* xg, const double* X_init, double* X,

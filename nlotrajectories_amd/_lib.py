@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 # symbols include/nlot.h declares (checked by tests/test_abi.py)
 EXPORTED = [
     "nlot_abi_version", "nlot_last_error", "nlot_default_options", "nlot_mlp_create", "nlot_mlp_destroy",
-    "nlot_sdf_mlp_eval", "nlot_solve_workspace_size", "nlot_solve_batch", "nlot_set_timing",
+    "nlot_sdf_mlp_eval", "nlot_solve_workspace_size", "nlot_solve_workspace_size_slots", "nlot_solve_batch", "nlot_set_timing",
     "nlot_last_stats", "nlot_casadi_bind", "nn_sdf_n_in", "nn_sdf_n_out", "nn_sdf_sparsity_in",
     "nn_sdf_sparsity_out", "nn_sdf", "jac_nn_sdf_n_in", "jac_nn_sdf_n_out", "jac_nn_sdf",
     "adj1_nn_sdf_n_in", "adj1_nn_sdf_n_out", "adj1_nn_sdf", "jac_adj1_nn_sdf_n_in",
@@ -63,6 +63,8 @@ def lib():
     L.nlot_sdf_mlp_eval.restype = C.c_int32
     L.nlot_solve_workspace_size.argtypes = [C.POINTER(_abi.NlotProblem), C.c_int64]
     L.nlot_solve_workspace_size.restype = C.c_size_t
+    L.nlot_solve_workspace_size_slots.argtypes = [C.POINTER(_abi.NlotProblem), C.c_int64, C.c_int32]
+    L.nlot_solve_workspace_size_slots.restype = C.c_size_t
     L.nlot_solve_batch.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions), vp, vp, vp, vp,
                                    vp, vp, vp, vp, vp, vp, C.c_int64, vp, C.c_size_t, vp]
     L.nlot_solve_batch.restype = C.c_int32
@@ -75,7 +77,7 @@ def lib():
     L.nlot_rrt_init.restype = C.c_int32
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 9:
+    if L.nlot_abi_version() != 10:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

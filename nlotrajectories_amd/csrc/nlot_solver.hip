@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <type_traits>
 #include <cmath>
 #include <cstdlib>
@@ -93,9 +94,16 @@ enum Scal {
     // and filter entries, restoration phases started (statistics)
     SC_RESTO, SC_RFIRST, SC_RMUO, SC_RTAUO, SC_RDWO, SC_THR, SC_PHR, SC_RHO, SC_ZETA, SC_RTHMAX, SC_RTHMIN,
     SC_RNFILT, SC_NRESTO,
+    // inertia correction carried over to the next global step (k_ric's attempt cap): the next delta_w to try (-1:
+    // none pending) and the delta_w already added into hg
+    SC_RETRY, SC_DWHG,
     SC_COUNT
 };
 constexpr int FILT_MAX = 64;
+// ints per step-parity counter set (workspace counters: 2 sets): [0..8) the phase machine's counts (Ws::cnt), [8..11)
+// diagnostics of the factorising Newton solves (attempts summed, their maximum, solves needing more than one), [13]
+// where k_admit's slots start in the active list.  After the two sets: the free-slot count and k_admit's error flag.
+constexpr int CSET = 16;
 constexpr int NSPEC = 8;  // step lengths evaluated per line-search round after a first rejection
 constexpr int MMAX = 4;  // inequalities per knot (rectangle without slack)
 
@@ -173,7 +181,7 @@ __host__ __device__ constexpr int ldl_len(int n) { return n * n + n; }
     X_(wdd, it_len(N, nx, nu, M)) X_(rp, ne_len(N, nx, M)) X_(rn, ne_len(N, nx, M)) X_(rzp, ne_len(N, nx, M))     \
     X_(rzn, ne_len(N, nx, M)) X_(rdp, ne_len(N, nx, M)) X_(rdn, ne_len(N, nx, M)) X_(rdzp, ne_len(N, nx, M))      \
     X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)   \
-    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx))
+    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx)) X_(x0s, nx) X_(xgs, nx)
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -189,11 +197,20 @@ struct Ws {
     float* tval[2];      // its values [slot][P]
     uint32_t* tmask[2];  // its hidden-layer ReLU patterns [4][slot][P]
     int* tsrc;           // per evaluation rank: trial slot whose forward the full launch may reuse, or -1
-    int* cnt;  // counters of step parity q at cnt + 8 q: [0] evaluation ranks, [1] trial slots, [2] next active
+    int* cnt;  // counters of step parity q at cnt + CSET q: [0] evaluation ranks, [1] trial slots, [2] next active
                // count, [3] full-launch points whose forward was reused, [4] Newton solves, [5] restoration list count,
                // [6] second-order corrections, [7] restoration Newton solves
     int* act[2]; // active instance lists (ping-pong)
     int* actr[2]; // the instances of act in a restoration phase (count: counter [5] of the step's set)
+    int* ricl;    // this step's factorising Newton solves (count: counter [4]), compacted by k_iter_a for k_ric
+    int* socl;    // this step's second-order corrections (count: counter [6])
+    // Slots: every array above is indexed by slot (cap slots); sinst[slot] is the instance a slot holds.  An instance
+    // leaving the active list (k_accept) writes its outputs (o*, instance-indexed, caller-owned) and frees its slot
+    // (freel, count at cnt[2 CSET]); k_admit gives free slots to the next instances, k_init_state starts them.
+    int* sinst;
+    int* freel;
+    double *oX, *oU, *oS, *ocost;
+    int32_t *ostat, *oiters;
     int64_t cap;
     int ppk;
 };
@@ -227,7 +244,9 @@ static size_t ws_bytes(const Dims& d, int64_t B, bool mlp) {
     }
     b += align256(2 * (size_t)B * sizeof(int));
     b += align256(2 * (size_t)B * sizeof(int));  // restoration lists
-    b += 256;  // counters
+    b += 2 * align256((size_t)B * sizeof(int));  // Newton-solve and correction lists
+    b += 2 * align256((size_t)B * sizeof(int));  // slot -> instance, free slots
+    b += 256;  // counters (2 sets of CSET ints)
     return b;
 }
 
@@ -268,6 +287,14 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
     w.actr[0] = (int*)c;
     w.actr[1] = (int*)c + B;
     c += align256(2 * (size_t)B * sizeof(int));
+    w.ricl = (int*)c;
+    c += align256((size_t)B * sizeof(int));
+    w.socl = (int*)c;
+    c += align256((size_t)B * sizeof(int));
+    w.sinst = (int*)c;
+    c += align256((size_t)B * sizeof(int));
+    w.freel = (int*)c;
+    c += align256((size_t)B * sizeof(int));
     w.cnt = (int*)c;
     return w;
 }
@@ -967,7 +994,8 @@ struct RicWpe {
 template <int DYN, bool RESTO, bool SOC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, SOC>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
-                                            const int* __restrict__ nact, int mode) {
+                                            const int* __restrict__ nact, int mode, int* __restrict__ diag,
+                                            int max_tries) {
     using R = RicG<DYN>;
     using SV = Solver<DYN>;
     constexpr int NX = R::NX, NU = R::NU, NV = R::NV, NZ = R::NZ, NC = R::NC, NCOL = R::NCOL, NQE = R::NQE;
@@ -988,6 +1016,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     if ((int)SC(SC_RIC) != 1) return;
     if ((SC(SC_RESTO) != 0.0) != RESTO) return;
     if (!RESTO && (SC(SC_RICFIX) >= 0.0) != SOC) return;
+    if (mode == MODE_LSQ && SC(SC_RETRY) >= 0.0) return;  // a deferred Newton solve, not an INIT instance
     typename R::Sh& sh = shg[grp];
     const int N = dm.N, nc = dm.nc, ns = dm.ns;
     const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
@@ -1678,6 +1707,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     const double fixdw = SC(SC_RICFIX);  // >= 0: second-order correction, stages built with this delta_w
     const bool fixed = fixdw >= 0.0;
     double dw = fixed ? fixdw : 0.0, dw_in_hg = dw;
+    // an inertia correction this instance started in an earlier launch (the attempt cap deferred it): hg holds
+    // dw_in_hg, the next delta_w of IPOPT's sequence is dw (the same sequence as in one launch)
+    const bool resume = !SOC && !RESTO && mode == MODE_NEWTON && !fixed && SC(SC_RETRY) >= 0.0;
+    if (resume) {
+        dw = SC(SC_RETRY);
+        dw_in_hg = SC(SC_DWHG);
+    }
     int fail = 0;
 #ifdef NLOT_PHASE_PROF
     long long t_build = 0, t_back = 0;
@@ -1685,7 +1721,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     PROF_T(tr0);
 #endif
     if constexpr (SOC) backward_rhs();
-    for (int attempt = 0; !SOC; ++attempt) {
+    int n_tries = 0;
+    bool deferred = false;
+    for (int attempt = resume ? 1 : 0; !SOC; ++attempt) {
+        ++n_tries;
 #ifdef NLOT_PHASE_PROF
         PROF_T(ta);
         ++n_att;
@@ -1706,10 +1745,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         if (!fail || mode != MODE_NEWTON || fixed) break;
         dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
         if (dw > 1e40) break;
+        // attempt cap (not RESTO): a wrong inertia after max_tries factorisations in this launch continues in the
+        // next global step's launch, so one instance's long delta_w sequence does not hold the whole launch
+        if (!RESTO && n_tries >= max_tries && (int)SC(SC_PHASE) == PH_EVAL) {
+            deferred = true;
+            break;
+        }
     }
 #ifdef NLOT_PHASE_PROF
     PROF_T(tr1);
 #endif
+    if (diag && l == 0 && !SOC && !RESTO && mode == MODE_NEWTON) {  // diagnostics (CSET [8..11))
+        atomicAdd(diag, n_tries);
+        atomicMax(diag + 1, n_tries);
+        if (n_tries > 1) atomicAdd(diag + 2, 1);
+    }
+    if (deferred) {  // SC_RIC stays 1: k_iter_b and k_accept pass the instance by, k_iter_a lists it again
+        if (l == 0) {
+            SC(SC_RETRY) = dw;
+            SC(SC_DWHG) = dw_in_hg;
+        }
+        return;
+    }
     if (fail) {
         __syncthreads();
         if (l == 0) {
@@ -1946,6 +2003,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 #endif
     if (l == 0) {
         if (dw > 0.0 && mode == MODE_NEWTON && !fixed) SC(SC_DWLAST) = dw;
+        SC(SC_RETRY) = -1.0;
         SC(SC_DW) = dw;
         SC(SC_RIC) = 2;
     }
@@ -1966,16 +2024,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 // ---------------------------------------------------------------------------------------------
 static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
                                                    const double* __restrict__ x0, const double* __restrict__ xg,
-                                                   const double* __restrict__ Xinit) {
+                                                   const double* __restrict__ Xinit, const int* __restrict__ adm,
+                                                   const int* __restrict__ adm_base) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
-    const int b = blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
+    // the first fill (adm = NULL): slot i holds instance i; an admission: the slots k_admit appended to the next
+    // active list at adm[*adm_base ..], holding the instances k_admit assigned (ws.sinst)
+    const int b = adm ? adm[*adm_base + (int)blockIdx.x] : (int)blockIdx.x;
+    const int64_t inst = adm ? ws.sinst[b] : b;
     const int N = dm.N, nx = dm.nx, nu = dm.nu, M = dm.M;
     const double k1 = o.bound_push, k2 = o.bound_frac;
+    for (int i = lane; i < nx; i += 64) {
+        AT(x0s, i) = x0[inst * nx + i];
+        AT(xgs, i) = xg[inst * nx + i];
+    }
     for (int e = lane; e < (N + 1) * nx; e += 64) {
         const int k = e / nx, i = e % nx;
-        const double v = Xinit ? Xinit[((size_t)b * (N + 1) + k) * nx + i]
-                               : x0[(size_t)b * nx + i] + (xg[(size_t)b * nx + i] - x0[(size_t)b * nx + i]) * ((double)k / (double)N);
+        const double v = Xinit ? Xinit[((size_t)inst * (N + 1) + k) * nx + i]
+                               : x0[inst * nx + i] + (xg[inst * nx + i] - x0[inst * nx + i]) * ((double)k / (double)N);
         AT(X, e) = v;  // LinearInitializer (trajectory_initialization.py:54-55)
         AT(dX, e) = 0.0;
     }
@@ -2023,16 +2090,36 @@ static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __r
         SC(SC_RESTO) = 0;
         SC(SC_RNFILT) = 0;
         SC(SC_NRESTO) = 0;
-        ws.act[0][b] = b;
+        SC(SC_RETRY) = -1.0;
+        if (!adm) {
+            ws.act[0][b] = b;
+            ws.sinst[b] = b;
+        }
     }
 }
 
-// continuous batching: instances first .. first + n - 1 join the active list of the next step (its count cnt[2])
-static __global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, int* __restrict__ cnt, int first, int n) {
-    const int base = cnt[2];
-    for (int t = threadIdx.x; t < n; t += blockDim.x) act[base + t] = first + t;
+// continuous batching: instances first .. first + n - 1 take the n most recently freed slots, which join the active
+// list of the next step (its count cnt[2]; the position they start at goes to cnt[13] for k_init_state).  The host
+// asks for n <= the free slots (capacity - next active count); a shortfall sets the error flag cnt[2 CSET + 1].
+static __global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, int* __restrict__ cnt, int* __restrict__ sinst,
+                                                        const int* __restrict__ freel, int* __restrict__ gcnt, int first,
+                                                        int n) {
+    const int base = cnt[2], nf = gcnt[0];
+    if (nf < n) {
+        if (threadIdx.x == 0) gcnt[1] = 1;
+        n = nf;
+    }
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const int slot = freel[nf - n + t];
+        act[base + t] = slot;
+        sinst[slot] = first + t;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) cnt[2] = base + n;
+    if (threadIdx.x == 0) {
+        cnt[2] = base + n;
+        cnt[13] = base;
+        gcnt[0] = nf - n;
+    }
 }
 
 // number of step lengths of a later line-search round starting at alpha a: a, a/2, ... while >= alpha_min,
@@ -2239,6 +2326,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     if (SC(SC_RESTO) != 0.0) return;  // k_resto_a
     const int ph = (int)SC(SC_PHASE);
     if (ph != PH_INIT && ph != PH_EVAL && ph != PH_SOC && ph != PH_SOFT2) return;
+    if (ph == PH_EVAL && SC(SC_RETRY) >= 0.0) {  // k_ric's inertia correction continues (attempt cap): stages kept
+        if (lane == 0 && !init_pass) ws.ricl[atomicAdd(&cnt[4], 1)] = b;
+        return;
+    }
     if (init_pass && ph != PH_INIT) return;
     double* SL = &AT(stg, 0);
     if (ph == PH_SOC) {
@@ -2253,7 +2344,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
             SC(SC_USEQF) = 0.0;
             SC(SC_RICFIX) = dw;
             SC(SC_RIC) = 1;
-            atomicAdd(&cnt[6], 1);  // statistics: second-order corrections (k_ric<DYN, false, true>)
+            ws.socl[atomicAdd(&cnt[6], 1)] = b;  // k_ric<DYN, false, true>'s list (and the statistics)
         }
         return;
     }
@@ -2701,7 +2792,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         SC(SC_PRIMAL) = primal;
         SC(SC_RICFIX) = -1.0;
         SC(SC_RIC) = 1;
-        atomicAdd(&cnt[4], 1);  // statistics: Newton solves of this step (k_ric's work)
+        ws.ricl[atomicAdd(&cnt[4], 1)] = b;  // k_ric's list of Newton solves (and the statistics)
     }
 }
 
@@ -3196,6 +3287,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     emit_points(p, dm, ws, b, lane, cnt, true, tp, tiny ? 0 : 1, amax);
 }
 
+// An instance leaves the active list (k_accept): its outputs (X, U, S, cost = the objective at X, status, iterations;
+// run_benchmark.py:146-167) go to the caller's arrays at its instance index, and its slot joins the free list.
+__device__ void retire(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane) {
+    const int N = dm.N, nx = dm.nx, nu = dm.nu;
+    const size_t inst = (size_t)ws.sinst[b];
+    for (int i = lane; i < (N + 1) * nx; i += 64) ws.oX[inst * (N + 1) * nx + i] = AT(X, i);
+    for (int i = lane; i < N * nu; i += 64) ws.oU[inst * N * nu + i] = AT(U, i);
+    if (ws.oS)
+        for (int k = lane; k <= N; k += 64) ws.oS[inst * (N + 1) + k] = dm.ns ? AT(S, k) : 0.0;
+    const double c = objective_w(p, dm, ws, b, lane, 0.0);
+    if (lane == 0) {
+        ws.ocost[inst] = c;
+        const int st = (int)SC(SC_STATUS);
+        ws.ostat[inst] = st < 0 ? NLOT_MAXITER : st;
+        ws.oiters[inst] = (int)SC(SC_ITERS);
+        ws.freel[atomicAdd(&ws.cnt[2 * CSET], 1)] = b;
+    }
+}
+
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_accept(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* __restrict__ next,
@@ -3524,7 +3634,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
     }
     wsync();
     ph = (int)SC(SC_PHASE);
-    if (ph != PH_DONE && lane == 0) {  // the next step's active list (and restoration list) and counts
+    if (ph == PH_DONE) {
+        retire(p, dm, ws, b, lane);
+    } else if (lane == 0) {  // the next step's active list (and restoration list) and counts
         next[atomicAdd(&cnt_next[2], 1)] = b;
         if (SC(SC_RESTO) != 0.0) nextr[atomicAdd(&cnt_next[5], 1)] = b;
     }
@@ -4277,34 +4389,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
     }
 }
 
-static __global__ __launch_bounds__(64) void k_finalize(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, Ws ws, double* Xo, double* Uo, double* So,
-                                                 double* cost, int32_t* status, int32_t* iters) {
-    const NlotProblem& p = *pp_;
-    const Dims& dm = *dd_;
-    const int b = blockIdx.x, lane = threadIdx.x;
-    const int N = dm.N, nx = dm.nx, nu = dm.nu;
-    for (int i = lane; i < (N + 1) * nx; i += 64) {
-        Xo[(size_t)b * (N + 1) * nx + i] = AT(X, i);
-        AT(dX, i) = 0;
-    }
-    for (int i = lane; i < N * nu; i += 64) {
-        Uo[(size_t)b * N * nu + i] = AT(U, i);
-        AT(dU, i) = 0;
-    }
-    for (int k = lane; k <= N; k += 64) {
-        if (So) So[(size_t)b * (N + 1) + k] = dm.ns ? AT(S, k) : 0.0;
-        AT(dS, k) = 0;
-    }
-    wsync();
-    const double c = objective_w(p, dm, ws, b, lane, 0.0);
-    if (lane == 0) {
-        cost[b] = c;
-        const int st = (int)SC(SC_STATUS);
-        status[b] = st < 0 ? NLOT_MAXITER : st;
-        iters[b] = (int)SC(SC_ITERS);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
@@ -4381,7 +4465,15 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
                int64_t B, void* workspace, hipStream_t st) {
     const Dims dm = make_dims(p);
     const bool use_mlp = p.sdf_kind == NLOT_SDF_MLP;
-    Ws ws = carve(dm, B, use_mlp, workspace);
+    // slots: min(B, max_active) (continuous batching) or B; the workspace holds the slots' state only
+    const int cap_slots = (int)(o.max_active > 0 && o.max_active < B ? o.max_active : B);
+    Ws ws = carve(dm, cap_slots, use_mlp, workspace);
+    ws.oX = X;
+    ws.oU = U;
+    ws.oS = S;
+    ws.ocost = cost;
+    ws.ostat = status;
+    ws.oiters = iters;
     NlotProblem* dP = (NlotProblem*)((char*)workspace + kHdrProblem);
     Dims* dD = (Dims*)((char*)workspace + kHdrDims);
     Ws* dW = (Ws*)((char*)workspace + kHdrWs);
@@ -4393,7 +4485,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     const int Bi = (int)B;
     const int64_t P = (int64_t)dm.ppk * (dm.N + 1);
     g_stats = NlotSolveStats{};
-    hipLaunchKernelGGL(k_init_state, dim3(Bi), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit);
+    hipLaunchKernelGGL(k_init_state, dim3(cap_slots), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit, nullptr, nullptr);
     NLOT_HIP_CHECK(hipGetLastError());
     // Steps run ahead of the host: every kernel reads its step's active count on the device (cnt[2] of the
     // step's counter set, written by the previous step's k_accept), and grids are sized by the host's last
@@ -4405,7 +4497,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     struct Res {
         int* hcnt = nullptr;
         hipEvent_t ev[KPIPE][8] = {};
-        hipStream_t s2 = nullptr;                                   // side stream: SOC and restoration solves
+        hipStream_t s2 = nullptr, s3 = nullptr;                     // side streams: SOC / restoration solves
         hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr;  // fork after k_iter_a, joins
         ~Res() {
             for (auto& r : ev)
@@ -4414,26 +4506,28 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             for (hipEvent_t e : {e_a, e_soc, e_r})
                 if (e) (void)hipEventDestroy(e);
             if (s2) (void)hipStreamDestroy(s2);
+            if (s3) (void)hipStreamDestroy(s3);
             if (hcnt) (void)hipHostFree(hcnt);
         }
     } res;
-    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, KPIPE * 16 * sizeof(int), hipHostMallocDefault));
+    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, KPIPE * 2 * CSET * sizeof(int), hipHostMallocDefault));
     // The second-order corrections (substitution, short) and the restoration instances' Newton solves (a longer
     // sequential sweep, few instances) touch disjoint instances from the main Newton solve: they run on a side
     // stream, forked after k_iter_a, so their latency hides under k_ric's; k_iter_b joins the corrections, the
     // value-MLP launch joins the restoration chain (k_resto_b appends to the same trial list).
     NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s2, hipStreamNonBlocking));
+    NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s3, hipStreamNonBlocking));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_a, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_soc, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_r, hipEventDisableTiming));
-    hipStream_t s2 = res.s2;
+    hipStream_t s2 = res.s2, s3 = res.s3;
     if (g_timing)
         for (int k = 0; k < KPIPE; ++k)
             for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
     MlpOut mo{}, mo_t[2] = {};
     MlpReuse reuse[2] = {};
     if (use_mlp) {
-        const int64_t plane = P * B * NSPEC;
+        const int64_t plane = P * (int64_t)cap_slots * NSPEC;  // the MLP output planes hold the slots' points
         mo.val = ws.mo; mo.gx = ws.mo + plane; mo.gy = ws.mo + 2 * plane; mo.hxx = ws.mo + 3 * plane;
         mo.hxy = ws.mo + 4 * plane; mo.hyx = mo.hxy; mo.hyy = ws.mo + 5 * plane;
         mo.sv = mo.sg = mo.sh = 1;
@@ -4460,6 +4554,15 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     }
     if (const char* e = getenv("NLOT_SPEC_THRESHOLD")) spec_threshold = atoi(e);
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
+    // k_ric's inertia-correction attempts per launch while more than ric_tries_min instances are active (the rest of
+    // an instance's delta_w sequence continues in the next step's launch)
+    int ric_tries = 2, ric_tries_min = 2048;
+    if (const char* e = getenv("NLOT_RIC_TRIES")) ric_tries = std::max(1, atoi(e));
+    if (const char* e = getenv("NLOT_RIC_TRIES_MIN")) ric_tries_min = atoi(e);
+    double progress_s = 0, t_prog = 0;
+    if (const char* e = getenv("NLOT_PROGRESS")) progress_s = atof(e);
+    t_prog = progress_s;
+    const auto t_prog0 = std::chrono::steady_clock::now();
     int kpipe = KPIPE;
     if (const char* e = getenv("NLOT_PIPE")) kpipe = std::max(1, std::min(KPIPE, atoi(e)));
     // a safety net against a phase-machine bug, not an iteration limit (max_iter bounds every instance): at most
@@ -4472,7 +4575,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     // list and run their INIT step (corners, slack push, least-squares multipliers) in the next step.  Every
     // instance runs the same iteration sequence whenever it starts, so the results do not depend on capacity;
     // what changes is that the latency-bound tail of one group overlaps the bulk of the next.
-    const int capacity = o.max_active > 0 && o.max_active < Bi ? o.max_active : Bi;
+    const int capacity = cap_slots;
     const int min_admit = std::max(1, capacity / 32);
     int next_admit = capacity;
     bool init_step = true;  // this step runs the INIT pass (step 0, and the step after an admission)
@@ -4481,7 +4584,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     int resto_bound = o.resto ? Bi : 0;
     int rc = NLOT_OK, n_active = capacity, cur = 0, synced = 0;
     int64_t step = 0;
-    NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 16 * sizeof(int), st));
+    NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 64 * sizeof(int), st));  // both sets, the free-slot count, error flag
     res.hcnt[0] = capacity;  // step 0's active count (cnt[2] of counter set 0)
     NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
@@ -4489,18 +4592,19 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     // NLOT_STEP_LOG=path (diagnostics, scripts/step_trace.py): one line per global step appended to path —
     // step, active, full-eval instances, trial slots, reused points, Newton solves, restoration count, corrections,
     // restoration solves, next active
-    static const char* step_log = getenv("NLOT_STEP_LOG");
+    const char* step_log = getenv("NLOT_STEP_LOG");
     std::vector<int> slog;
     auto fold = [&](int64_t last) {
         for (int64_t sj = synced; sj <= last; ++sj) {
             const int j = (int)(sj % kpipe), qj = (int)(sj & 1);
-            const int* hc = res.hcnt + 16 * j + 8 * qj;
-            const int next_active = res.hcnt[16 * j + 8 * (qj ^ 1) + 2];
+            const int* hc = res.hcnt + 2 * CSET * j + CSET * qj;
+            const int next_active = res.hcnt[2 * CSET * j + CSET * (qj ^ 1) + 2];
             if (step_log) {
                 slog.push_back((int)sj);
                 slog.push_back(n_active);
                 for (int c = 0; c < 8; ++c) slog.push_back(c == 2 ? 0 : hc[c]);
                 slog.push_back(next_active);
+                for (int c = 8; c < 11; ++c) slog.push_back(hc[c]);
             }
             g_stats.iterations = (int)(sj + 1);
             if (use_mlp) {
@@ -4545,9 +4649,9 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
         // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
         const int q = step & 1;
-        int* C = ws.cnt + 8 * q;
-        int* Cn = ws.cnt + 8 * (q ^ 1);
-        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, 8 * sizeof(int), st));
+        int* C = ws.cnt + CSET * q;
+        int* Cn = ws.cnt + CSET * (q ^ 1);
+        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, CSET * sizeof(int), st));
         // speculative backtracking only while the GPU is latency-bound (few active instances); in the
         // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
@@ -4563,36 +4667,41 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         }
         if (ev[4]) (void)hipEventRecord(ev[4], st);
         if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
-            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 1, C, Cn);
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs, 1, C, Cn);
             hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
-                               st, dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ);
+                               st, dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ, nullptr, 1 << 30);
         }
         // restoration phases (list actr, count C[5]): before k_iter_a, which continues the iteration of an instance
         // that k_resto_a returns to the original problem
         const int n_resto = std::min(n_active, resto_bound);
         if (n_resto > 0)
-            hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, x0, xg, C);
-        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, x0, xg, 0, C, Cn);
+            hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C);
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs, 0, C, Cn);
+        // the Newton solves and the corrections run over the compacted lists k_iter_a wrote (ws.ricl / ws.socl,
+        // counts C[4] / C[6]; the grids are host bounds, blocks past the count exit): one group per instance that
+        // has work, so a launch holds as many wavefronts as it has solves / 4
         NLOT_HIP_CHECK(hipEventRecord(res.e_a, st));
         NLOT_HIP_CHECK(hipStreamWaitEvent(s2, res.e_a, 0));
         hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
-                           s2, dP, dD, dW, act, n_active, C + 2, (int)MODE_NEWTON);
+                           s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
         NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
-        if (n_resto > 0) {
-            hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s2,
-                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON);
-            hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, s2, dP, dD, o, dW, actr, C,
+        if (n_resto > 0) {  // the restoration chain on a stream of its own (disjoint instances)
+            NLOT_HIP_CHECK(hipStreamWaitEvent(s3, res.e_a, 0));
+            hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s3,
+                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON, nullptr, 1 << 30);
+            hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, s3, dP, dD, o, dW, actr, C,
                                use_mlp ? ws.tpts[q] : nullptr);
+            NLOT_HIP_CHECK(hipEventRecord(res.e_r, s3));
         }
-        NLOT_HIP_CHECK(hipEventRecord(res.e_r, s2));
         if (ev[6]) (void)hipEventRecord(ev[6], st);
         hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, st,
-                           dP, dD, dW, act, n_active, C + 2, (int)MODE_NEWTON);
+                           dP, dD, dW, ws.ricl, n_active, C + 4, (int)MODE_NEWTON, C + 8,
+                           n_active > ric_tries_min ? ric_tries : 1 << 30);
         if (ev[6]) (void)hipEventRecord(ev[7], st);
         NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_soc, 0));
         hipLaunchKernelGGL(k_iter_b<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, C,
                            use_mlp ? ws.tpts[q] : nullptr, Cn);
-        NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_r, 0));
+        if (n_resto > 0) NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_r, 0));
         if (ev[4]) (void)hipEventRecord(ev[5], st);
         if (use_mlp) {
             if (ev[0]) (void)hipEventRecord(ev[2], st);
@@ -4604,27 +4713,41 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         // the next round's candidate count uses this step's nspec (n_active only shrinks: speculation
         // starts at most KPIPE steps late; the accepted alpha is the same either way)
         if (n_resto > 0)
-            hipLaunchKernelGGL(k_resto_ls<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, x0, xg, C, Cn,
+            hipLaunchKernelGGL(k_resto_ls<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C, Cn,
                                use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
-        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, nxtr, x0, xg, C, Cn,
+        hipLaunchKernelGGL(k_accept<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, nxt, nxtr, ws.x0s, ws.xgs, C, Cn,
                            use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
         // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
-        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 16 * kq, ws.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
+        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 2 * CSET * kq, ws.cnt, 2 * CSET * sizeof(int), hipMemcpyDeviceToHost, st));
         cur ^= 1;
         init_step = false;
         if (kq != kpipe - 1) continue;
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         // restoration lists of the window: the next launches' grid bound (their kernels read the exact count)
         int rmax = 0;
-        for (int j = 0; j <= kq; ++j) rmax = std::max(rmax, res.hcnt[16 * j + 8 * (((step - kq + j) & 1) ^ 1) + 5]);
+        for (int j = 0; j <= kq; ++j) rmax = std::max(rmax, res.hcnt[2 * CSET * j + CSET * (((step - kq + j) & 1) ^ 1) + 5]);
         resto_bound = std::min(Bi, 2 * rmax + 256);
         fold(step);
+        if (progress_s > 0) {  // NLOT_PROGRESS=seconds: a line on stderr now and then (long continuous calls)
+            const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_prog0).count();
+            if (t >= t_prog) {
+                fprintf(stderr, "[nlot] %.0f s: step %lld, %d active, %d of %d instances admitted\n", t, (long long)step,
+                        n_active, next_admit, Bi);
+                fflush(stderr);
+                t_prog = t + progress_s;
+            }
+        }
         if (next_admit < Bi && (capacity - n_active >= min_admit || n_active == 0)) {
-            // append instances next_admit .. next_admit + n_new - 1 to the next step's active list and count
+            // instances next_admit .. next_admit + n_new - 1 take free slots (the free-slot count is capacity - the
+            // next active count: every instance that left the list freed its slot), join the next step's active
+            // list, and start (k_init_state on those slots)
             const int n_new = std::min(capacity - n_active, Bi - next_admit);
-            hipLaunchKernelGGL(k_admit, dim3(1), dim3(1024), 0, st, ws.act[cur], ws.cnt + 8 * ((step + 1) & 1), next_admit,
-                               n_new);
+            int* Cadm = ws.cnt + CSET * ((step + 1) & 1);
+            hipLaunchKernelGGL(k_admit, dim3(1), dim3(1024), 0, st, ws.act[cur], Cadm, ws.sinst, ws.freel,
+                               ws.cnt + 2 * CSET, next_admit, n_new);
+            hipLaunchKernelGGL(k_init_state, dim3(n_new), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit, ws.act[cur],
+                               Cadm + 13);
             NLOT_HIP_CHECK(hipGetLastError());
             next_admit += n_new;
             n_active += n_new;
@@ -4642,16 +4765,20 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     }
     if (step_log && !slog.empty()) {
         if (FILE* f = fopen(step_log, "a")) {
-            for (size_t i = 0; i < slog.size(); i += 11) {
-                for (int c = 0; c < 11; ++c) fprintf(f, c ? " %d" : "%d", slog[i + c]);
+            for (size_t i = 0; i < slog.size(); i += 14) {
+                for (int c = 0; c < 14; ++c) fprintf(f, c ? " %d" : "%d", slog[i + c]);
                 fputc('\n', f);
             }
             fclose(f);
         }
     }
-    hipLaunchKernelGGL(k_finalize, dim3(Bi), dim3(64), 0, st, dP, dD, ws, X, U, S, cost, status, iters);
-    NLOT_HIP_CHECK(hipGetLastError());
+    // every instance wrote its outputs when it left the active list (k_accept -> retire)
+    NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));
+    if (res.hcnt[1] != 0 || res.hcnt[0] != capacity) {
+        set_error("nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)");
+        return NLOT_ERR_INVALID;
+    }
     return NLOT_OK;
 }
 
@@ -4676,6 +4803,9 @@ extern "C" size_t nlot_solve_workspace_size(const NlotProblem* p, int64_t B) {
     nlot::Dims d = nlot::make_dims(*p);
     return nlot::ws_bytes(d, B, p->sdf_kind == NLOT_SDF_MLP);
 }
+extern "C" size_t nlot_solve_workspace_size_slots(const NlotProblem* p, int64_t B, int32_t max_active) {
+    return nlot_solve_workspace_size(p, max_active > 0 && max_active < B ? (int64_t)max_active : B);
+}
 
 extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlp* mlp,
                                     const double* x0, const double* xg, const double* Xinit, double* X, double* U,
@@ -4688,7 +4818,7 @@ extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOption
         set_error("nlot_solve_batch: null pointer");
         return NLOT_ERR_INVALID;
     }
-    if (wbytes < nlot_solve_workspace_size(p, B)) {
+    if (wbytes < nlot_solve_workspace_size_slots(p, B, o->max_active)) {
         set_error("nlot_solve_batch: workspace too small");
         return NLOT_ERR_WORKSPACE;
     }

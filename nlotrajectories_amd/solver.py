@@ -50,7 +50,7 @@ def solve_batch(problem: Problem, x0, xg, mlp: Optional[DeviceMlp] = None, optio
     cost = torch.empty(B, **f64)
     status = torch.empty(B, dtype=torch.int32, device=device)
     iters = torch.empty(B, dtype=torch.int32, device=device)
-    nbytes = lib().nlot_solve_workspace_size(C.byref(pc), B)
+    nbytes = lib().nlot_solve_workspace_size_slots(C.byref(pc), B, int(opt.max_active))
     if workspace is None or workspace.numel() < nbytes:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=device)
     check(lib().nlot_solve_batch(C.byref(pc), C.byref(opt), mlp.handle if mlp is not None else None, _ptr(x0),
@@ -59,8 +59,9 @@ def solve_batch(problem: Problem, x0, xg, mlp: Optional[DeviceMlp] = None, optio
     return dict(X=X, U=U, S=S, cost=cost, status=status, iters=iters)
 
 
-def workspace_bytes(problem: Problem, B: int) -> int:
-    return int(lib().nlot_solve_workspace_size(C.byref(problem.to_c()), B))
+def workspace_bytes(problem: Problem, B: int, slots: int = 0) -> int:
+    """Workspace bytes for B instances through `slots` concurrent slots (0: all B at once)."""
+    return int(lib().nlot_solve_workspace_size_slots(C.byref(problem.to_c()), B, slots))
 
 
 def set_timing(enabled: bool):

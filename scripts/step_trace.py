@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 STEP_COLS = ["step", "active", "evals", "trials", "unused", "reused", "solves", "resto", "soc", "resto_solves",
-             "next_active"]
+             "next_active", "att_sum", "att_max", "att_multi"]
 KERNELS = [("mlp_full", "mlp_bf16<128, true>"), ("mlp_value", "mlp_bf16<128, false>"),
            ("iter_a", "k_iter_a<"), ("ric", "k_ric<3, false, false>"), ("ric_soc", "k_ric<3, false, true>"),
            ("ric_resto", "k_ric<3, true"), ("iter_b", "k_iter_b<"), ("accept", "k_accept<"),
@@ -105,7 +105,7 @@ def report(outdir):
     edges = [0, 256, 1024, 4096, 8192, 16384, 24576, 32768, 65536, 1 << 30]
     print(f"{len(act)} steps; Newton solves {cols['solves'].sum()}, corrections {cols['soc'].sum()}, "
           f"trial slots {cols['trials'].sum()}, restoration solves {cols['resto_solves'].sum()}")
-    hdr = "active<=  steps  mean_act  solves/step  soc/step  trials/step  steps/iter"
+    hdr = "active<=  steps  mean_act  solves/step  soc/step  trials/step  steps/iter  att/solve  att_max  multi/step"
     if Kz is not None:
         names = list(Kz["names"])
         hdr += "  wall_ms/step " + " ".join(f"{n[:9]:>9}" for n in names if n not in ("copy", "fill", "admit", "points"))
@@ -115,7 +115,9 @@ def report(outdir):
         if not m.any():
             continue
         line = (f"{hi:8d} {m.sum():6d} {act[m].mean():9.0f} {cols['solves'][m].mean():12.0f} {cols['soc'][m].mean():9.0f}"
-                f" {cols['trials'][m].mean():12.0f} {act[m].sum() / max(cols['solves'][m].sum(), 1):10.2f}")
+                f" {cols['trials'][m].mean():12.0f} {act[m].sum() / max(cols['solves'][m].sum(), 1):10.2f}"
+                f" {cols['att_sum'][m].sum() / max(cols['solves'][m].sum(), 1):10.3f} {cols['att_max'][m].mean():8.2f}"
+                f" {cols['att_multi'][m].mean():10.0f}")
         if Kz is not None:
             K, wall = Kz["K"], Kz["wall"]
             line += f"  {wall[m].mean() / 1e6:12.3f} " + " ".join(
