@@ -83,6 +83,9 @@ struct MlpReuse {
     const uint32_t* tmask;
     int64_t plane;
     int* nreused;  // if set: += the number of points whose forward was reused (statistics)
+    // if set (ld == 0, mlp_bf16 only): the launch covers ranks [*base, cnt) instead of [0, cnt) (the solver splits a
+    // step's value launch in two: the candidates known at the start of the step, then those k_iter_b adds)
+    const int* base;
 };
 
 // Launch the MFMA SDF-MLP kernel on cnt * P_per points, cnt = *n_dev if n_dev else n (n = upper bound

@@ -456,6 +456,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
 
     const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
     const int64_t npts = cnt * P_per;
+    const int64_t g0 = (ru.base && ld == 0) ? (int64_t)(*ru.base) * P_per : 0;  // first point of the launch
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int il = lane & 31, hl = lane >> 5;
     const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     };
     const bool reuse_on = FULL && ru.src && ld == 0;
     auto load_in = [&](int64_t tile, TileIn& a) {
-        const int64_t gi = tile * TP + wave * 32 + il;
+        const int64_t gi = g0 + tile * TP + wave * 32 + il;
         a.px = a.py = 0.f;
         a.src = -1;
         if (gi < npts) {
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
         r.tx = r.ty = r.tv = 0.f;
         r.m0 = r.m1 = 0u;
         if (reuse_on && a.src >= 0) {
-            const int64_t gi = tile * TP + wave * 32 + il;
+            const int64_t gi = g0 + tile * TP + wave * 32 + il;
             const int64_t q = (int64_t)a.src * P_per + (gi - (gi / P_per) * P_per);
             r.tx = ru.tpts[2 * q];
             r.ty = ru.tpts[2 * q + 1];
@@ -504,12 +505,12 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     load_in(blockIdx.x, in0);
     load_reuse(blockIdx.x, in0, re0);
     load_in(blockIdx.x + G, in1);
-    for (int64_t tile = blockIdx.x; tile * TP < npts; tile += G) {
+    for (int64_t tile = blockIdx.x; g0 + tile * TP < npts; tile += G) {
         TileIn in2;
         ReuseIn re1;
         load_in(tile + 2 * G, in2);
         load_reuse(tile + G, in1, re1);
-        const int64_t gi = tile * TP + wave * 32 + il;
+        const int64_t gi = g0 + tile * TP + wave * 32 + il;
         const bool valid = gi < npts;
         const int64_t pi = valid ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
         const float px = in0.px, py = in0.py;

@@ -45,6 +45,8 @@ namespace nlot {
 // evaluation, then MinC_1NrmRestorationPhase's initialisation); while SC_RESTO = 1 the EVAL / LS phases belong to
 // the restoration problem (k_resto_a / k_ric<DYN, true> / k_resto_b / k_resto_ls).
 enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4, PH_SOFT1 = 5, PH_SOFT2 = 6, PH_RINIT = 7 };
+// k_iter_a's passes (run() launches SOC on the side stream at the start of a step and EVAL after the full MLP launch)
+enum IterPass { PASS_ALL = 0, PASS_INIT = 1, PASS_SOC = 2, PASS_EVAL = 3 };
 
 // Minimum waves per SIMD the per-instance kernels are compiled for (register budget 512 / w per lane),
 // and the depth of k_ric's stage ring (its LDS per wavefront sets k_ric's occupancy).  These kernels wait
@@ -61,6 +63,9 @@ enum Phase { PH_INIT = 0, PH_EVAL = 1, PH_LS = 2, PH_DONE = 3, PH_SOC = 4, PH_SO
 #endif
 #ifndef NLOT_WPE_RIC
 #define NLOT_WPE_RIC 2  // k_ric at 2 waves/SIMD: 12 % less k_ric time at the metric config than 1 (r02i A/B)
+#endif
+#ifndef NLOT_WPE_SOC
+#define NLOT_WPE_SOC 2  // the correction (substitution) instantiation of k_ric
 #endif
 #ifndef NLOT_RIC_RING
 #define NLOT_RIC_RING 2
@@ -982,7 +987,7 @@ __device__ __forceinline__ void ric_sync_reads() {
 // waves per SIMD of k_ric: NLOT_WPE_RIC, except ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
 template <int DYN, bool SOC = false>
 struct RicWpe {
-    static constexpr int value = SOC ? 2 : DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
+    static constexpr int value = SOC ? NLOT_WPE_SOC : DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
 };
 // RESTO = true: the restoration problem's Newton solve (instances with SC_RESTO = 1, list ws.actr): every
 // equality row is soft (p, n eliminated, oracle soft_transform): before stage k uses the value function of
@@ -1016,7 +1021,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     if ((int)SC(SC_RIC) != 1) return;
     if ((SC(SC_RESTO) != 0.0) != RESTO) return;
     if (!RESTO && (SC(SC_RICFIX) >= 0.0) != SOC) return;
-    if (mode == MODE_LSQ && SC(SC_RETRY) >= 0.0) return;  // a deferred Newton solve, not an INIT instance
+    // least squares: the INIT instances only (phase read, not SC_RIC: the side stream's corrections set theirs concurrently)
+    if (mode == MODE_LSQ && (int)SC(SC_PHASE) != PH_INIT) return;
     typename R::Sh& sh = shg[grp];
     const int N = dm.N, nc = dm.nc, ns = dm.ns;
     const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
@@ -2309,13 +2315,15 @@ __device__ int ls_failed(const NlotSolverOptions& o, const NlotProblem& p, const
 }
 
 // k_iter_a: evaluation, optimality test, barrier update, then the stage matrices of the Newton system
-// (k_ric solves it).  init_pass = 1 (first step only): slack push and the least-squares multiplier
-// system of the instances in INIT; init_pass = 0: everything else (INIT instances first take their
+// (k_ric solves it).  pass (IterPass): INIT = slack push and the least-squares multiplier system of the instances in
+// INIT (their first step); SOC = the second-order corrections' stages only (side stream, at the start of the step: they
+// need no MLP evaluation); EVAL = everything but the corrections; ALL = both.  (INIT instances first take their
 // least-squares multipliers from k_ric's solve).
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
-                                               const double* __restrict__ xg, int init_pass, int* cnt, int* cnt_next) {
+                                               const double* __restrict__ xg, int pass, int* cnt, int* cnt_next) {
+    const bool init_pass = pass == PASS_INIT;
     if ((int)blockIdx.x >= cnt[2]) return;  // grid sized by a stale (larger) host count: steps run ahead of the host
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -2327,10 +2335,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     const int ph = (int)SC(SC_PHASE);
     if (ph != PH_INIT && ph != PH_EVAL && ph != PH_SOC && ph != PH_SOFT2) return;
     if (ph == PH_EVAL && SC(SC_RETRY) >= 0.0) {  // k_ric's inertia correction continues (attempt cap): stages kept
-        if (lane == 0 && !init_pass) ws.ricl[atomicAdd(&cnt[4], 1)] = b;
+        if (lane == 0 && (pass == PASS_ALL || pass == PASS_EVAL)) ws.ricl[atomicAdd(&cnt[4], 1)] = b;
         return;
     }
     if (init_pass && ph != PH_INIT) return;
+    if ((pass == PASS_SOC) != (ph == PH_SOC) && pass != PASS_ALL && !init_pass) return;
     double* SL = &AT(stg, 0);
     if (ph == PH_SOC) {
         // second-order correction: the same Newton matrix (the iteration's delta_w, no inertia loop) with the
@@ -4497,16 +4506,17 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     struct Res {
         int* hcnt = nullptr;
         hipEvent_t ev[KPIPE][8] = {};
-        hipStream_t s2 = nullptr, s3 = nullptr;                     // side streams: SOC / restoration solves
-        hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr;  // fork after k_iter_a, joins
+        hipStream_t s2 = nullptr, s3 = nullptr, s4 = nullptr;       // side streams: SOC / restoration / early values
+        hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr, e_s = nullptr, e_v0 = nullptr, e_v1 = nullptr;
         ~Res() {
             for (auto& r : ev)
                 for (auto& e : r)
                     if (e) (void)hipEventDestroy(e);
-            for (hipEvent_t e : {e_a, e_soc, e_r})
+            for (hipEvent_t e : {e_a, e_soc, e_r, e_s, e_v0, e_v1})
                 if (e) (void)hipEventDestroy(e);
             if (s2) (void)hipStreamDestroy(s2);
             if (s3) (void)hipStreamDestroy(s3);
+            if (s4) (void)hipStreamDestroy(s4);
             if (hcnt) (void)hipHostFree(hcnt);
         }
     } res;
@@ -4520,7 +4530,14 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_a, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_soc, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_r, hipEventDisableTiming));
-    hipStream_t s2 = res.s2, s3 = res.s3;
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_s, hipEventDisableTiming));
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_v0, hipEventDisableTiming));
+    NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_v1, hipEventDisableTiming));
+    NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s4, hipStreamNonBlocking));
+    hipStream_t s2 = res.s2, s3 = res.s3, s4 = res.s4;
+    int soc_fork = 0, early_value = 0;  // A/B knobs of the step's stream layout (NLOT_SOC_FORK, NLOT_EARLY_VALUE)
+    if (const char* e = getenv("NLOT_SOC_FORK")) soc_fork = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("NLOT_EARLY_VALUE")) early_value = atoi(e) != 0;
     if (g_timing)
         for (int k = 0; k < KPIPE; ++k)
             for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
@@ -4652,6 +4669,33 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         int* C = ws.cnt + CSET * q;
         int* Cn = ws.cnt + CSET * (q ^ 1);
         NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, CSET * sizeof(int), st));
+        // the second-order corrections' chain (k_iter_a's SOC pass: their stages; k_ric<DYN, false, true>: the
+        // substitutions) needs no MLP evaluation: it forks to the side stream at the start of the step (soc_fork 1),
+        // after the full MLP launch (2), or after the one k_iter_a launch that also does the evaluations (0)
+        auto soc_chain = [&](bool with_pass) {
+            NLOT_HIP_CHECK(hipEventRecord(res.e_s, st));
+            NLOT_HIP_CHECK(hipStreamWaitEvent(s2, res.e_s, 0));
+            if (with_pass)
+                hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, s2, dP, dD, o, dW, act, ws.x0s, ws.xgs,
+                                   (int)PASS_SOC, C, Cn);
+            hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64),
+                               0, s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
+            NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
+            return NLOT_OK;
+        };
+        if (soc_fork == 1) NLOT_HIP_CHECK((hipError_t)(soc_chain(true) == NLOT_OK ? hipSuccess : hipErrorUnknown));
+        // the value launch's first part: the candidates the previous step's k_accept / k_resto_ls listed (ranks
+        // [0, C[14]), C[14] = C[1] now) evaluate on a side stream while this step's evaluations and Newton solves run;
+        // the second part (after k_iter_b) covers the candidates added since (ranks [C[14], C[1]))
+        if (use_mlp && early_value) {
+            NLOT_HIP_CHECK(hipMemcpyAsync(C + 14, C + 1, sizeof(int), hipMemcpyDeviceToDevice, st));
+            NLOT_HIP_CHECK(hipEventRecord(res.e_v0, st));
+            NLOT_HIP_CHECK(hipStreamWaitEvent(s4, res.e_v0, 0));
+            rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 14, (int)P, 0, nullptr,
+                                    mo_t[q], false, s4);
+            if (rc) break;
+            NLOT_HIP_CHECK(hipEventRecord(res.e_v1, s4));
+        }
         // speculative backtracking only while the GPU is latency-bound (few active instances); in the
         // throughput-bound bulk it would multiply the value-MLP work for the same accepted steps
         const int nspec = n_active > spec_threshold ? spec_bulk : NSPEC;
@@ -4665,9 +4709,11 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             if (rc) break;
             if (ev[0]) (void)hipEventRecord(ev[1], st);
         }
+        if (soc_fork == 2) NLOT_HIP_CHECK((hipError_t)(soc_chain(true) == NLOT_OK ? hipSuccess : hipErrorUnknown));
         if (ev[4]) (void)hipEventRecord(ev[4], st);
         if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
-            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs, 1, C, Cn);
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
+                               (int)PASS_INIT, C, Cn);
             hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
                                st, dP, dD, dW, act, n_active, C + 2, (int)MODE_LSQ, nullptr, 1 << 30);
         }
@@ -4676,15 +4722,13 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         const int n_resto = std::min(n_active, resto_bound);
         if (n_resto > 0)
             hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C);
-        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs, 0, C, Cn);
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
+                           (int)(soc_fork == 0 ? PASS_ALL : PASS_EVAL), C, Cn);
+        if (soc_fork == 0) NLOT_HIP_CHECK((hipError_t)(soc_chain(false) == NLOT_OK ? hipSuccess : hipErrorUnknown));
         // the Newton solves and the corrections run over the compacted lists k_iter_a wrote (ws.ricl / ws.socl,
         // counts C[4] / C[6]; the grids are host bounds, blocks past the count exit): one group per instance that
         // has work, so a launch holds as many wavefronts as it has solves / 4
         NLOT_HIP_CHECK(hipEventRecord(res.e_a, st));
-        NLOT_HIP_CHECK(hipStreamWaitEvent(s2, res.e_a, 0));
-        hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
-                           s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
-        NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
         if (n_resto > 0) {  // the restoration chain on a stream of its own (disjoint instances)
             NLOT_HIP_CHECK(hipStreamWaitEvent(s3, res.e_a, 0));
             hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s3,
@@ -4705,8 +4749,11 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         if (ev[4]) (void)hipEventRecord(ev[5], st);
         if (use_mlp) {
             if (ev[0]) (void)hipEventRecord(ev[2], st);
+            MlpReuse vb{};
+            vb.base = C + 14;
+            if (early_value) NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_v1, 0));
             rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
-                                    mo_t[q], false, st);
+                                    mo_t[q], false, st, early_value ? &vb : nullptr);
             if (rc) break;
             if (ev[0]) (void)hipEventRecord(ev[3], st);
         }

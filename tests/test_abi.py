@@ -56,3 +56,16 @@ def test_default_options_agree():
     d = _abi.default_options()
     for k, _ in o._fields_:
         assert getattr(o, k) == getattr(d, k), k
+
+
+def test_workspace_holds_the_slots_only():
+    """ABI v10: the solver's state is slot-indexed, so B instances streamed through S slots need the workspace of S
+    (plus nothing per instance: outputs go to the caller's arrays when an instance finishes)."""
+    from nlotrajectories_amd.problem import METRIC_PROBLEM
+    from nlotrajectories_amd.solver import workspace_bytes
+
+    full = workspace_bytes(METRIC_PROBLEM, 4096)
+    assert workspace_bytes(METRIC_PROBLEM, 4096, 0) == full
+    assert workspace_bytes(METRIC_PROBLEM, 4096, 4096) == full
+    assert workspace_bytes(METRIC_PROBLEM, 1 << 20, 4096) == full
+    assert workspace_bytes(METRIC_PROBLEM, 4096, 512) == workspace_bytes(METRIC_PROBLEM, 512) < full
