@@ -4573,7 +4573,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     if (const char* e = getenv("NLOT_SPEC_BULK")) spec_bulk = std::max(1, std::min(NSPEC, atoi(e)));
     // k_ric's inertia-correction attempts per launch while more than ric_tries_min instances are active (the rest of
     // an instance's delta_w sequence continues in the next step's launch)
-    int ric_tries = 2, ric_tries_min = 2048;
+    int ric_tries = 1, ric_tries_min = 2048;
     if (const char* e = getenv("NLOT_RIC_TRIES")) ric_tries = std::max(1, atoi(e));
     if (const char* e = getenv("NLOT_RIC_TRIES_MIN")) ric_tries_min = atoi(e);
     double progress_s = 0, t_prog = 0;
