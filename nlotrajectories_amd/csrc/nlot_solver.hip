@@ -186,7 +186,7 @@ __host__ __device__ constexpr int ldl_len(int n) { return n * n + n; }
     X_(wdd, it_len(N, nx, nu, M)) X_(rp, ne_len(N, nx, M)) X_(rn, ne_len(N, nx, M)) X_(rzp, ne_len(N, nx, M))     \
     X_(rzn, ne_len(N, nx, M)) X_(rdp, ne_len(N, nx, M)) X_(rdn, ne_len(N, nx, M)) X_(rdzp, ne_len(N, nx, M))      \
     X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)   \
-    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx)) X_(x0s, nx) X_(xgs, nx)
+    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx)) X_(x0s, nx) X_(xgs, nx) X_(phi, N * nx * (nx + 2))
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -696,7 +696,8 @@ struct Solver {
     __host__ __device__ static constexpr int qe_col(int c) { return c < NX ? c : NZ + (c - NX); }
 
     // Build every stage's matrices in parallel (lane = knot): [H | g] -> hg (HBM); [A B 0 | c], M -> slot.
-    // GONLY: hg's g columns only (second-order correction; the slot is rebuilt: the forward sweep overwrote it)
+    // GONLY: hg's g columns and the slot's c column only (second-order correction: A, B and M are the iteration's,
+    // which the forward sweep leaves in place)
     template <bool LDS, bool GONLY = false>
     __device__ static void build_stages(const NlotProblem& p, const Dims& dm, const Ws& ws, int b, int lane, int mode,
                                         double dw, double mu0, double mu1, int nr, double* SL, int stride = 64) {
@@ -704,6 +705,12 @@ struct Solver {
         for (int k = lane; k <= N; k += stride) {
             double* o = SL + (size_t)k * SLOT;
             stage<GONLY>(p, dm, ws, b, k, mode, dw, mu0, mu1, nr, &AT(hg, k * HG));
+            if constexpr (GONLY) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+                    o[sAB + i * NAB + NZ] = (k < N && mode == MODE_NEWTON) ? -AT(rcd, k * NX + i) : 0.0;
+                continue;
+            }
             double A[NX][NX], Bu[NX][NU];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -1789,11 +1796,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         return;
     }
 
-    // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots, in place: row i of
-    // [A B 0 | c] becomes [Phi_i | B_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r)
+    // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots: row i of stage k's phi block is
+    // [Phi_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r); the slot's [A B 0 | c] stays, so a
+    // second-order correction (same A, B, K: the same Phi) recomputes the offsets only, and k_iter_a rebuilds only c
     static_assert(NU + 1 == NV, "slack is the last control column");
+    constexpr int PR = NX + 2;  // phi row: Phi_i | off_0,i | off_1,i
     for (int k = l; k < N; k += G) {
         double* slot = SL + (size_t)k * SLOT;
+        double* ph = &AT(phi, (size_t)k * NX * PR);
         const double* GN = slot + sGN;
         double dv[2][NU], Kt[NU][NX];
 #pragma unroll
@@ -1811,7 +1821,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             for (int c = 0; c < NX; ++c) Kt[v][c] = GN[c * NV + v];
 #pragma unroll 1
         for (int i = 0; i < NX; ++i) {
-            double* r_ = slot + sAB + i * NAB;
+            const double* r_ = slot + sAB + i * NAB;
+            double* pr = ph + i * PR;
             double Bi[NU];
 #pragma unroll
             for (int v = 0; v < NU; ++v) Bi[v] = r_[NX + v];
@@ -1821,15 +1832,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 o0 += Bi[v] * dv[0][v];
                 o1 += Bi[v] * dv[1][v];
             }
+            if constexpr (!SOC) {
 #pragma unroll
-            for (int c = 0; c < NX; ++c) {
-                double t = r_[c];
+                for (int c = 0; c < NX; ++c) {
+                    double t = r_[c];
 #pragma unroll
-                for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][c];
-                r_[c] = t;
+                    for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][c];
+                    pr[c] = t;
+                }
             }
-            r_[NX + NU] = o0;
-            r_[NZ] = o1;
+            pr[NX] = o0;
+            pr[NX + 1] = o1;
         }
         if constexpr (RESTO) {  // soft dynamics rows: x_{k+1} = S K^-1 S^-1 (Phi x_k + off - D (p + G nu))
             const double* v1 = &AT(vf, (k + 1) * VF);
@@ -1851,15 +1864,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             ldl_factor<NX>(K, NX, perm, &nneg);  // positive definite: the backward sweep factorised it
 #pragma unroll 1
             for (int c = 0; c <= NX; ++c) {  // the NX columns of Phi, then the offset
-                const int cs = c < NX ? c : NX + NU;
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    const double y = slot[sAB + i * NAB + cs];
+                    const double y = ph[i * PR + c];
                     col[i] = (c < NX ? y : y - Dd[i] * w[i]) / Sd[i];
                 }
                 ldl_solve1<NX>(K, NX, perm, col);
 #pragma unroll
-                for (int i = 0; i < NX; ++i) slot[sAB + i * NAB + cs] = Sd[i] * col[i];
+                for (int i = 0; i < NX; ++i) ph[i * PR + c] = Sd[i] * col[i];
             }
         }
     }
@@ -1902,11 +1914,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         double row[NX + 2], rr_[FRING][NX + 2];
         auto load_row = [&](int k, double* rw) {
             if (k >= N) return;
-            const double* sl = SL + (size_t)k * SLOT + sAB + li * NAB;
+            const double* sl = &AT(phi, ((size_t)k * NX + li) * PR);
 #pragma unroll
-            for (int c = 0; c < NX; ++c) rw[c] = sl[c];
-            rw[NX] = sl[NX + NU];
-            rw[NX + 1] = sl[NZ];
+            for (int c = 0; c < NX + 2; ++c) rw[c] = sl[c];
         };
 #pragma unroll
         for (int r = 0; r < FRING; ++r) load_row(r, rr_[r]);
