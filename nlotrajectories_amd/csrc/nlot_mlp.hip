@@ -412,8 +412,13 @@ __device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int co
 // one weight image per CU, shared by NLOT_MLP_*_THREADS / 256 waves per SIMD: value-only launches 3 (162
 // VGPRs); FULL (value + reverse sweep) 1, with the whole 512-register file (at 2 per SIMD it spills
 // ~440 B/lane and ran 3 % slower in the solve, profiles/r01/variants_v14.log)
+// NLOT_MLP_VALUE_PG: 32-point groups per wave of the value-only kernel; with 2 every A fragment read from LDS feeds
+// two MFMAs (one per group), at 2 waves per SIMD (the accumulators of both groups: ~230 VGPRs)
+#ifndef NLOT_MLP_VALUE_PG
+#define NLOT_MLP_VALUE_PG 1  // 2 measured: value launch -2 % alone, solve +1 % (profiles/r03/steps/ab_value_pg.txt)
+#endif
 #ifndef NLOT_MLP_VALUE_THREADS
-#define NLOT_MLP_VALUE_THREADS 768
+#define NLOT_MLP_VALUE_THREADS (NLOT_MLP_VALUE_PG > 1 ? 512 : 768)
 #endif
 #ifndef NLOT_MLP_FULL_THREADS
 #define NLOT_MLP_FULL_THREADS 256
@@ -462,6 +467,111 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
     const float scale = w.scale;
     constexpr int TP = bf16_threads(FULL) / 2;  // points per block tile (32 per wave)
+    if constexpr (!FULL && NLOT_MLP_VALUE_PG > 1) {
+        // value-only launches, VPG groups of 32 points per wave: the same arithmetic per point as the loop below
+        // (input layer, split, the six products in the same k order, bias + ReLU + output layer), each A fragment
+        // read once for the VPG groups' MFMAs
+        constexpr int VPG = NLOT_MLP_VALUE_PG, TPV = TP * VPG;
+        const int64_t G = gridDim.x;
+        auto loadp = [&](int64_t tile, float* px, float* py) {
+#pragma unroll
+            for (int pg = 0; pg < VPG; ++pg) {
+                const int64_t gi = g0 + tile * TPV + (int64_t)wave * 32 * VPG + pg * 32 + il;
+                px[pg] = py[pg] = 0.f;
+                if (gi < npts) {
+                    const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
+                    px[pg] = pts[2 * pi];
+                    py[pg] = pts[2 * pi + 1];
+                }
+            }
+        };
+        float ax[VPG], ay[VPG], bx[VPG], by[VPG];
+        loadp(blockIdx.x, ax, ay);
+        loadp(blockIdx.x + G, bx, by);
+        for (int64_t tile = blockIdx.x; g0 + tile * TPV < npts; tile += G) {
+            float cx[VPG], cy[VPG];
+            loadp(tile + 2 * G, cx, cy);
+            bool valid[VPG];
+            int64_t pi[VPG];
+            bool any = false;
+#pragma unroll
+            for (int pg = 0; pg < VPG; ++pg) {
+                const int64_t gi = g0 + tile * TPV + (int64_t)wave * 32 * VPG + pg * 32 + il;
+                valid[pg] = gi < npts;
+                pi[pg] = valid[pg] ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
+                any = any || valid[pg];
+            }
+            if (__any(any)) {
+                f32x16 acc[VPG][NT];
+#pragma unroll
+                for (int pg = 0; pg < VPG; ++pg)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) acc[pg][t] = f32x16{};
+#pragma unroll 1
+                for (int s = 0; s < NKB; ++s) {
+                    bf16x8 bh[VPG], bm[VPG], bl[VPG];
+#pragma unroll
+                    for (int pg = 0; pg < VPG; ++pg)
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) {
+                            const int k = 16 * s + 8 * hl + jj;
+                            const float z = fmaf(ay[pg], sA1[k], ax[pg] * sA0[k]) + sb0[k];
+                            float h0;
+                            if (fourier) {
+                                h0 = __builtin_amdgcn_cosf(turns_fourier(z)) * scale;
+                            } else {
+                                h0 = z > 0.f ? z : 0.f;
+                            }
+                            __bf16 a, b, c;
+                            split3(h0, a, b, c);
+                            bh[pg][jj] = a;
+                            bm[pg][jj] = b;
+                            bl[pg][jj] = c;
+                        }
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        const __bf16* rowp = sWp + (size_t)(t * 32 + il) * RS + 16 * s + 8 * hl;
+                        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
+                        const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
+                        const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
+#pragma unroll
+                        for (int pg = 0; pg < VPG; ++pg) acc[pg][t] = mfma6(ah, am, al, bh[pg], bm[pg], bl[pg], acc[pg][t]);
+                    }
+                }
+#pragma unroll
+                for (int pg = 0; pg < VPG; ++pg) {
+                    float fpart = 0.f;
+                    uint64_t mk = 0;
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int j = t * 32 + acc_row(r, hl);
+                            const float v = acc[pg][t][r] + sb[j];
+                            const bool on = v > 0.f;
+                            fpart = fmaf(sw[j], on ? v : 0.f, fpart);
+                            mk |= (uint64_t)on << (t * 16 + r);
+                        }
+                    const float fw = fpart + __shfl_xor(fpart, 32) + w.b_out;
+                    if (valid[pg]) {
+                        if (hl == 0) out.val[pi[pg] * out.sv] = fw;
+                        if (out.mask) {
+                            out.mask[(2 * hl) * out.mask_plane + pi[pg]] = (uint32_t)mk;
+                            out.mask[(2 * hl + 1) * out.mask_plane + pi[pg]] = (uint32_t)(mk >> 32);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int pg = 0; pg < VPG; ++pg) {
+                ax[pg] = bx[pg];
+                ay[pg] = by[pg];
+                bx[pg] = cx[pg];
+                by[pg] = cy[pg];
+            }
+        }
+        return;
+    }
 
     // A block's tiles are tile0, tile0 + G, ...: each tile's inputs (point, the reuse source and, one tile later,
     // the source's trial point / value / ReLU pattern) are loaded ahead, so the dependent global round trips of a
