@@ -284,7 +284,8 @@ typedef struct NlotRrtOptions {
     double goal_sample_rate;   /* probability of sampling the goal (0.05) */
     uint64_t seed;             /* counter-based RNG seed (the reference draws from Python's global `random`) */
     int32_t max_iter;          /* tree extensions tried (1000) */
-    int32_t pad_;
+    int32_t first_instance;    /* index of instance 0 of this call in the caller's batch (the random stream is keyed by
+                                  it: a batch split into calls draws as one call; 0 otherwise) */
 } NlotRrtOptions;
 
 /* Bytes of device workspace nlot_rrt_init needs for B instances (tree, path and spline buffers). */

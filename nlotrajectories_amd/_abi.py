@@ -113,4 +113,4 @@ NO_RESTO = dict(resto=0, soft_resto_pderror_reduction_factor=0.0)
 class NlotRrtOptions(C.Structure):
     """include/nlot.h NlotRrtOptions (RRTInitializer arguments, trajectory_initialization.py:68-81)."""
     _fields_ = [("bounds", (C.c_double * 2) * 2), ("step_size", C.c_double), ("margin", C.c_double),
-                ("goal_sample_rate", C.c_double), ("seed", C.c_uint64), ("max_iter", C.c_int32), ("pad_", C.c_int32)]
+                ("goal_sample_rate", C.c_double), ("seed", C.c_uint64), ("max_iter", C.c_int32), ("first_instance", C.c_int32)]

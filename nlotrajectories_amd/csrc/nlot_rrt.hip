@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64) void k_rrt(const NlotProblem* __restrict__ pp, 
     const InstWs w = inst_ws(ws + (size_t)b * inst_ws_doubles(cap), cap);
     const double sx = x0[b * nx], sy = x0[b * nx + 1], gx = xg[b * nx], gy = xg[b * nx + 1];
     const double step = o.step_size;
-    const uint64_t key = mix64(o.seed ^ mix64((uint64_t)b));
+    const uint64_t key = mix64(o.seed ^ mix64((uint64_t)(b + o.first_instance)));
     if (lane == 0) {
         w.nx[0] = sx;
         w.ny[0] = sy;

@@ -19,8 +19,10 @@ from .problem import Problem
 
 
 
-_WS = {}  # device -> workspace reused across calls (25 (max_iter + 2) doubles per instance: 16 GB for benchmark 6's
-#            16,384 instances at max_iter 5000; allocated once, not inside every timed step)
+_WS = {}  # device -> workspace reused across calls (25 (max_iter + 2) doubles per instance, sized for one chunk)
+CHUNK = 4096  # instances per nlot_rrt_init call: the workspace is bounded by the chunk (4 GB for benchmark 6's
+#               max_iter 5000, 16 GB for all 16,384 instances at once); the draws are keyed by the global instance
+#               index (NlotRrtOptions.first_instance), so the result is the same as one call
 
 
 def _workspace(nbytes, device):
@@ -62,10 +64,13 @@ def rrt_initial_guess(problem: Problem, x0, xg, bounds, step_size=0.05, max_iter
         raise ValueError(f"x0/xg must be [B, {problem.nx}]")
     X = torch.empty(B, problem.N + 1, nx, dtype=torch.float64, device=device)
     ok = torch.empty(B, dtype=torch.int32, device=device)
-    nbytes = lib().nlot_rrt_workspace_size(C.byref(o), B)
+    nbytes = lib().nlot_rrt_workspace_size(C.byref(o), min(B, CHUNK))
     ws = _workspace(nbytes, device)
-    check(lib().nlot_rrt_init(C.byref(pc), C.byref(o), x0.data_ptr(), xg.data_ptr(), X.data_ptr(), ok.data_ptr(), B,
-                              ws.data_ptr(), nbytes, stream_ptr()), "nlot_rrt_init")
+    for c0 in range(0, B, CHUNK):
+        n = min(CHUNK, B - c0)
+        o.first_instance = c0
+        check(lib().nlot_rrt_init(C.byref(pc), C.byref(o), x0[c0].data_ptr(), xg[c0].data_ptr(), X[c0].data_ptr(),
+                                  ok[c0:].data_ptr(), n, ws.data_ptr(), nbytes, stream_ptr()), "nlot_rrt_init")
     return X, ok.bool()
 
 

@@ -5,6 +5,7 @@ import json
 import os
 
 import numpy as np
+import torch
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -77,6 +78,25 @@ def test_gpu_rrt_matches_oracle(fn):
         print(fn, b, "ok", okc, bool(okg[b]), "max |dX|", err, flush=True)
         assert bool(okg[b]) == okc
         assert err < 1e-9, (fn, b, err)
+
+
+@pytest.mark.gpu
+def test_gpu_rrt_chunked_equals_one_call(monkeypatch):
+    """rrt_initial_guess splits a batch into nlot_rrt_init calls of CHUNK instances (bounded workspace); the draws
+    are keyed by the global instance index (NlotRrtOptions.first_instance), so the result equals one call's."""
+    import nlotrajectories_amd.rrt as rrt
+
+    prob, x0, xg, kw = _case(CASES[0])
+    rng = np.random.default_rng(11)
+    B = 13
+    X0 = np.repeat(x0[None], B, 0)
+    X0[:, :2] += rng.uniform(-0.02, 0.02, (B, 2))
+    XG = np.repeat(xg[None], B, 0)
+    Xa, oka = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
+    monkeypatch.setattr(rrt, "CHUNK", 4)
+    rrt.release_workspace()
+    Xb, okb = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
+    assert torch.equal(Xa, Xb) and torch.equal(oka, okb)
 
 
 # ---- reference-pinned fixtures (tests/golden/make_rrt_golden.py: the REFERENCE's RRTInitializer driven like
