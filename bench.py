@@ -263,6 +263,12 @@ def main():
     ric_solves_per_launch = agg["ric_solves"] / n_r
     ric_bytes = ric_bytes_per_solve(prob)
     ric_achieved = ric_solves_per_launch * ric_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
+    # SURVEY.md §8d's algorithmic figure per problem-iteration: 2 * 4 * (nvar + ncon) bytes (read + write the
+    # primal-dual iterate; ~7 KB at N = 50)
+    nvar = (prob.N + 1) * prob.nx + prob.N * prob.nu + (prob.N + 1)
+    ncon = prob.nx + prob.N * prob.nx + prob.nx + (prob.N + 1) * (1 if prob.use_slack else len(prob.body))
+    alg_bytes = 2 * 4 * (nvar + ncon)
+    ric_alg = ric_solves_per_launch * alg_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     ric_traffic = None
     # PMC at bench size (B = 65536): scripts/pmc_r03.sh -> profiles/r03/pmc_traffic_r03m_B65536.json
     tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_r03m_B65536.json")
@@ -313,6 +319,9 @@ def main():
             "frac": ric_achieved / PEAK_HBM_GBS,
             "traffic": ric_traffic if not stress else None,
             "bytes_per_solve": ric_bytes,
+            "algorithmic": {"bytes_per_solve": alg_bytes, "achieved": ric_alg, "frac": ric_alg / PEAK_HBM_GBS,
+                            "note": "SURVEY.md §8d: 2 * 4 * (nvar + ncon) bytes per problem-iteration; achieved and frac "
+                                    "above use the design bytes of the stage layouts"},
             "solves_per_launch": ric_solves_per_launch,
             "avg_launch_ms": ric_avg_ms,
             "launches": agg["ric_launches"],
