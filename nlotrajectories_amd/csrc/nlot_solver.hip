@@ -4574,7 +4574,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     // speculation while one value launch stays below ~56 GFLOP of forward work: 8192 instances of the metric
     // (P = 204 corners x 33,536 FLOP; measured best of {512, 2048, 8192} x {1, 2} at B = 65536), 138 of the
     // stress config (P = 1028 x 394,752 FLOP)
-    int spec_threshold = 8192, spec_bulk = 1;
+    int spec_threshold = 8192, spec_bulk = 2;  // 2 step lengths per later round in the bulk: -1.5 % (r03 ab8)
     if (use_mlp) {
         const double H = mlp->dev.H, fwd = 2.0 * (2.0 * H + mlp->dev.n_hidden * H * H + H);
         spec_threshold = (int)std::max(1.0, std::min(1e9, 5.6e10 / (fwd * (double)P)));
