@@ -4515,7 +4515,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     // host-side resources released on every return path (NLOT_HIP_CHECK returns early)
     struct Res {
         int* hcnt = nullptr;
-        hipEvent_t ev[KPIPE][8] = {};
+        hipEvent_t ev[KPIPE][10] = {};  // [8], [9]: the early value launch (NLOT_EARLY_VALUE) on its stream
         hipStream_t s2 = nullptr, s3 = nullptr, s4 = nullptr;       // side streams: SOC / restoration / early values
         hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr, e_s = nullptr, e_v0 = nullptr, e_v1 = nullptr;
         ~Res() {
@@ -4550,7 +4550,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     if (const char* e = getenv("NLOT_EARLY_VALUE")) early_value = atoi(e) != 0;
     if (g_timing)
         for (int k = 0; k < KPIPE; ++k)
-            for (int i = 0; i < 8; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
+            for (int i = 0; i < 10; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
     MlpOut mo{}, mo_t[2] = {};
     MlpReuse reuse[2] = {};
     if (use_mlp) {
@@ -4652,6 +4652,11 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
                 (void)hipEventElapsedTime(&c, e[2], e[3]);
                 g_stats.mlp_full_ms += a;
                 g_stats.mlp_value_ms += c;
+                if (early_value) {
+                    float v0 = 0;
+                    (void)hipEventElapsedTime(&v0, e[8], e[9]);
+                    g_stats.mlp_value_ms += v0;
+                }
             }
             if (e[4]) {
                 float a = 0, r = 0;
@@ -4701,8 +4706,10 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             NLOT_HIP_CHECK(hipMemcpyAsync(C + 14, C + 1, sizeof(int), hipMemcpyDeviceToDevice, st));
             NLOT_HIP_CHECK(hipEventRecord(res.e_v0, st));
             NLOT_HIP_CHECK(hipStreamWaitEvent(s4, res.e_v0, 0));
+            if (ev[0]) (void)hipEventRecord(ev[8], s4);
             rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 14, (int)P, 0, nullptr,
                                     mo_t[q], false, s4);
+            if (ev[0]) (void)hipEventRecord(ev[9], s4);
             if (rc) break;
             NLOT_HIP_CHECK(hipEventRecord(res.e_v1, s4));
         }
