@@ -5,8 +5,8 @@ One step = one batch of B synthetic start/goal instances per GPU of the metric N
 benchmark_3's body/bounds/slack penalty, N = 50 knots, learned SDF = the reference artefact FourierMLP
 (2-128-128-1, scale 10), linear initial guess; B = 32,768 by default (so that `--steps 20 --warmup 5` fits
 600 s; `--batch 65536` measures ~7 % more).  By default (--continuous on) the K timed batches stream through the
-solver with B instances in flight (continuous batching, NlotSolverOptions.max_active; up to 8 batches, ~120 GB
-of workspace, per nlot_solve_batch call), so one batch's latency-bound tail overlaps the next batch's bulk; every
+solver in one nlot_solve_batch call with 65,536 instances in flight (continuous batching, NlotSolverOptions.max_active;
+slot-indexed state: 22.6 GB of workspace whatever the number of batches), so the latency-bound tail is paid once; every
 instance's result is the same as in a call of its own.  Instances are independent, so each rank solves its
 own seeded batches (weak scaling) and the solved trajectories are gathered to rank 0 over RCCL after every
 solve call (the only collective).
@@ -75,7 +75,7 @@ def parse():
                     help="CPU-baseline threads (default: the host's CPU share: min(affinity, cgroup cpu.max quota))")
     ap.add_argument("--continuous", choices=["on", "off"], default="on",
                     help="on (metric / stress): the timed steps' batches flow through the solver with --batch slots "
-                         "(continuous batching, NlotSolverOptions.max_active; up to 4 batches per solve call), so one "
+                         "(continuous batching, NlotSolverOptions.max_active; all of them in one solve call), so one "
                          "batch's latency-bound tail overlaps the next batch's bulk; off: one solve call per batch")
     ap.add_argument("--slots", type=int, default=None,
                     help="continuous batching: instances in flight (default 65536 metric, --batch otherwise; the "
