@@ -276,3 +276,31 @@ def test_continuous_batching_same_results(artefact, case):
     print(case, "statuses", np.bincount(ra["status"].cpu().numpy(), minlength=7).tolist())
     for k in ("status", "iters", "cost", "X", "U", "S"):
         assert torch.equal(ra[k], rc[k]), k
+
+
+@pytest.mark.parametrize("knobs", [
+    {"NLOT_RIC_TRIES": "1", "NLOT_RIC_TRIES_MIN": "0"},     # every wrong inertia continues in the next step
+    {"NLOT_SOC_FORK": "1"}, {"NLOT_SOC_FORK": "2"},          # correction chain forked at the step start / after the MLP
+    {"NLOT_EARLY_VALUE": "1"},                               # previous step's candidates on a fourth stream
+    {"NLOT_SPEC_THRESHOLD": "100000", "NLOT_SPEC_BULK": "4"},
+])
+def test_scheduling_knobs_same_results(artefact, knobs, monkeypatch):
+    """The solver's scheduling (attempt cap per launch, stream layout, speculation) changes when an instance's work
+    runs, never its arithmetic: statuses, iterations, costs and trajectories are bitwise those of the defaults."""
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import METRIC_PROBLEM
+    from nlotrajectories_amd.sampling import sample_start_goal
+    from nlotrajectories_amd.solver import solve_batch
+
+    mlp = DeviceMlp(artefact)
+    tm = artefact.torch_module()
+    sdf = lambda P: tm(torch.tensor(np.asarray(P), dtype=torch.float32)).detach().numpy()[:, 0]
+    x0, xg = sample_start_goal(METRIC_PROBLEM, 96, seed=5, sdf=sdf)
+    opt = _abi.gpu_options(max_iter=300, max_active=48)
+    ra = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rb = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)
+    for k in ("status", "iters", "cost", "X", "U", "S"):
+        assert torch.equal(ra[k], rb[k]), (knobs, k)
