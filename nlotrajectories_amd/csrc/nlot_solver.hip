@@ -2200,6 +2200,7 @@ __device__ void emit_points(const NlotProblem& p, const Dims& dm, const Ws& ws, 
 // first global step: the corners of every instance (phase INIT)
 static __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                                const Ws* __restrict__ ws_, const int* __restrict__ active, int* cnt) {
+    if ((int)blockIdx.x >= cnt[2]) return;  // the host's count may exceed the device's (k_admit shortfall)
     const Ws& ws = *ws_;
     const int b = active[blockIdx.x];
     if ((int)SC(SC_PHASE) != PH_INIT) return;
@@ -4530,7 +4531,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             if (hcnt) (void)hipHostFree(hcnt);
         }
     } res;
-    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, KPIPE * 2 * CSET * sizeof(int), hipHostMallocDefault));
+    // + 2: the free-slot count and k_admit's error flag, read at every synchronisation
+    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, (KPIPE * 2 * CSET + 2) * sizeof(int), hipHostMallocDefault));
     // The second-order corrections (substitution, short) and the restoration instances' Newton solves (a longer
     // sequential sweep, few instances) touch disjoint instances from the main Newton solve: they run on a side
     // stream, forked after k_iter_a, so their latency hides under k_ric's; k_iter_b joins the corrections, the
@@ -4787,7 +4789,13 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         cur ^= 1;
         init_step = false;
         if (kq != kpipe - 1) continue;
+        int* hflag = res.hcnt + KPIPE * 2 * CSET;
+        NLOT_HIP_CHECK(hipMemcpyAsync(hflag, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        if (hflag[1] != 0) {  // k_admit found fewer free slots than the host asked for: fail now, not at the end
+            set_error("nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)");
+            return NLOT_ERR_INVALID;
+        }
         // restoration lists of the window: the next launches' grid bound (their kernels read the exact count)
         int rmax = 0;
         for (int j = 0; j <= kq; ++j) rmax = std::max(rmax, res.hcnt[2 * CSET * j + CSET * (((step - kq + j) & 1) ^ 1) + 5]);

@@ -17,26 +17,9 @@ from . import _abi
 from ._lib import check, lib, require_gpu, stream_ptr
 from .problem import Problem
 
-
-
-_WS = {}  # device -> workspace reused across calls (25 (max_iter + 2) doubles per instance, sized for one chunk)
 CHUNK = 4096  # instances per nlot_rrt_init call: the workspace is bounded by the chunk (4 GB for benchmark 6's
 #               max_iter 5000, 16 GB for all 16,384 instances at once); the draws are keyed by the global instance
 #               index (NlotRrtOptions.first_instance), so the result is the same as one call
-
-
-def _workspace(nbytes, device):
-    key = str(torch.device(device))
-    ws = _WS.get(key)
-    if ws is None or ws.numel() < nbytes:
-        _WS.pop(key, None)
-        ws = _WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    return ws
-
-
-def release_workspace():
-    """Free the cached RRT workspace."""
-    _WS.clear()
 
 
 def rrt_options(bounds, step_size=0.05, max_iter=1000, margin=0.01, goal_sample_rate=0.05, seed=0):
@@ -65,7 +48,9 @@ def rrt_initial_guess(problem: Problem, x0, xg, bounds, step_size=0.05, max_iter
     X = torch.empty(B, problem.N + 1, nx, dtype=torch.float64, device=device)
     ok = torch.empty(B, dtype=torch.int32, device=device)
     nbytes = lib().nlot_rrt_workspace_size(C.byref(o), min(B, CHUNK))
-    ws = _workspace(nbytes, device)
+    # per call, on the caller's stream: two calls on different streams or threads never share a workspace (torch's
+    # caching allocator reuses the memory; 25 (max_iter + 2) doubles per instance of one chunk)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
     for c0 in range(0, B, CHUNK):
         n = min(CHUNK, B - c0)
         o.first_instance = c0

@@ -140,6 +140,7 @@ static jet jcompose2(double f, const double g[2], const double H[3] /*xx,xy,yy*/
 /* ============================================================================================ */
 /* out: [0]=f [1..2]=lam*grad [3..5]=lam*hess (xx,xy,yy).  lam scales the adjoint seed
  * (adj1 / jac_adj1, gen/nn_sdf.cpp:79-104); lam = 1 gives jac_nn_sdf.  want = 0: value only. */
+#define ORACLE_ACT_SOFTPLUS 90 /* not in the ABI: a diagnostic of the oracle (ReLU-kink experiment) */
 /* s, s', s'' of a smooth hidden activation (core/nn_architectures.py:47-52; SineLayer :8-26 with omega_0) */
 static void oracle_act3(int act, float omega, float z, float* s, float* d1, float* d2) {
     switch (act) {
@@ -149,6 +150,15 @@ static void oracle_act3(int act, float omega, float z, float* s, float* d1, floa
         case NLOT_ACT_SINE: {
             const float u = omega * z;
             *s = sinf(u); *d1 = omega * cosf(u); *d2 = -omega * omega * *s;
+            break;
+        }
+        case ORACLE_ACT_SOFTPLUS: { /* diagnostic only (scripts/ipopt_variants.py): ReLU smoothed, beta from env */
+            static float beta = 0.f;
+            if (beta == 0.f) beta = getenv("NLOT_ORACLE_SOFTPLUS_BETA") ? (float)atof(getenv("NLOT_ORACLE_SOFTPLUS_BETA")) : 100.f;
+            const float t = beta * z, e = expf(-fabsf(t)), sg = t >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+            *s = fmaxf(z, 0.f) + log1pf(e) / beta;
+            *d1 = sg;
+            *d2 = beta * sg * (1.f - sg);
             break;
         }
         default: *s = z > 0.f ? z : 0.f; *d1 = z > 0.f ? 1.f : 0.f; *d2 = 0.f;
@@ -703,7 +713,12 @@ static void ldl_solve(const double* a, int n, const int* perm, double* Bm, int m
 /* ============================================================================================ */
 /* Solver state                                                                                 */
 /* ============================================================================================ */
-#define FILT_MAX 64 /* same capacity as the GPU solver (csrc/nlot_solver.hip) */
+/* Filters (line search, adaptive-mu progress, restoration): IPOPT's Filter is an unbounded list from which
+ * dominated entries are removed (Filter::AddEntry).  At most one entry enters per iteration (plus one per
+ * restoration entry), so a capacity of 2 max_iter + 64 never overflows: the list is unbounded in effect.
+ * NLOT_ORACLE_FILT_CAP forces a smaller capacity that forgets the oldest entry (round-3 behaviour, kept only
+ * to measure that variant). */
+#define FILT_MIN 64
 #define XMAX 8
 #define VMAX 5
 #define ZMAX (XMAX + VMAX)
@@ -740,12 +755,13 @@ typedef struct {
     double *dzl, *dzu, *dzs, *dvt;
     /* scalars */
     double mu, tau, dw_last, theta_max, theta_min;
-    int nfilt;
-    double filt_theta[FILT_MAX], filt_phi[FILT_MAX];
+    int nfilt, fcap;
+    int filt_ovf, afilt_ovf, max_nfilt, max_nafilt; /* overflows (forgotten entries) and peak sizes: diagnostics */
+    double *filt_theta, *filt_phi;
     /* adaptive mu (IpAdaptiveMuUpdate): free/fixed mode, mu_max and the obj-constr progress filter */
     int free_mode, nafilt;
     double mu_dc; /* mu for delta_c (the iterate's mu; the affine solve uses mu = 0 in the RHS) */
-    double mu_max, af_f[FILT_MAX], af_th[FILT_MAX];
+    double mu_max, *af_f, *af_th;
     double lin_resid; /* debug: max residual of the linear KKT system */
     double dc_used;   /* delta_c applied to the terminal block in the last solve */
     /* ---- feasibility restoration problem (IPOPT MinC_1NrmRestorationPhase), active when resto = 1:
@@ -803,7 +819,9 @@ static int sol_alloc(Sol* s) {
     TAKE(XR, (N + 1) * nx) TAKE(UR, N * nu) TAKE(SR, N + 1) TAKE(DRX, (N + 1) * nx) TAKE(DRU, N * nu)           \
     TAKE(DRS, N + 1) TAKE(rp, NE) TAKE(rn, NE) TAKE(rzp, NE) TAKE(rzn, NE) TAKE(rdp, NE) TAKE(rdn, NE)          \
     TAKE(rdzp, NE) TAKE(rdzn, NE) TAKE(Dsoft, NE) TAKE(esoft, NE) TAKE(sb, NB) TAKE(yb, NB) TAKE(zbl, NB)           \
-    TAKE(zbu, NB) TAKE(rcb, NB) TAKE(dsb, NB) TAKE(yb_n, NB) TAKE(dzbl, NB) TAKE(dzbu, NB)
+    TAKE(zbu, NB) TAKE(rcb, NB) TAKE(dsb, NB) TAKE(yb_n, NB) TAKE(dzbl, NB) TAKE(dzbu, NB)                  \
+    TAKE(filt_theta, FC) TAKE(filt_phi, FC) TAKE(af_f, FC) TAKE(af_th, FC)
+    const int FC = s->fcap;
     const int NB = N * nu + N + 1;
     const int NE = nx + N * nx + CMAX + (N + 1) * M + NB;
     ALLOCS
@@ -1864,14 +1882,16 @@ static void filter_add(Sol* s, double theta, double phi) {
             ++w;
         }
     s->nfilt = w;
-    if (s->nfilt == FILT_MAX) { /* capacity: forget the oldest entry */
-        memmove(s->filt_theta, s->filt_theta + 1, sizeof(double) * (FILT_MAX - 1));
-        memmove(s->filt_phi, s->filt_phi + 1, sizeof(double) * (FILT_MAX - 1));
+    if (s->nfilt == s->fcap) { /* only under NLOT_ORACLE_FILT_CAP: forget the oldest entry */
+        memmove(s->filt_theta, s->filt_theta + 1, sizeof(double) * (s->fcap - 1));
+        memmove(s->filt_phi, s->filt_phi + 1, sizeof(double) * (s->fcap - 1));
         s->nfilt--;
+        s->filt_ovf++;
     }
     s->filt_theta[s->nfilt] = nt;
     s->filt_phi[s->nfilt] = np;
     s->nfilt++;
+    if (s->nfilt > s->max_nfilt) s->max_nfilt = s->nfilt;
 }
 static int filter_ok(const Sol* s, double theta, double phi) {
     for (int i = 0; i < s->nfilt; ++i)
@@ -2010,14 +2030,16 @@ static void afilt_add(Sol* s, double f, double th) {
             ++w;
         }
     s->nafilt = w;
-    if (s->nafilt == FILT_MAX) { /* capacity: forget the oldest entry */
-        memmove(s->af_f, s->af_f + 1, sizeof(double) * (FILT_MAX - 1));
-        memmove(s->af_th, s->af_th + 1, sizeof(double) * (FILT_MAX - 1));
+    if (s->nafilt == s->fcap) { /* only under NLOT_ORACLE_FILT_CAP: forget the oldest entry */
+        memmove(s->af_f, s->af_f + 1, sizeof(double) * (s->fcap - 1));
+        memmove(s->af_th, s->af_th + 1, sizeof(double) * (s->fcap - 1));
         s->nafilt--;
+        s->afilt_ovf++;
     }
     s->af_f[s->nafilt] = nf;
     s->af_th[s->nafilt] = nt;
     s->nafilt++;
+    if (s->nafilt > s->max_nafilt) s->max_nafilt = s->nafilt;
 }
 
 /* step = aff + sigma * cen over every step array (layout of step_save) */
@@ -2412,6 +2434,9 @@ static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, 
     s->gcb = o->general_bounds ? 1 : 0;
     s->nb = s->gcb ? s->N * s->nu + s->ns * (s->N + 1) : 0;
     s->ne = s->nx + s->N * s->nx + s->nc + (s->N + 1) * s->M + s->nb;
+    s->fcap = 2 * (o->max_iter > 0 ? o->max_iter : 0) + FILT_MIN;
+    const char* fc = getenv("NLOT_ORACLE_FILT_CAP");
+    if (fc && atoi(fc) > 0 && atoi(fc) < s->fcap) s->fcap = atoi(fc);
 }
 
 /* IPOPT MinC_1NrmRestorationPhase (Waechter & Biegler 2006 §3.3, IPOPT's documented defaults), run on the
@@ -2651,7 +2676,9 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
 /* info[0] = final objective, [1] = max dual inf, [2] = constr viol, [3] = max linear-KKT residual
  * seen, [4] = final mu, [5] = E_0 (scaled overall error), [6] = restoration phases, [7] = watchdog /
  * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny),
- * [8] = theta (1-norm) at the last line-search failure, -1 if none.  info holds >= 9 doubles. */
+ * [8] = theta (1-norm) at the last line-search failure, -1 if none, [9] / [10] = peak size of the line-search
+ * (incl. restoration) / adaptive-mu filter, [11] / [12] = their forgotten entries (NLOT_ORACLE_FILT_CAP only).
+ * info holds >= 16 doubles. */
 /* oracle_solve_one with an initial guess for the controls and slacks too (Uinit / Sinit, NULL = the reference's
  * U = S = 0), pushed into their bounds as IPOPT pushes a starting point; test infrastructure (warm starts from a
  * returned solution: is it a local optimum of the same NLP). */
@@ -2762,10 +2789,15 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
     double theta_fail = -1.0; /* theta of the last iterate whose line search failed (diagnostic) */
     LsRef wd_ref = {0, 0, 0, 0, 1};
     double wd_amax = 1, wd_az = 1, wd_amin = 0, wd_mu = 0, wd_tau = 0;
+    FILE* dump = getenv("NLOT_ORACLE_DUMP") ? fopen(getenv("NLOT_ORACLE_DUMP"), "wb") : NULL; /* diagnostics */
     for (;;) {
         eval_full(s);
         errors(s, &e);
         double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
+        if (dump) { /* iterate X and the knot multipliers yd, one record per iteration */
+            fwrite(s->X, sizeof(double), (size_t)(N + 1) * nx, dump);
+            fwrite(s->yd, sizeof(double), (size_t)(N + 1) * M, dump);
+        }
         if (info) info[5] = E0;
         if (!isfinite(E0)) {
             status = NLOT_NUMERIC;
@@ -3068,6 +3100,7 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         tiny_last = is_tiny;
         ++iter;
     }
+    if (dump) fclose(dump);
     free(tb);
     free(wd_it);
     free(qf_aff);
@@ -3085,6 +3118,11 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         info[6] = n_resto;
         info[7] = 1e6 * n_wd + 1e4 * n_soft + 1e2 * (s->n_soc_tried > 99 ? 99 : s->n_soc_tried) + n_tiny;
         info[8] = theta_fail;
+        const int mr = r_alloc ? r->max_nfilt : 0;
+        info[9] = s->max_nfilt > mr ? s->max_nfilt : mr;
+        info[10] = s->max_nafilt;
+        info[11] = s->filt_ovf + (r_alloc ? r->filt_ovf : 0);
+        info[12] = s->afilt_ovf;
     }
     if (r_alloc) free(r->arena);
     free(s->arena);

@@ -146,7 +146,7 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init
     S = np.zeros(N + 1)
     cost = np.zeros(1)
     it = (C.c_int * 1)()
-    info = np.zeros(9)
+    info = np.zeros(16)
     x0 = np.ascontiguousarray(x0, np.float64)
     xg = np.ascontiguousarray(xg, np.float64)
     Xi = None if X_init is None else np.ascontiguousarray(X_init, np.float64)
@@ -158,7 +158,8 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init
     return dict(status=st, X=X, U=U, S=S, cost=float(cost[0]), iters=int(it[0]), dual_inf=info[1],
                 constr_viol=info[2], lin_resid=info[3], mu=info[4], E0=info[5], resto_phases=int(info[6]),
                 watchdogs=ev // 1000000, soft_resto_steps=(ev // 10000) % 100, soc_tried=(ev // 100) % 100,
-                tiny_steps=ev % 100, theta_fail=float(info[8]))
+                tiny_steps=ev % 100, theta_fail=float(info[8]), max_filter=int(info[9]),
+                max_mu_filter=int(info[10]), filter_forgotten=int(info[11]), mu_filter_forgotten=int(info[12]))
 
 
 def solve_batch(problem, x0, xg, hm: HostMlp = None, opt=None, threads=0):

@@ -94,9 +94,33 @@ def test_gpu_rrt_chunked_equals_one_call(monkeypatch):
     XG = np.repeat(xg[None], B, 0)
     Xa, oka = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
     monkeypatch.setattr(rrt, "CHUNK", 4)
-    rrt.release_workspace()
     Xb, okb = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
     assert torch.equal(Xa, Xb) and torch.equal(oka, okb)
+
+
+@pytest.mark.gpu
+def test_gpu_rrt_concurrent_streams():
+    """Two rrt_initial_guess calls in flight on two streams (each call allocates its own workspace on its stream):
+    both results equal the sequential ones (a shared cached workspace let such calls corrupt each
+    other's trees)."""
+    import nlotrajectories_amd.rrt as rrt
+
+    prob, x0, xg, kw = _case(CASES[0])
+    rng = np.random.default_rng(12)
+    B = 64
+    X0 = np.repeat(x0[None], B, 0)
+    X0[:, :2] += rng.uniform(-0.02, 0.02, (B, 2))
+    XG = np.repeat(xg[None], B, 0)
+    Xa, oka = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
+    Xb, okb = rrt.rrt_initial_guess(prob, X0, XG, seed=6, **kw)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        Xc, okc = rrt.rrt_initial_guess(prob, X0, XG, seed=5, **kw)
+    with torch.cuda.stream(s2):
+        Xd, okd = rrt.rrt_initial_guess(prob, X0, XG, seed=6, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(Xa, Xc) and torch.equal(oka, okc)
+    assert torch.equal(Xb, Xd) and torch.equal(okb, okd)
 
 
 # ---- reference-pinned fixtures (tests/golden/make_rrt_golden.py: the REFERENCE's RRTInitializer driven like
