@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 10
+#define NLOT_ABI_VERSION 11
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -262,6 +262,9 @@ typedef struct NlotSolveStats {
     int64_t ric_solves;        /* instance Newton solves (factorisations) those launches performed */
     int64_t ric_soc_solves;    /* second-order corrections: substitutions with the stored factors (side stream) */
     int64_t ric_resto_solves;  /* restoration-phase Newton solves (side stream) */
+    int32_t filter_capacity;   /* entries per filter (line search, adaptive-mu progress, restoration); ABI v11 */
+    int32_t filter_peak;       /* the largest size any filter reached */
+    int64_t filter_forgotten;  /* entries forgotten at capacity (IPOPT's filter is unbounded: 0 = faithful) */
 } NlotSolveStats;
 /* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
 void nlot_set_timing(int32_t enabled);

@@ -74,7 +74,8 @@ class NlotSolveStats(C.Structure):
         ("iterate_ms", C.c_double), ("slots_in_lds", C.c_int32), ("pad_", C.c_int32),
         ("mlp_points_full_reused", C.c_int64), ("ric_ms", C.c_double), ("ric_launches", C.c_int32),
         ("pad2_", C.c_int32), ("ric_solves", C.c_int64), ("ric_soc_solves", C.c_int64),
-        ("ric_resto_solves", C.c_int64),
+        ("ric_resto_solves", C.c_int64), ("filter_capacity", C.c_int32), ("filter_peak", C.c_int32),
+        ("filter_forgotten", C.c_int64),
     ]
 
 

@@ -782,6 +782,11 @@ typedef struct {
      * free.  Bound row b: control b = k nu + i (umin_i <= sigma <= umax_i), then slack rows N nu + k (sigma >= 0);
      * zbl / zbu are sigma's bound multipliers, yb the row multiplier, rcb = U - sigma (or S - sigma). */
     int gcb, nb;
+    /* IPOPT bound_relax_factor (variant, NLOT_ORACLE_BOUND_RELAX = r): every bound relaxed by r max(1, |bound|)
+     * (TNLPAdapter); prel is the problem with the relaxed control bounds, brel the relaxation of the zero bounds
+     * of S and of the inequality slacks (the bound distances are S + brel and T = d(x) + brel). */
+    double brel;
+    NlotProblem prel;
     double *sb, *yb, *zbl, *zbu, *rcb, *dsb, *yb_n, *dzbl, *dzbu;
     double *arena;
 } Sol;
@@ -793,7 +798,7 @@ static int row_b(const Sol* s, int b) { return row_q(s, (s->N + 1) * s->M) + b; 
 static double bvar(const Sol* s, const double* U, const double* S, int b) {
     return b < s->N * s->nu ? U[b] : S[b - s->N * s->nu];
 }
-static double blo(const Sol* s, int b) { return b < s->N * s->nu ? s->p->umin[b % s->nu] : 0.0; }
+static double blo(const Sol* s, int b) { return b < s->N * s->nu ? s->p->umin[b % s->nu] : -s->brel; }
 static int bhi_on(const Sol* s, int b) { return b < s->N * s->nu; }
 static double bhi(const Sol* s, int b) { return b < s->N * s->nu ? s->p->umax[b % s->nu] : 0.0; }
 
@@ -890,7 +895,7 @@ static void residuals(const Sol* s, const double* X, const double* U, const doub
     for (int k = 0; k <= N; ++k) {
         jet d[NLOT_MAX_BODY];
         knot_ineq(p, s->m, X + k * nx, 0, d);
-        for (int j = 0; j < M; ++j) rcq[k * M + j] = d[j].v + (s->sd ? S[k] : 0.0) - T[k * M + j];
+        for (int j = 0; j < M; ++j) rcq[k * M + j] = d[j].v + (s->sd ? S[k] : 0.0) + s->brel - T[k * M + j];
     }
     if (rcb)
         for (int q = 0; q < s->nb; ++q) rcb[q] = bvar(s, U, S, q) - SB[q];
@@ -918,8 +923,8 @@ static void barrier_terms(const Sol* s, const double* U, const double* S, const 
             for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
         if (s->ns)
             for (int k = 0; k <= N; ++k) {
-                bar += log(S[k]);
-                lin += S[k];
+                bar += log(S[k] + s->brel);
+                lin += S[k] + s->brel;
             }
     }
     *bar_out = bar;
@@ -1054,7 +1059,7 @@ static void eval_full(Sol* s) {
         memset(Hd, 0, sizeof(double) * 9);
         for (int j = 0; j < M; ++j) {
             s->dv[k * M + j] = d[j].v + (s->sd ? s->S[k] : 0.0);
-            s->rcq[k * M + j] = s->dv[k * M + j] - s->T[k * M + j];
+            s->rcq[k * M + j] = s->dv[k * M + j] + s->brel - s->T[k * M + j];
             if (s->resto) s->rcq[k * M + j] += -s->rp[row_q(s, k * M + j)] + s->rn[row_q(s, k * M + j)];
             for (int a = 0; a < 3; ++a) s->Jd[(k * M + j) * 3 + a] = d[j].g[a];
             double w = s->yd[k * M + j];
@@ -1173,7 +1178,7 @@ static void errors(const Sol* s, Errs* e) {
                 COMPL(s->zu[k * nu + i], p->umax[i] - s->U[k * nu + i]);
             }
         if (s->ns)
-            for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k]);
+            for (int k = 0; k <= N; ++k) COMPL(s->zs[k], s->S[k] + s->brel);
     }
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < M; ++j) COMPL(s->vt[k * M + j], s->T[k * M + j]);
@@ -1320,8 +1325,8 @@ static void build(Sol* s, int mode, double dw) {
                     g[iu + i] += -mu / sl + mu / su;
                 }
             if (s->ns && !s->gcb) {
-                HH(is, is) += s->zs[k] / s->S[k];
-                g[is] += -mu / s->S[k] + kappa_d * mu;
+                HH(is, is) += s->zs[k] / (s->S[k] + s->brel);
+                g[is] += -mu / (s->S[k] + s->brel) + kappa_d * mu;
             }
             for (int i = 0; i < nzk; ++i) HH(i, i) += dw;
         } else {
@@ -1853,7 +1858,7 @@ static void recover(Sol* s, double dw) {
             s->dzu[q] = mu / su - s->zu[q] + (s->zu[q] / su) * du;
         }
     if (s->ns)
-        for (int k = 0; k <= N; ++k) s->dzs[k] = mu / s->S[k] - s->zs[k] - (s->zs[k] / s->S[k]) * s->dS[k];
+        for (int k = 0; k <= N; ++k) s->dzs[k] = mu / (s->S[k] + s->brel) - s->zs[k] - (s->zs[k] / (s->S[k] + s->brel)) * s->dS[k];
 }
 
 /* ============================================================================================ */
@@ -1937,7 +1942,7 @@ static double primal_frac(const Sol* s, double tau) {
             a = frac_to_bound(p->umax[i] - s->U[q], -s->dU[q], tau, a);
         }
     if (s->ns && !s->gcb)
-        for (int k = 0; k <= N; ++k) a = frac_to_bound(s->S[k], s->dS[k], tau, a);
+        for (int k = 0; k <= N; ++k) a = frac_to_bound(s->S[k] + s->brel, s->dS[k], tau, a);
     for (int q = 0; q < s->nb; ++q) {
         a = frac_to_bound(s->sb[q] - blo(s, q), s->dsb[q], tau, a);
         if (bhi_on(s, q)) a = frac_to_bound(bhi(s, q) - s->sb[q], -s->dsb[q], tau, a);
@@ -2064,7 +2069,11 @@ static double qf_eval(Sol* s, const QfCtx* q, double sigma) {
     const NlotProblem* p = s->p;
     int nu = s->nu, N = s->N, M = s->M;
     step_combine(s, q->aff, q->cen, sigma);
-    const double tau = fmax(0.99, 1.0 - sigma * q->avg);
+    /* tau inside q(sigma) is a reconstruction; NLOT_ORACLE_QF_TAU=curr uses the current iteration's
+     * tau instead (variant) */
+    static int tau_curr = -1;
+    if (tau_curr < 0) tau_curr = getenv("NLOT_ORACLE_QF_TAU") && !strcmp(getenv("NLOT_ORACLE_QF_TAU"), "curr");
+    const double tau = tau_curr ? s->tau : fmax(0.99, 1.0 - sigma * q->avg);
     const double ap = primal_frac(s, tau), ad = dual_frac(s, tau);
     double csq = 0;
 #define CQ(sl, dsl, z, dz)                                                                       \
@@ -2079,7 +2088,7 @@ static double qf_eval(Sol* s, const QfCtx* q, double sigma) {
             CQ(p->umax[i] - s->U[j], -s->dU[j], s->zu[j], s->dzu[j]);
         }
     if (s->ns && !s->gcb)
-        for (int k = 0; k <= N; ++k) CQ(s->S[k], s->dS[k], s->zs[k], s->dzs[k]);
+        for (int k = 0; k <= N; ++k) CQ(s->S[k] + s->brel, s->dS[k], s->zs[k], s->dzs[k]);
     for (int q = 0; q < s->nb; ++q) {
         CQ(s->sb[q] - blo(s, q), s->dsb[q], s->zbl[q], s->dzbl[q]);
         if (bhi_on(s, q)) CQ(bhi(s, q) - s->sb[q], -s->dsb[q], s->zbu[q], s->dzbu[q]);
@@ -2228,7 +2237,7 @@ static void accept_step(Sol* s, double al, double az, const Trial* t) {
             ZUPD(s->zu[q], s->dzu[q], p->umax[i] - s->U[q]);
         }
     if (s->ns && !s->gcb)
-        for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k]);
+        for (int k = 0; k <= N; ++k) ZUPD(s->zs[k], s->dzs[k], s->S[k] + s->brel);
     for (int q = 0; q < s->nb; ++q) {
         ZUPD(s->zbl[q], s->dzbl[q], s->sb[q] - blo(s, q));
         if (bhi_on(s, q)) ZUPD(s->zbu[q], s->dzbu[q], bhi(s, q) - s->sb[q]);
@@ -2258,7 +2267,7 @@ static double barrier_gd(const Sol* s) {
             gd += (s->gcb ? s->gU[q] : s->gU[q] - mu / (s->U[q] - p->umin[i]) + mu / (p->umax[i] - s->U[q])) * s->dU[q];
         }
     if (s->ns)
-        for (int k = 0; k <= N; ++k) gd += (s->gcb ? s->gS[k] : s->gS[k] - mu / s->S[k] + kappa_d * mu) * s->dS[k];
+        for (int k = 0; k <= N; ++k) gd += (s->gcb ? s->gS[k] : s->gS[k] - mu / (s->S[k] + s->brel) + kappa_d * mu) * s->dS[k];
     for (int q = 0; q < s->nb; ++q) {
         double Sig, bg;
         bound_sig(s, q, &Sig, &bg);
@@ -2435,6 +2444,17 @@ static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, 
     s->nb = s->gcb ? s->N * s->nu + s->ns * (s->N + 1) : 0;
     s->ne = s->nx + s->N * s->nx + s->nc + (s->N + 1) * s->M + s->nb;
     s->fcap = 2 * (o->max_iter > 0 ? o->max_iter : 0) + FILT_MIN;
+    const char* br = getenv("NLOT_ORACLE_BOUND_RELAX");
+    if (br && atof(br) > 0.0) {
+        const double r = atof(br);
+        s->prel = *p;
+        for (int i = 0; i < p->nu; ++i) {
+            s->prel.umin[i] -= r * fmax(1.0, fabs(p->umin[i]));
+            s->prel.umax[i] += r * fmax(1.0, fabs(p->umax[i]));
+        }
+        s->p = &s->prel;
+        s->brel = r;
+    }
     const char* fc = getenv("NLOT_ORACLE_FILT_CAP");
     if (fc && atoi(fc) > 0 && atoi(fc) < s->fcap) s->fcap = atoi(fc);
 }
@@ -2625,7 +2645,7 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
             s->dzu[q] = DZ(s->zu[q], p->umax[i] - s->U[q], p->umax[i] - r->U[q]);
         }
     if (s->ns && !s->gcb)
-        for (int k = 0; k <= N; ++k) s->dzs[k] = DZ(s->zs[k], s->S[k], r->S[k]);
+        for (int k = 0; k <= N; ++k) s->dzs[k] = DZ(s->zs[k], s->S[k] + s->brel, r->S[k] + s->brel);
     for (int q = 0; q < (N + 1) * M; ++q) s->dvt[q] = DZ(s->vt[q], s->T[q], r->T[q]);
 #undef DZ
     az = dual_frac(s, s->tau);
@@ -2719,14 +2739,14 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         }
     for (int k = 0; k <= N; ++k) {
         const double s0 = Sinit ? Sinit[k] : 0.0;
-        s->S[k] = (s->ns && !s->gcb) ? fmax(s0, k1) : (s->ns ? s0 : 0.0);
+        s->S[k] = (s->ns && !s->gcb) ? fmax(s0, k1 - s->brel) : (s->ns ? s0 : 0.0);
         if (s->gcb && s->ns) s->sb[N * nu + k] = fmax(s0, k1); /* slack_bound_push of d(x0) = S_k */
     }
     for (int q = 0; q < s->nb; ++q) s->zbl[q] = s->zbu[q] = 1.0;
     for (int k = 0; k <= N; ++k) {
         jet d[NLOT_MAX_BODY];
         knot_ineq(p, m, s->X + k * nx, 0, d);
-        for (int j = 0; j < M; ++j) s->T[k * M + j] = fmax(d[j].v + (s->sd ? s->S[k] : 0.0), k1);
+        for (int j = 0; j < M; ++j) s->T[k * M + j] = fmax(d[j].v + (s->sd ? s->S[k] : 0.0) + s->brel, k1);
     }
     for (int i = 0; i < N * nu; ++i) s->zl[i] = s->zu[i] = 1.0;
     for (int k = 0; k <= N; ++k) s->zs[k] = 1.0;
@@ -2794,7 +2814,10 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         eval_full(s);
         errors(s, &e);
         double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
-        if (dump) { /* iterate X and the knot multipliers yd, one record per iteration */
+        if (dump) { /* [iter, mu, f, E0, dual, primal, free mode, resto phases], X and yd, one record per iteration */
+            const double hd[8] = {(double)iter, s->mu, s->f, E0, e.dual, e.primal, (double)s->free_mode,
+                                  (double)n_resto};
+            fwrite(hd, sizeof(double), 8, dump);
             fwrite(s->X, sizeof(double), (size_t)(N + 1) * nx, dump);
             fwrite(s->yd, sizeof(double), (size_t)(N + 1) * M, dump);
         }

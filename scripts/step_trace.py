@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 STEP_COLS = ["step", "active", "evals", "trials", "unused", "reused", "solves", "resto", "soc", "resto_solves",
-             "next_active", "att_sum", "att_max", "att_multi"]
+             "next_active", "att_sum", "att_max", "att_multi", "resto_att_max"]
 KERNELS = [("mlp_full", "mlp_bf16<128, true>"), ("mlp_value", "mlp_bf16<128, false>"),
            ("iter_a", "k_iter_a<"), ("ric", "k_ric<3, false, false>"), ("ric_soc", "k_ric<3, false, true>"),
            ("ric_resto", "k_ric<3, true"), ("iter_b", "k_iter_b<"), ("accept", "k_accept<"),
