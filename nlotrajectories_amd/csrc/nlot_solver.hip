@@ -67,6 +67,9 @@ enum IterPass { PASS_ALL = 0, PASS_INIT = 1, PASS_SOC = 2, PASS_EVAL = 3 };
 #ifndef NLOT_WPE_SOC
 #define NLOT_WPE_SOC 2  // the correction (substitution) instantiation of k_ric
 #endif
+#ifndef NLOT_WPE_TPI
+#define NLOT_WPE_TPI 1  // k_ric_tpi: one instance per lane, the 512-register file (AGPRs as spill space)
+#endif
 #ifndef NLOT_RIC_RING
 #define NLOT_RIC_RING 2
 #endif
@@ -2060,7 +2063,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 // One wave per SIMD: the recursion's live set (value function, stage block, gains) is ~150 doubles per lane.
 // ---------------------------------------------------------------------------------------------
 template <int DYN, int NCR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_ric_tpi(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_TPI))) void k_ric_tpi(
     const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, const Ws* __restrict__ ws_,
     const int* __restrict__ active, int n_active, const int* __restrict__ nact, int mode, int* __restrict__ diag,
     int max_tries) {
@@ -2103,6 +2106,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
         }
         int negsum = 0;
         if (newton) SC(SC_DC) = 0.0;
+#pragma unroll 1
         for (int k = N; k >= 0; --k) {
             const int nv = (k < N ? NU : 0) + ns;
             const double* hgk = &AT(hg, k * HG);
@@ -2265,7 +2269,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
                     GN[NX * NV + v] = kg[0][v];
                     GN[(NX + 1) * NV + v] = kg[1][v];
 #pragma unroll
-                    for (int a = 0; a < NX; ++a) GN[(NX + 2 + a) * NV + v] = a < NCR ? Kn[v][a] : 0.0;
+                    for (int a = 0; a < NX; ++a) GN[(NX + 2 + a) * NV + v] = a < NCR ? Kn[v][a < NCR ? a : 0] : 0.0;
                 }
             }
             // terminal system: Psi += QN_v' Kn, psi_r += QN_v' k_r (QN's slack row is zero)
@@ -2391,6 +2395,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     // delta_w enters the stage matrices linearly (k_ric's add_dw): H += ddw (I_nz + sum_q J_q J_q'), g += ddw sum_q J_q c_q
     auto add_dw = [&](double ddw) {
         const int M = dm.M, sd = dm.sd;
+#pragma unroll 1
         for (int k = 0; k <= N; ++k) {
             double* o = &AT(hg, k * HG);
             const int is = k < N ? NX + NU : NX, nz = is + (ns ? 1 : 0);
@@ -2430,6 +2435,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     }
     int fail = 0, n_tries = 0;
     bool deferred = false;
+#pragma unroll 1
     for (int attempt = resume ? 1 : 0;; ++attempt) {
         ++n_tries;
         if (attempt > 0) {
@@ -2466,6 +2472,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
         return;
     }
 
+    // the forward sweep runs in k_ric_tpi_fwd (its own register budget): nu_r in yt_n / yt2, SC_RIC = 5
+#pragma unroll
+    for (int a = 0; a < NCR; ++a) {
+        AT(yt_n, a) = nu_[0][a];
+        AT(yt2, a) = nu_[1][a];
+    }
+    if (dw > 0.0 && newton) SC(SC_DWLAST) = dw;
+    SC(SC_RETRY) = -1.0;
+    SC(SC_DW) = dw;
+    SC(SC_RIC) = 5;
+}
+
+// Forward sweep of k_ric_tpi (instances with SC_RIC = 5): its own kernel, so the backward sweep's register budget
+// does not bound it.  Reads the gains, vf and the slots' [A B 0 | c] | M, nu_r from yt_n / yt2.
+template <int DYN, int NCR>
+__global__ __launch_bounds__(64) void k_ric_tpi_fwd(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+                                                    const Ws* __restrict__ ws_, const int* __restrict__ active,
+                                                    int n_active, const int* __restrict__ nact, int mode, int write_phi) {
+    using SV = Solver<DYN>;
+    constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NCOL = SV::NCOL, NAB = SV::NAB;
+    constexpr int SLOT = SV::SLOT, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
+    constexpr int PR = NX + 2;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    const int si = (int)(blockIdx.x * 64 + threadIdx.x);
+    const int nlist = std::min(n_active, *nact);
+    if (si >= nlist) return;
+    const int b = active[si];
+    if ((int)SC(SC_RIC) != 5) return;
+    const int N = dm.N, ns = dm.ns, nr = (int)SC(SC_RNR);
+    const bool newton = mode == MODE_NEWTON;
+    double* SL = &AT(stg, 0);
+    double nu_[2][NCR];
+#pragma unroll
+    for (int a = 0; a < NCR; ++a) {
+        nu_[0][a] = AT(yt_n, a);
+        nu_[1][a] = AT(yt2, a);
+    }
     // forward sweep: dv_k = k_r + K dx_k + Kn nu_r; the closed-loop map Phi = A + B K and offsets off_r = c + B (k_r +
     // Kn nu_r) go to phi (the corrections reuse Phi); dx_{k+1} = Phi dx_k + off_r; multipliers y_k = -grad V_{k+1}(dx_{k+1})
     // - M_k' dx_k, y_init = -grad V_0(dx_0), y_term = nu
@@ -2474,10 +2518,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
     double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
     double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
-    double* yto[2] = {&AT(yt_n, 0), &AT(yt2, 0)};
     double x[2][NX], xp[2][NX], Mp[2][2] = {{0, 0}, {0, 0}};
 #pragma unroll
     for (int i = 0; i < NX; ++i) x[0][i] = x[1][i] = newton ? -AT(rci, i) : 0.0;
+#pragma unroll 1
     for (int k = 0; k <= N; ++k) {
         const double* sk = SL + (size_t)k * SLOT;
         const double* GN = sk + sGN;
@@ -2530,7 +2574,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
             }
         }
         if (k == N) break;
-        double* ph = &AT(phi, (size_t)k * NX * PR);
+        double* ph = write_phi ? &AT(phi, (size_t)k * NX * PR) : nullptr;
         double xn[2][NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
@@ -2549,12 +2593,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
                 double f = sk[sAB + i * NAB + j];
 #pragma unroll
                 for (int v = 0; v < NU; ++v) f += Bi[v] * Kt[v][j];
-                ph[i * PR + j] = f;
+                if (ph) ph[i * PR + j] = f;
                 t0 += f * x[0][j];
                 t1 += f * x[1][j];
             }
-            ph[i * PR + NX] = o0;
-            ph[i * PR + NX + 1] = o1;
+            if (ph) {
+                ph[i * PR + NX] = o0;
+                ph[i * PR + NX + 1] = o1;
+            }
             xn[0][i] = t0;
             xn[1][i] = t1;
         }
@@ -2570,15 +2616,201 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
             x[1][i] = xn[1][i];
         }
     }
+    SC(SC_RIC) = 2;
+}
+
+// Second-order corrections, thread-per-instance (k_soc_tpi): the substitution of k_ric<DYN, false, true> (same
+// recursion: w = P' c + p', q = g + M c + AB' w, k = -Q_vv^-1 q_v with the stored factor, p = q_x + K' q_v, psi +=
+// Gamma'(c + B k), nu from the stored terminal factor; then the forward sweep) with one instance per lane.  Reads
+// what the iteration's Newton solve stored (gains, vf, qfac, tfac) and k_iter_a's corrected g and c; writes k_0 into
+// the gains and p_0 into vf, the step and the multipliers.  The closed-loop maps are recomputed from A, B and K.
+template <int DYN, int NCR>
+__global__ __launch_bounds__(64) 
+void k_soc_tpi(
+    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, const Ws* __restrict__ ws_,
+    const int* __restrict__ active, int n_active, const int* __restrict__ nact) {
+    using SV = Solver<DYN>;
+    constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NCOL = SV::NCOL, NAB = SV::NAB;
+    constexpr int NZA = NX + NU;
+    constexpr int SLOT = SV::SLOT, HG = SV::HG, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
+    constexpr int QFL = ldl_len(NV), HW = NZ + 2;
+    const Dims& dm = *dd_;
+    const Ws& ws = *ws_;
+    if (ws.prio) __builtin_amdgcn_s_setprio(2);  // NLOT_SETPRIO (see k_ric)
+    const int si = (int)(blockIdx.x * 64 + threadIdx.x);
+    const int nlist = std::min(n_active, *nact);
+    if (si >= nlist) return;
+    const int b = active[si];
+    if ((int)SC(SC_RIC) != 1 || SC(SC_RESTO) != 0.0 || SC(SC_RICFIX) < 0.0) return;
+    const int N = dm.N, ns = dm.ns;
+    double* SL = &AT(stg, 0);
+    // backward substitution
+    double pn[NX], psi[NCR];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-        if (rr >= nr) break;
+    for (int i = 0; i < NX; ++i) pn[i] = 0.0;
 #pragma unroll
-        for (int a = 0; a < NCR; ++a) yto[rr][a] = nu_[rr][a];
+    for (int a = 0; a < NCR; ++a) psi[a] = 0.0;
+#pragma unroll 1
+    for (int k = N; k >= 0; --k) {
+        const int nv = (k < N ? NU : 0) + ns;
+        const bool kn = k < N;
+        const double* sk = SL + (size_t)k * SLOT;
+        double* GN = SL + (size_t)k * SLOT + sGN;
+        const double* hgk = &AT(hg, k * HG);
+        const double* vn = &AT(vf, (kn ? k + 1 : N) * VF);
+        double c[NX], w[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) c[i] = kn ? sk[sAB + i * NAB + NZ] : 0.0;
+        // w = P' c + p' (the value function of stage k + 1; zero beyond the horizon)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double t = pn[i];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) t += vn[i * NCOL + j] * c[j];
+            w[i] = kn ? t : 0.0;
+        }
+        double q[NZ];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) {
+            double t = hgk[i * HW + NZ];
+            if (kn) {
+                if (i < 2) t += sk[sM + 2 * i] * c[0] + sk[sM + 2 * i + 1] * c[1];
+                if (i < NZA) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) t += sk[sAB + r * NAB + i] * w[r];
+                }
+            }
+            q[i] = t;
+        }
+        double kv[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) kv[v] = v < nv ? -q[NX + v] : 0.0;
+        if (nv > 0) {
+            double L[NV][NV];
+            int perm[NV];
+            const double* f = &AT(qfac, k * QFL);
+#pragma unroll
+            for (int a = 0; a < NV; ++a) {
+#pragma unroll
+                for (int cc = 0; cc < NV; ++cc) L[a][cc] = f[a * NV + cc];
+                perm[a] = (int)f[NV * NV + a];
+            }
+            ldl_solve1<NV>(L, nv, perm, kv);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) GN[NX * NV + v] = kv[v];  // k_0
+        // p = q_x + K' q_v (K' q_v = Q_xv k), e = c + B k, psi += Gamma' e (at N: psi = the terminal residuals)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double t = q[i];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) t += GN[i * NV + v] * q[NX + v];
+            pn[i] = t;
+            AT(vf, k * VF + i * NCOL + NX) = t;  // p_0
+        }
+        if (!kn) {
+#pragma unroll
+            for (int a = 0; a < NCR; ++a) psi[a] = AT(rct, a);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double e = c[i];
+#pragma unroll
+                for (int v = 0; v < NU; ++v) e += sk[sAB + i * NAB + NX + v] * kv[v];
+#pragma unroll
+                for (int a = 0; a < NCR; ++a) psi[a] += vn[i * NCOL + NX + 2 + a] * e;
+            }
+        }
     }
-    if (dw > 0.0 && newton) SC(SC_DWLAST) = dw;
+    // terminal multiplier: (-Psi + delta_c) nu = psi + Gamma_0' dx0 with the Newton solve's stored factor
+    double dx0[NX], nu[NCR];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) dx0[i] = -AT(rci, i);
+    {
+        const double* v0 = &AT(vf, 0);
+#pragma unroll
+        for (int a = 0; a < NCR; ++a) {
+            double t = psi[a];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) t += v0[r * NCOL + NX + 2 + a] * dx0[r];
+            nu[a] = t;
+        }
+        double L[NCR][NCR];
+        int perm[NCR];
+        const double* f = &AT(tfac, 0);
+#pragma unroll
+        for (int a = 0; a < NCR; ++a) {
+#pragma unroll
+            for (int cc = 0; cc < NCR; ++cc) L[a][cc] = f[a * NX + cc];
+            perm[a] = (int)f[NX * NX + a];
+        }
+        ldl_solve1<NCR>(L, NCR, perm, nu);
+    }
+    // forward sweep (one right-hand side): dv_k = k_0 + K dx_k + Kn nu, dx_{k+1} = A dx_k + B dv_k + c_k, multipliers
+    double x[NX], xp[NX], Mp[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll
+    for (int i = 0; i < NX; ++i) x[i] = dx0[i];
+#pragma unroll 1
+    for (int k = 0; k <= N; ++k) {
+        const double* sk = SL + (size_t)k * SLOT;
+        const double* GN = sk + sGN;
+        const double* vfk = &AT(vf, k * VF);
+        double dv[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            double t = GN[NX * NV + v];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) t += GN[j * NV + v] * x[j];
+#pragma unroll
+            for (int a = 0; a < NCR; ++a) t += GN[(NX + 2 + a) * NV + v] * nu[a];
+            dv[v] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) AT(dX, k * NX + i) = x[i];
+        if (k < N)
+#pragma unroll
+            for (int v = 0; v < NU; ++v) AT(dU, k * NU + v) = dv[v];
+        if (ns) AT(dS, k) = k < N ? dv[NU] : dv[0];
+        double mx[2] = {0.0, 0.0};
+        if (k > 0) {
+            mx[0] = Mp[0][0] * xp[0] + Mp[1][0] * xp[1];
+            mx[1] = Mp[0][1] * xp[0] + Mp[1][1] * xp[1];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double t = vfk[i * NCOL + NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) t += vfk[i * NCOL + j] * x[j];
+#pragma unroll
+            for (int a = 0; a < NCR; ++a) t += vfk[i * NCOL + NX + 2 + a] * nu[a];
+            if (k == 0) AT(yi_n, i) = -t;
+            else AT(yk_n, (k - 1) * NX + i) = -t - (i < 2 ? mx[i] : 0.0);
+        }
+        if (k == N) break;
+        double xn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double t = sk[sAB + i * NAB + NZ];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) t += sk[sAB + i * NAB + j] * x[j];
+#pragma unroll
+            for (int v = 0; v < NU; ++v) t += sk[sAB + i * NAB + NX + v] * dv[v];
+            xn[i] = t;
+        }
+        Mp[0][0] = sk[sM];
+        Mp[0][1] = sk[sM + 1];
+        Mp[1][0] = sk[sM + 2];
+        Mp[1][1] = sk[sM + 3];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            xp[i] = x[i];
+            x[i] = xn[i];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < NCR; ++a) AT(yt_n, a) = nu[a];
     SC(SC_RETRY) = -1.0;
-    SC(SC_DW) = dw;
+    SC(SC_DW) = SC(SC_RICFIX);
     SC(SC_RIC) = 2;
 }
 
@@ -5091,13 +5323,20 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     // sequential sweep, few instances) touch disjoint instances from the main Newton solve: they run on a side
     // stream, forked after k_iter_a, so their latency hides under k_ric's; k_iter_b joins the corrections, the
     // value-MLP launch joins the restoration chain (k_resto_b appends to the same trial list).
-    // NLOT_STREAM_PRIO (A/B knob): 1 = the restoration stream at the highest priority, 2 = the correction stream too
+    // NLOT_STREAM_PRIO (A/B knob, measured neutral in round 4): 1 = the restoration stream at the highest priority,
+    // 2 = the correction stream too; unset: default-priority streams
     int stream_prio = 0;
     if (const char* e = getenv("NLOT_STREAM_PRIO")) stream_prio = atoi(e);
-    int prio_lo = 0, prio_hi = 0;
-    NLOT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    NLOT_HIP_CHECK(hipStreamCreateWithPriority(&res.s2, hipStreamNonBlocking, stream_prio >= 2 ? prio_hi : prio_lo));
-    NLOT_HIP_CHECK(hipStreamCreateWithPriority(&res.s3, hipStreamNonBlocking, stream_prio >= 1 ? prio_hi : prio_lo));
+    if (stream_prio > 0) {
+        int prio_least = 0, prio_greatest = 0;
+        NLOT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+        if (stream_prio >= 2) NLOT_HIP_CHECK(hipStreamCreateWithPriority(&res.s2, hipStreamNonBlocking, prio_greatest));
+        else NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s2, hipStreamNonBlocking));
+        NLOT_HIP_CHECK(hipStreamCreateWithPriority(&res.s3, hipStreamNonBlocking, prio_greatest));
+    } else {
+        NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s2, hipStreamNonBlocking));
+        NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s3, hipStreamNonBlocking));
+    }
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_a, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_soc, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_r, hipEventDisableTiming));
@@ -5234,19 +5473,29 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         }
         synced = last + 1;
     };
-    // the factorising Newton solves (main stream): thread-per-instance (k_ric_tpi, default) or the lane-group k_ric
-    // (NLOT_RIC_TPI=0); k_ric_tpi is instantiated for nc = nx - 1 (free terminal heading) and nc = nx
-    const bool ric_tpi = !(getenv("NLOT_RIC_TPI") && atoi(getenv("NLOT_RIC_TPI")) == 0) &&
+    // the factorising Newton solves (main stream): the lane-group k_ric, or thread-per-instance (k_ric_tpi, opt-in
+    // NLOT_RIC_TPI=1, nx <= 5: measured slower in round 4, kept for the A/B); k_ric_tpi is instantiated for nc = nx - 1
+    // (free terminal heading) and nc = nx
+    const bool ric_tpi = getenv("NLOT_RIC_TPI") && atoi(getenv("NLOT_RIC_TPI")) != 0 && Dyn<DYN>::NX <= 5 &&
                          (dm.nc == Dyn<DYN>::NX || dm.nc == Dyn<DYN>::NX - 1);
     auto launch_ric = [&](const int* list, const int* count, int mode, int* diag, int tries) {
         if (ric_tpi) {
             const dim3 grid((n_active + 63) / 64);
-            if (dm.nc == Dyn<DYN>::NX)
-                hipLaunchKernelGGL((k_ric_tpi<DYN, Dyn<DYN>::NX>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active,
-                                   count, mode, diag, tries);
-            else
-                hipLaunchKernelGGL((k_ric_tpi<DYN, (Dyn<DYN>::NX > 1 ? Dyn<DYN>::NX - 1 : 1)>), grid, dim3(64), 0, st, dP,
-                                   dD, dW, list, n_active, count, mode, diag, tries);
+            constexpr int NXD = Dyn<DYN>::NX, NXM = NXD > 1 ? NXD - 1 : 1;
+            // phi (closed-loop maps) only for the lane-group corrections (NLOT_RIC_TPI=0 for them is not offered:
+            // both paths switch together), so the thread-per-instance forward sweep skips it
+            const int write_phi = 0;
+            if (dm.nc == NXD) {
+                hipLaunchKernelGGL((k_ric_tpi<DYN, NXD>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count, mode,
+                                   diag, tries);
+                hipLaunchKernelGGL((k_ric_tpi_fwd<DYN, NXD>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count,
+                                   mode, write_phi);
+            } else {
+                hipLaunchKernelGGL((k_ric_tpi<DYN, NXM>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count, mode,
+                                   diag, tries);
+                hipLaunchKernelGGL((k_ric_tpi_fwd<DYN, NXM>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count,
+                                   mode, write_phi);
+            }
         } else {
             hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
                                st, dP, dD, dW, list, n_active, count, mode, diag, tries);
@@ -5275,8 +5524,18 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             if (with_pass)
                 hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, s2, dP, dD, o, dW, act, ws.x0s, ws.xgs,
                                    (int)PASS_SOC, C, Cn);
-            hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64),
-                               0, s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
+            if (ric_tpi) {
+                const dim3 grid((n_active + 63) / 64);
+                if (dm.nc == Dyn<DYN>::NX)
+                    hipLaunchKernelGGL((k_soc_tpi<DYN, Dyn<DYN>::NX>), grid, dim3(64), 0, s2, dP, dD, dW, ws.socl,
+                                       n_active, C + 6);
+                else
+                    hipLaunchKernelGGL((k_soc_tpi<DYN, (Dyn<DYN>::NX > 1 ? Dyn<DYN>::NX - 1 : 1)>), grid, dim3(64), 0, s2,
+                                       dP, dD, dW, ws.socl, n_active, C + 6);
+            } else {
+                hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per),
+                                   dim3(64), 0, s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
+            }
             NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
             return NLOT_OK;
         };

@@ -1,0 +1,55 @@
+"""tests/golden/oracle_outcomes.npz still describes this oracle (CPU): the GPU parity tests compare against its stored
+oracle outcomes (tests/outcomes.py), so a change of the oracle's arithmetic must regenerate it
+(tests/golden/make_oracle_outcomes.py).  Re-runs the fixture's quickest instances (fewest iterations) at x0 and
+x0 + 1e-13 and asks for bitwise the same status, iterations and final cost."""
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _fixture():
+    return dict(np.load(os.path.join(HERE, "golden", "oracle_outcomes.npz")))
+
+
+def test_fixture_layout():
+    f = _fixture()
+    for case, n in (("metric", 128), ("b6", 24)):
+        assert f[f"{case}_x0"].shape[0] == n and f[f"{case}_status"].shape == (3, n)
+        assert f[f"{case}_cost"].shape == (3, n) and f[f"{case}_iters"].shape == (3, n)
+    assert f["b6_xinit"].shape == (24, 101, 7)
+    # the split has both groups on the headline workload (tests/outcomes.py)
+    import sys
+
+    sys.path.insert(0, HERE)
+    from outcomes import reproducible
+
+    R = reproducible({k: f[f"metric_{k}"] for k in ("status", "cost")})
+    print("metric fixture: reproducible", int(R.sum()), "of", len(R))
+    assert 0 < R.sum() < len(R)
+
+
+def test_fixture_matches_oracle():
+    import oracle as O
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
+
+    f = _fixture()
+    opt = _abi.default_options()
+    hm = O.HostMlp(MlpWeights.artefact())
+    its = f["metric_iters"][0]
+    for i in np.argsort(its, kind="stable")[:4]:
+        for r, d in ((0, 0.0), (1, 1e-13)):
+            x0 = f["metric_x0"][i].copy()
+            x0[0] += d
+            res = O.solve_one(METRIC_PROBLEM, x0, f["metric_xg"][i], hm, opt=opt)
+            assert res["status"] == f["metric_status"][r, i] and res["iters"] == f["metric_iters"][r, i], (i, r)
+            assert res["cost"] == f["metric_cost"][r, i], (i, r, res["cost"], f["metric_cost"][r, i])
+    hm6 = O.HostMlp(MlpWeights.load(os.path.join(os.path.dirname(HERE), "nlotrajectories_amd", "data",
+                                                 "b6_mlp128_seed0.npz")))
+    i = int(np.argmin(f["b6_iters"][0]))
+    res = O.solve_one(B6_PROBLEM, f["b6_x0"][i], f["b6_xg"][i], hm6, opt=opt, X_init=f["b6_xinit"][i])
+    assert res["status"] == f["b6_status"][0, i] and res["iters"] == f["b6_iters"][0, i]
+    assert res["cost"] == f["b6_cost"][0, i]

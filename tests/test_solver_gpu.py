@@ -63,36 +63,20 @@ def test_iterates_match_oracle_learned(artefact, strategy):
         np.testing.assert_allclose(rg["U"][0].cpu().numpy(), rc["U"], atol=1e-4)
 
 
-def _stats(rg, rc):
-    sg, sc = rg["status"].cpu().numpy(), rc["status"]
-    both = (sg == 0) & (sc == 0)
-    rel = np.abs(rg["cost"].cpu().numpy() - rc["cost"]) / np.abs(rc["cost"])
-    return (sg == sc).mean(), both, rel
+def _fixture():
+    import os
 
-
-def _self_agreement(O, problem, x0, xg, opt, hm=None):
-    """The oracle run twice, the second time with x0 perturbed by 1e-13: how reproducible its outcomes are."""
-    rc = O.solve_batch(problem, x0, xg, hm, opt=opt)
-    xp = x0.copy()
-    xp[:, 0] += 1e-13
-    rp = O.solve_batch(problem, xp, xg, hm, opt=opt)
-    return rc, rp
-
-
-def _agreement(sa, ca, sb, cb):
-    both = (sa == 0) & (sb == 0)
-    rel = np.abs(ca - cb) / np.abs(cb)
-    return (sa == sb).mean(), int(both.sum()), float((rel[both] <= 1e-4).mean()) if both.any() else 1.0, rel[both]
+    return dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_outcomes.npz")))
 
 
 @pytest.mark.parametrize("strategy", list(STRATEGIES))
 def test_batch_b2_analytic_matches_oracle(strategy):
-    """64 seeded b2 instances (analytic SDF).  Monotone mu at tol 1e-4; adaptive mu at tol 1e-8 (its tol 1e-4
-    termination point depends on the sigma choices along the path).  Outcome parity is measured against the
-    oracle's own reproducibility under a 1e-13 change of x0 (IPOPT's discrete decisions -- filter, watchdog,
-    second-order corrections, mode switches -- amplify rounding): the GPU must agree with the oracle at
-    least as well, less 5 % (64 samples), and jointly solved costs agree to 1e-4 on >= 80 % (median <= 1e-6)."""
+    """64 seeded b2 instances (analytic SDF).  Monotone mu at tol 1e-4; adaptive mu at tol 1e-8.  Solve-level
+    parity split by the oracle's own reproducibility (tests/outcomes.py): on the instances whose oracle outcome is
+    unchanged by +-1e-13 start perturbations the GPU gives the same status and a final cost within 1e-4 on 100 %;
+    on the rest, agreement at least as good as the oracle's with itself."""
     O = _oracle()
+    from outcomes import check_outcome_parity, oracle_outcomes
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.sampling import sample_start_goal
@@ -104,62 +88,32 @@ def test_batch_b2_analytic_matches_oracle(strategy):
     tight = dict(tol=1e-8, constr_viol_tol=1e-8, compl_inf_tol=1e-8) if strategy == "adaptive" else {}
     opt = _abi.gpu_options(**STRATEGIES[strategy], **tight)
     rg = solve_batch(p, x0, xg, options=opt)
-    rc, rp = _self_agreement(O, p, x0, xg, opt)
+    out = oracle_outcomes(O, p, x0, xg, opt=opt)
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
-    st_g, n_g, c_g, rel_g = _agreement(sg, cg, rc["status"], rc["cost"])
-    st_s, n_s, c_s, _ = _agreement(rp["status"], rp["cost"], rc["status"], rc["cost"])
-    print(f"b2 {strategy}: GPU vs oracle status {st_g:.3f} jointly solved {n_g} cost<=1e-4 {c_g:.3f} median "
-          f"{np.median(rel_g) if len(rel_g) else 0:.1e}; oracle self: status {st_s:.3f} jointly solved {n_s} "
-          f"cost<=1e-4 {c_s:.3f}; GPU {np.bincount(sg, minlength=7).tolist()} oracle "
-          f"{np.bincount(rc['status'], minlength=7).tolist()}", flush=True)
-    assert st_g >= st_s - 0.15  # 64 samples of a chaotic outcome (adaptive mu swings, restoration phases)
-    assert n_g >= 0.5 * len(x0)
-    assert c_g >= 0.8 and np.median(rel_g) <= 1e-6
+    info = check_outcome_parity(f"b2 {strategy}", sg, cg, out, min_reproducible=16)
+    assert ((sg == 0) & (out["status"][0] == 0)).sum() >= 0.5 * len(x0), info
 
 
 def test_batch_learned_sdf_matches_oracle(artefact):
-    """The metric workload (learned SDF, the reference's tol 1e-4, the IPOPT settings the GPU runs) on 256
-    seeded instances, with max_iter 300 (the oracle's 1000-iteration runs would keep this test on the CPU for
-    minutes; solved instances take 116 iterations on average).  Outcomes at tol 1e-4 are path-sensitive (ReLU
-    kinks, discrete filter / watchdog / mode decisions), so the bar is the oracle's own reproducibility,
-    measured on the first 128 instances with x0 perturbed by 1e-13: the GPU must agree with the oracle at least
-    as well, less 4 % (status) and 6 % (1e-4-relative final cost of jointly solved instances), with a 75 %
-    floor on status agreement."""
-    O = _oracle()
+    """The metric workload (learned SDF, the reference's settings: tol 1e-4, max_iter 1000, adaptive mu,
+    restoration) on the 128 seeded instances of tests/golden/oracle_outcomes.npz, whose oracle outcomes at x0 and
+    x0 +- 1e-13 the fixture holds (tests/golden/make_oracle_outcomes.py; the oracle's 1000-iteration runs take
+    minutes of CPU).  Split parity (tests/outcomes.py): identical status and final cost within 1e-4 on every
+    oracle-reproducible instance; the oracle's own spread on the chaotic ones."""
+    from outcomes import check_outcome_parity
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.ops import DeviceMlp
     from nlotrajectories_amd.problem import METRIC_PROBLEM
-    from nlotrajectories_amd.sampling import sample_start_goal
     from nlotrajectories_amd.solver import solve_batch
 
-    tm = artefact.torch_module()
-    sdf = lambda P: tm(torch.tensor(np.asarray(P), dtype=torch.float32)).detach().numpy()[:, 0]
-    x0, xg = sample_start_goal(METRIC_PROBLEM, 256, seed=0, sdf=sdf)
-    opt = _abi.gpu_options(max_iter=300)
-    rg = solve_batch(METRIC_PROBLEM, x0, xg, mlp=DeviceMlp(artefact), options=opt)
-    hm = O.HostMlp(artefact)
-    parts = []
-    for c in range(0, 256, 32):
-        parts.append(O.solve_batch(METRIC_PROBLEM, x0[c:c + 32], xg[c:c + 32], hm, opt=opt))
-        print(f"oracle {c + 32}/256", flush=True)
-    rc = {k: np.concatenate([p[k] for p in parts]) for k in ("status", "cost")}
-    xp = x0[:128].copy()
-    xp[:, 0] += 1e-13
-    parts = []
-    for c in range(0, 128, 32):
-        parts.append(O.solve_batch(METRIC_PROBLEM, xp[c:c + 32], xg[c:c + 32], hm, opt=opt))
-        print(f"perturbed oracle {c + 32}/128", flush=True)
-    rp = {k: np.concatenate([p[k] for p in parts]) for k in ("status", "cost")}
+    f = _fixture()
+    out = {k: f[f"metric_{k}"] for k in ("status", "cost", "iters")}
+    rg = solve_batch(METRIC_PROBLEM, f["metric_x0"], f["metric_xg"], mlp=DeviceMlp(artefact),
+                     options=_abi.gpu_options())
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
-    st_g, n_g, c_g, rel_g = _agreement(sg, cg, rc["status"], rc["cost"])
-    st_s, n_s, c_s, _ = _agreement(rp["status"], rp["cost"], rc["status"][:128], rc["cost"][:128])
-    print(f"metric: GPU vs oracle status {st_g:.3f}, jointly solved {n_g}, cost<=1e-4 {c_g:.3f}, median rel "
-          f"{np.median(rel_g) if len(rel_g) else 0:.2e}; oracle vs perturbed oracle (128): status {st_s:.3f}, "
-          f"jointly solved {n_s}, cost<=1e-4 {c_s:.3f}; GPU status counts {np.bincount(sg, minlength=7).tolist()}, "
-          f"oracle {np.bincount(rc['status'], minlength=7).tolist()}", flush=True)
-    assert st_g >= 0.75 and st_g >= st_s - 0.04  # the oracle agrees with itself on ~80 % (max_iter vs solved late)
-    assert n_g >= 0.25 * len(x0)
-    assert c_g >= c_s - 0.06
+    print("metric GPU status counts", np.bincount(sg, minlength=7).tolist(), "oracle",
+          np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
+    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=32)
 
 
 def test_safeguards_iterate_parity(artefact):
