@@ -3041,12 +3041,12 @@ __device__ inline void filter_add(const Ws& ws, int b, double* filt, int sc_n, d
             filt[2 * i + 1] = filt[2 * (i + 1) + 1];
         }
         w--;
-        atomicAdd(cs + 12, 1);
+        if (cs) atomicAdd(cs + 12, 1);
     }
     filt[2 * w] = ntv;
     filt[2 * w + 1] = npv;
     SC(sc_n) = w + 1;
-    atomicMax(cs + 11, w + 1);
+    if (cs) atomicMax(cs + 11, w + 1);
 }
 
 // The line search of the original problem failed and the soft restoration did not help: IPOPT's feasibility
@@ -5142,7 +5142,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
         if (!(na < SC(SC_AMIN))) emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
         return;
     }
-    if (!fa && lane == 0) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, cnt);
+    if (!fa && lane == 0) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, nullptr);  // no statistics here
     // accept: primal, p, n and equality multipliers with alpha; bound multipliers (z_p, z_n included) with alpha_z
     const double az = SC(SC_AZ), ks = 1e10;
     auto zupd = [&](double z, double dz, double sl) {

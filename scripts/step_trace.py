@@ -24,7 +24,8 @@ KERNELS = [("mlp_full", "mlp_bf16<128, true>"), ("mlp_value", "mlp_bf16<128, fal
            ("iter_a", "k_iter_a<"), ("ric", "k_ric<3, false, false>"), ("ric_soc", "k_ric<3, false, true>"),
            ("ric_resto", "k_ric<3, true"), ("iter_b", "k_iter_b<"), ("accept", "k_accept<"),
            ("resto_a", "k_resto_a<"), ("resto_b", "k_resto_b<"), ("resto_ls", "k_resto_ls<"),
-           ("points", "k_points"), ("admit", "k_admit"), ("copy", "copyBuffer"), ("fill", "fillBuffer")]
+           ("points", "k_points"), ("admit", "k_admit"), ("copy", "copyBuffer"), ("fill", "fillBuffer"),
+           ("ric_tpi", "k_ric_tpi<"), ("ric_tpi_fwd", "k_ric_tpi_fwd<"), ("soc_tpi", "k_soc_tpi<")]
 
 
 def run(B, G, slots, outdir):
