@@ -376,6 +376,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+#pragma clang fp contract(off)  // x is the rounded fp32 input: never fuse its producer into the subtractions
     h = (__bf16)x;
     const float r = x - (float)h;  // exact
     m = (__bf16)r;
@@ -409,28 +410,51 @@ __device__ __forceinline__ bf16x8 wt_frag(const __bf16* plane, int jbase, int co
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// one weight image per CU, shared by NLOT_MLP_*_THREADS / 256 waves per SIMD: value-only launches 3 (162
-// VGPRs); FULL (value + reverse sweep) 1, with the whole 512-register file (at 2 per SIMD it spills
-// ~440 B/lane and ran 3 % slower in the solve, profiles/r01/variants_v14.log)
-// NLOT_MLP_VALUE_PG: 32-point groups per wave of the value-only kernel; with 2 every A fragment read from LDS feeds
-// two MFMAs (one per group), at 2 waves per SIMD (the accumulators of both groups: ~230 VGPRs)
-#ifndef NLOT_MLP_VALUE_PG
-#define NLOT_MLP_VALUE_PG 1  // 2 measured: value launch -2 % alone, solve +1 % (profiles/r03/steps/ab_value_pg.txt)
-#endif
+// one weight image per CU, shared by NLOT_MLP_*_THREADS / 256 waves per SIMD: value-only launches 3; FULL (value +
+// reverse sweep) NLOT_MLP_FULL_THREADS / 256.  Round 4: the input layer is a template parameter (no per-element
+// branch on the kind), its weights are read as float4 runs (a lane's 8 consecutive k of a 16-wide k block), and the
+// reverse sweep's contraction re-reads its LDS operands every tile (an opaque zero offset keeps the compiler from
+// hoisting 192 loop-invariant floats into registers across the tile loop, which had pinned FULL at one wave per
+// SIMD: 256 VGPRs + 184 AGPRs, or 504 B/lane of scratch at two).
 #ifndef NLOT_MLP_VALUE_THREADS
-#define NLOT_MLP_VALUE_THREADS (NLOT_MLP_VALUE_PG > 1 ? 512 : 768)
+#define NLOT_MLP_VALUE_THREADS 768
 #endif
 #ifndef NLOT_MLP_FULL_THREADS
-#define NLOT_MLP_FULL_THREADS 256
+#define NLOT_MLP_FULL_THREADS 512
 #endif
 __host__ __device__ constexpr int bf16_threads(bool full) { return full ? NLOT_MLP_FULL_THREADS : NLOT_MLP_VALUE_THREADS; }
 
 template <int H>
 __host__ __device__ constexpr size_t mlp_bf16_lds_bytes() {
-    return (size_t)3 * H * (H + 8) * 2 + (size_t)5 * H * 4;
+    return (size_t)3 * H * (H + 8) * 2 + (size_t)8 * H * 4;
 }
 
-template <int H, bool FULL>
+// a zero the compiler cannot see through (a VGPR written by an opaque move): added to an LDS offset inside a loop,
+// it keeps loop-invariant LDS reads in the loop
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
+__device__ __forceinline__ void lds8(const float* p, float (&o)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w;
+}
+
+// input-layer activation of z = p @ A + b0 (nn_architectures.py:38 for the Fourier layer)
+template <bool FOUR>
+__device__ __forceinline__ float in_act(float z, float scale) {
+    if constexpr (FOUR) {
+        // rounded product (no contraction into split3's subtraction): h0 is the fp32 value the oracle forms
+#pragma clang fp contract(off)
+        return __builtin_amdgcn_cosf(turns_fourier(z)) * scale;
+    } else {
+        return z > 0.f ? z : 0.f;
+    }
+}
+
+template <int H, bool FULL, bool FOUR>
 __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
                                                             const int* __restrict__ cnt_dev, int P_per, int64_t ld,
                                                             const float* __restrict__ lam, MlpOut out, MlpReuse ru) {
@@ -444,17 +468,22 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     float* sb0 = sA1 + H;
     float* sb = sb0 + H;
     float* sw = sb + H;
+    float* sq = sw + H;  // [3][H]: A0^2, A0 A1, A1^2 (the Fourier Hessian's per-k factors, as the oracle rounds them)
     __shared__ int s_reused;
     for (int idx = threadIdx.x; idx < 3 * H * H / 8; idx += blockDim.x) {  // 16-byte chunks of the planes
         const int pr = idx / (H / 8), c8 = idx % (H / 8);                   // pr = plane * H + row
         *reinterpret_cast<uint4*>(sWp + (size_t)pr * RS + c8 * 8) = reinterpret_cast<const uint4*>(w.Wp)[idx];
     }
     for (int idx = threadIdx.x; idx < H; idx += blockDim.x) {
-        sA0[idx] = w.A[idx];
-        sA1[idx] = w.A[H + idx];
+        const float a0 = w.A[idx], a1 = w.A[H + idx];
+        sA0[idx] = a0;
+        sA1[idx] = a1;
         sb0[idx] = w.b0[idx];
         sb[idx] = w.b[idx];
         sw[idx] = w.w_out[idx];
+        sq[idx] = a0 * a0;
+        sq[H + idx] = a0 * a1;
+        sq[2 * H + idx] = a1 * a1;
     }
     if (threadIdx.x == 0) s_reused = 0;
     __syncthreads();
@@ -464,118 +493,12 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     const int64_t g0 = (ru.base && ld == 0) ? (int64_t)(*ru.base) * P_per : 0;  // first point of the launch
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int il = lane & 31, hl = lane >> 5;
-    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
     const float scale = w.scale;
     constexpr int TP = bf16_threads(FULL) / 2;  // points per block tile (32 per wave)
-    if constexpr (!FULL && NLOT_MLP_VALUE_PG > 1) {
-        // value-only launches, VPG groups of 32 points per wave: the same arithmetic per point as the loop below
-        // (input layer, split, the six products in the same k order, bias + ReLU + output layer), each A fragment
-        // read once for the VPG groups' MFMAs
-        constexpr int VPG = NLOT_MLP_VALUE_PG, TPV = TP * VPG;
-        const int64_t G = gridDim.x;
-        auto loadp = [&](int64_t tile, float* px, float* py) {
-#pragma unroll
-            for (int pg = 0; pg < VPG; ++pg) {
-                const int64_t gi = g0 + tile * TPV + (int64_t)wave * 32 * VPG + pg * 32 + il;
-                px[pg] = py[pg] = 0.f;
-                if (gi < npts) {
-                    const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
-                    px[pg] = pts[2 * pi];
-                    py[pg] = pts[2 * pi + 1];
-                }
-            }
-        };
-        float ax[VPG], ay[VPG], bx[VPG], by[VPG];
-        loadp(blockIdx.x, ax, ay);
-        loadp(blockIdx.x + G, bx, by);
-        for (int64_t tile = blockIdx.x; g0 + tile * TPV < npts; tile += G) {
-            float cx[VPG], cy[VPG];
-            loadp(tile + 2 * G, cx, cy);
-            bool valid[VPG];
-            int64_t pi[VPG];
-            bool any = false;
-#pragma unroll
-            for (int pg = 0; pg < VPG; ++pg) {
-                const int64_t gi = g0 + tile * TPV + (int64_t)wave * 32 * VPG + pg * 32 + il;
-                valid[pg] = gi < npts;
-                pi[pg] = valid[pg] ? (ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld) : 0;
-                any = any || valid[pg];
-            }
-            if (__any(any)) {
-                f32x16 acc[VPG][NT];
-#pragma unroll
-                for (int pg = 0; pg < VPG; ++pg)
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) acc[pg][t] = f32x16{};
-#pragma unroll 1
-                for (int s = 0; s < NKB; ++s) {
-                    bf16x8 bh[VPG], bm[VPG], bl[VPG];
-#pragma unroll
-                    for (int pg = 0; pg < VPG; ++pg)
-#pragma unroll
-                        for (int jj = 0; jj < 8; ++jj) {
-                            const int k = 16 * s + 8 * hl + jj;
-                            const float z = fmaf(ay[pg], sA1[k], ax[pg] * sA0[k]) + sb0[k];
-                            float h0;
-                            if (fourier) {
-                                h0 = __builtin_amdgcn_cosf(turns_fourier(z)) * scale;
-                            } else {
-                                h0 = z > 0.f ? z : 0.f;
-                            }
-                            __bf16 a, b, c;
-                            split3(h0, a, b, c);
-                            bh[pg][jj] = a;
-                            bm[pg][jj] = b;
-                            bl[pg][jj] = c;
-                        }
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) {
-                        const __bf16* rowp = sWp + (size_t)(t * 32 + il) * RS + 16 * s + 8 * hl;
-                        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
-                        const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
-                        const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
-#pragma unroll
-                        for (int pg = 0; pg < VPG; ++pg) acc[pg][t] = mfma6(ah, am, al, bh[pg], bm[pg], bl[pg], acc[pg][t]);
-                    }
-                }
-#pragma unroll
-                for (int pg = 0; pg < VPG; ++pg) {
-                    float fpart = 0.f;
-                    uint64_t mk = 0;
-#pragma unroll
-                    for (int t = 0; t < NT; ++t)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int j = t * 32 + acc_row(r, hl);
-                            const float v = acc[pg][t][r] + sb[j];
-                            const bool on = v > 0.f;
-                            fpart = fmaf(sw[j], on ? v : 0.f, fpart);
-                            mk |= (uint64_t)on << (t * 16 + r);
-                        }
-                    const float fw = fpart + __shfl_xor(fpart, 32) + w.b_out;
-                    if (valid[pg]) {
-                        if (hl == 0) out.val[pi[pg] * out.sv] = fw;
-                        if (out.mask) {
-                            out.mask[(2 * hl) * out.mask_plane + pi[pg]] = (uint32_t)mk;
-                            out.mask[(2 * hl + 1) * out.mask_plane + pi[pg]] = (uint32_t)(mk >> 32);
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int pg = 0; pg < VPG; ++pg) {
-                ax[pg] = bx[pg];
-                ay[pg] = by[pg];
-                bx[pg] = cx[pg];
-                by[pg] = cy[pg];
-            }
-        }
-        return;
-    }
 
     // A block's tiles are tile0, tile0 + G, ...: each tile's inputs (point, the reuse source and, one tile later,
     // the source's trial point / value / ReLU pattern) are loaded ahead, so the dependent global round trips of a
-    // tile overlap the previous tile's MFMA work (one wave per SIMD: nothing else hides their latency)
+    // tile overlap the previous tile's MFMA work
     struct TileIn {
         float px, py;
         int src;
@@ -645,19 +568,18 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
         for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
 #pragma unroll 1
         for (int s = 0; s < NKB; ++s) {
+            // the lane's 8 consecutive k of this block: k = 16 s + 8 hl + jj
+            float a0[8], a1[8], c0[8];
+            const int k0 = 16 * s + 8 * hl;
+            lds8(sA0 + k0, a0);
+            lds8(sA1 + k0, a1);
+            lds8(sb0 + k0, c0);
             bf16x8 bh, bm, bl;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const int k = 16 * s + 8 * hl + jj;
-                const float z = fmaf(py, sA1[k], px * sA0[k]) + sb0[k];
-                float h0;
-                if (fourier) {
-                    h0 = __builtin_amdgcn_cosf(turns_fourier(z)) * scale;
-                } else {
-                    h0 = z > 0.f ? z : 0.f;
-                }
+                const float z = fmaf(py, a1[jj], px * a0[jj]) + c0[jj];
                 __bf16 a, b, c;
-                split3(h0, a, b, c);
+                split3(in_act<FOUR>(z, scale), a, b, c);
                 bh[jj] = a;
                 bm[jj] = b;
                 bl[jj] = c;
@@ -680,8 +602,10 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
             for (int r = 0; r < 16; ++r) {
                 const int j = t * 32 + acc_row(r, hl);
                 const float v = acc[t][r] + sb[j];
-                const bool on = v > 0.f;
-                fpart = fmaf(sw[j], on ? v : 0.f, fpart);
+                // on = v > 0 without a compare: the int image of a float is > 0 exactly for v > 0 (-0 and the
+                // negatives have the sign bit); clamp(., 0, 1) is one v_med3_i32, max(v, 0) one v_max_f32
+                const int on = min(max(__float_as_int(v), 0), 1);
+                fpart = fmaf(sw[j], fmaxf(v, 0.f), fpart);
                 mk |= (uint64_t)on << (t * 16 + r);
             }
         const float fw = fpart + __shfl_xor(fpart, 32) + w.b_out;
@@ -733,40 +657,49 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
             // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point); the
             // four rows of a register quad are consecutive k: one 16-byte read per input-layer vector
             float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+            const int zo = opaque_zero();
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int r4 = 0; r4 < 4; ++r4) {
-                    const int k0 = t * 32 + 8 * r4 + 4 * hl;
+                    const int k0 = t * 32 + 8 * r4 + 4 * hl + zo;
                     const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
                     const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
                     const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
+                    float4 Q0, Q1, Q2;  // A0^2, A0 A1, A1^2 (staged once per block)
+                    if constexpr (FOUR) {
+                        Q0 = *reinterpret_cast<const float4*>(sq + k0);
+                        Q1 = *reinterpret_cast<const float4*>(sq + H + k0);
+                        Q2 = *reinterpret_cast<const float4*>(sq + 2 * H + k0);
+                    }
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int r = 4 * r4 + rr;
                     const float ax = rr == 0 ? A0.x : rr == 1 ? A0.y : rr == 2 ? A0.z : A0.w;
                     const float ay = rr == 0 ? A1.x : rr == 1 ? A1.y : rr == 2 ? A1.z : A1.w;
                     const float bz = rr == 0 ? B0.x : rr == 1 ? B0.y : rr == 2 ? B0.z : B0.w;
-                    const float axx = ax * ax, axy = ax * ay, ayy = ay * ay;
                     const float z = fmaf(py, ay, px * ax) + bz;
                     const float d = g[t][r];
-                    float dz, c2;
-                    if (fourier) {  // the factor -scale is applied to the sums
+                    if constexpr (FOUR) {  // the factor -scale is applied to the sums
+                        const float qxx = rr == 0 ? Q0.x : rr == 1 ? Q0.y : rr == 2 ? Q0.z : Q0.w;
+                        const float qxy = rr == 0 ? Q1.x : rr == 1 ? Q1.y : rr == 2 ? Q1.z : Q1.w;
+                        const float qyy = rr == 0 ? Q2.x : rr == 1 ? Q2.y : rr == 2 ? Q2.z : Q2.w;
                         const float tz = turns_fourier(z);
-                        dz = d * __builtin_amdgcn_sinf(tz);
-                        c2 = d * __builtin_amdgcn_cosf(tz);
-                    } else {
-                        dz = z > 0.f ? d : 0.f;
-                        c2 = 0.f;
+                        const float dz = d * __builtin_amdgcn_sinf(tz);
+                        const float c2 = d * __builtin_amdgcn_cosf(tz);
+                        gx = fmaf(ax, dz, gx);
+                        gy = fmaf(ay, dz, gy);
+                        hxx = fmaf(qxx, c2, hxx);
+                        hxy = fmaf(qxy, c2, hxy);
+                        hyy = fmaf(qyy, c2, hyy);
+                    } else {  // ReLU input layer: piecewise linear, Hessian 0 a.e.
+                        const float dz = z > 0.f ? d : 0.f;
+                        gx = fmaf(ax, dz, gx);
+                        gy = fmaf(ay, dz, gy);
                     }
-                    gx = fmaf(ax, dz, gx);
-                    gy = fmaf(ay, dz, gy);
-                    hxx = fmaf(axx, c2, hxx);
-                    hxy = fmaf(axy, c2, hxy);
-                    hyy = fmaf(ayy, c2, hyy);
                 }
                 }
-            const float sg = fourier ? -scale : 1.f;
+            const float sg = FOUR ? -scale : 1.f;
             gx = sg * (gx + __shfl_xor(gx, 32));
             gy = sg * (gy + __shfl_xor(gy, 32));
             hxx = sg * (hxx + __shfl_xor(hxx, 32));
@@ -823,15 +756,20 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
         static const bool use_bf16 = !(getenv("NLOT_MLP") && strcmp(getenv("NLOT_MLP"), "f32") == 0);
         if (use_bf16 && w.Wp) {
             constexpr size_t lv = mlp_bf16_lds_bytes<H>();
-            static std::atomic<uint64_t> attr_v{0};
-            NLOT_HIP_CHECK(set_lds_attr_once(attr_v, (const void*)mlp_bf16<H, FULL>, (int)lv));
+            static std::atomic<uint64_t> attr_v{0}, attr_f{0};
+            NLOT_HIP_CHECK(set_lds_attr_once(attr_v, (const void*)mlp_bf16<H, FULL, false>, (int)lv));
+            NLOT_HIP_CHECK(set_lds_attr_once(attr_f, (const void*)mlp_bf16<H, FULL, true>, (int)lv));
             constexpr int NTB = bf16_threads(FULL);
             const int64_t tiles = (n * P_per + NTB / 2 - 1) / (NTB / 2);
             const int64_t cap = num_cus();
             const int grid = (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
             const MlpReuse ru = reuse ? *reuse : MlpReuse{};
-            hipLaunchKernelGGL((mlp_bf16<H, FULL>), dim3(grid), dim3(NTB), lv, stream, w, pts, n, n_dev, P_per, ld,
-                               lam, out, ru);
+            if (w.in_kind == NLOT_MLP_IN_FOURIER)
+                hipLaunchKernelGGL((mlp_bf16<H, FULL, true>), dim3(grid), dim3(NTB), lv, stream, w, pts, n, n_dev,
+                                   P_per, ld, lam, out, ru);
+            else
+                hipLaunchKernelGGL((mlp_bf16<H, FULL, false>), dim3(grid), dim3(NTB), lv, stream, w, pts, n, n_dev,
+                                   P_per, ld, lam, out, ru);
             NLOT_HIP_CHECK(hipGetLastError());
             return NLOT_OK;
         }
