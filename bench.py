@@ -68,11 +68,15 @@ def parse():
                          "8192 = 65536 over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="instances for the CPU baseline on all threads (0 = skip; default 256 metric / 32 stress)")
+                    help="instances for the CPU baseline on all threads (0 = skip; default 40 metric / 32 b6 / 16 stress)")
     ap.add_argument("--cpu-sample-1core", type=int, default=None,
-                    help="instances for the single-core CPU baseline (default 8 metric / 2 stress)")
+                    help="instances for the single-core CPU baseline (default 2; 1 stress)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the host's CPU share: min(affinity, cgroup cpu.max quota))")
+    ap.add_argument("--cpu-overlap", choices=["on", "off"], default="on",
+                    help="on (metric / b6, one rank): the CPU baseline runs on the host cores during the untimed warm-up "
+                         "(the GPU stays busy meanwhile) on one thread fewer than the host's share (the solver's launch "
+                         "thread keeps one); it is joined before the timed region starts.  off: after the timed region")
     ap.add_argument("--continuous", choices=["on", "off"], default="on",
                     help="on (metric / stress): the timed steps' batches flow through the solver with --batch slots "
                          "(continuous batching, NlotSolverOptions.max_active; all of them in one solve call), so one "
@@ -95,11 +99,14 @@ def batch_calls(steps, continuous, per_call=4):
     return G, [min(G, steps - i) for i in range(0, steps, G)]
 
 
-def timed_loop(step, steps, warmup, world, sync, device):
+def timed_loop(step, steps, warmup, world, sync, device, after_warmup=None):
     """W untimed warm-up steps, then EXACTLY `steps` timed steps bracketed by a barrier + device sync on
-    both sides; returns (per-step results, max-over-ranks elapsed seconds)."""
+    both sides; returns (per-step results, max-over-ranks elapsed seconds).  after_warmup: called between the two
+    (joins host work that overlapped the warm-up)."""
     for _ in range(warmup):
         step()
+    if after_warmup is not None:
+        after_warmup()
     if world > 1:
         dist.barrier()
     sync()
@@ -143,10 +150,10 @@ def main():
     stress, b6 = a.workload == "stress", a.workload == "b6"
     if a.batch is None:
         a.batch = 8192 if stress else 16384 if b6 else 32768
-    if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads
-        a.cpu_sample = 16 if stress else 32 if b6 else 48
+    if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads (metric: inside the warm-up)
+        a.cpu_sample = 16 if stress else 32 if b6 else 40
     if a.cpu_sample_1core is None:
-        a.cpu_sample_1core = 1 if stress else 2 if b6 else 3
+        a.cpu_sample_1core = 1 if stress else 2
     prob = STRESS_PROBLEM if stress else B6_PROBLEM if b6 else METRIC_PROBLEM
     if b6:
         wpath = os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")
@@ -247,7 +254,37 @@ def main():
         return step(a.warmup + sum(calls[:i]), g)
 
     warm_calls = 1 if (cont and a.warmup > 1) else a.warmup  # the W warm-up batches: one continuous call
-    results, elapsed = timed_loop(timed_call, len(calls), warm_calls, world, sync, dev)
+    # the CPU baseline (rank 0 of a one-rank run, not the stress estimate, which needs the GPU run's iteration counts)
+    # overlaps the warm-up: a host thread runs the oracle (ctypes releases the GIL) while the GPU warms up
+    cpu_box, cpu_thread = {}, None
+    cpu_here = rank == 0 and world == 1 and a.cpu_sample > 0
+    if cpu_here and not stress and a.cpu_overlap == "on" and warm_calls > 0:
+        import threading
+
+        share, _ = host_cpu_share()
+        th = a.cpu_threads or max(1, share - 1)
+        x0n, xgn = x0.cpu().numpy(), xg.cpu().numpy()
+
+        def _cpu():
+            print("[bench] CPU baseline (oracle), overlapping the warm-up ...", file=sys.stderr, flush=True)
+            try:
+                cpu_box["r"] = cpu_baseline(prob, w, x0n, xgn, a.cpu_sample, a.cpu_sample_1core, th, opt)
+                cpu_box["r"]["overlap"] = ("measured during the untimed GPU warm-up, on one thread fewer than the "
+                                           "host share (the solver's launch thread keeps one)")
+            except Exception as e:  # pragma: no cover
+                cpu_box["r"] = {"error": str(e)}
+
+        cpu_thread = threading.Thread(target=_cpu, daemon=True)
+        cpu_thread.start()
+
+    def join_cpu():
+        if cpu_thread is not None:
+            t = time.perf_counter()
+            cpu_thread.join()
+            print(f"[bench] CPU baseline joined ({time.perf_counter() - t:.1f} s after the warm-up)", file=sys.stderr,
+                  flush=True)
+
+    results, elapsed = timed_loop(timed_call, len(calls), warm_calls, world, sync, dev, after_warmup=join_cpu)
     set_timing(False)
     st_all = torch.cat([x["status"] for x in results]).long()
     it_all = torch.cat([x["iters"] for x in results]).double()
@@ -296,8 +333,8 @@ def main():
     v_avg_ms = agg["mlp_value_ms"] / n_v
     v_achieved = agg["mlp_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
 
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
+    cpu = cpu_box.get("r")
+    if cpu_here and cpu is None:
         print("[bench] CPU baseline (oracle) ...", file=sys.stderr, flush=True)
         if stress:  # per-iteration estimate (cpu_baseline docstring); iterations of ALL instances per solved one
             tot_it = sum(int(x["iters"].sum().item()) for x in results)

@@ -495,6 +495,108 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
     const int il = lane & 31, hl = lane >> 5;
     const float scale = w.scale;
     constexpr int TP = bf16_threads(FULL) / 2;  // points per block tile (32 per wave)
+    if constexpr (!FULL) {
+        // Value-only launches, software-pipelined inside the wave: the B fragment (input-layer activations, split)
+        // of k block s + 1 — or, in the last block, block 0 of the wave's NEXT tile — is computed between the MFMAs
+        // of block s (2 elements per 32x32 output tile), so a wave's VALU work issues into its own MFMA gaps
+        // instead of alternating with them.  Same arithmetic per point as the FULL forward below.
+        static_assert(8 % NT == 0, "two input-layer elements per output tile and k block");
+        constexpr int EPT = 8 / NT;
+        const int64_t G = gridDim.x;
+        auto point = [&](int64_t tile, float& x, float& y) {
+            const int64_t gi = g0 + tile * TP + wave * 32 + il;
+            x = y = 0.f;
+            if (gi < npts) {
+                const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
+                x = pts[2 * pi];
+                y = pts[2 * pi + 1];
+            }
+        };
+        float cx, cy, nx, ny;
+        point(blockIdx.x, cx, cy);
+        point(blockIdx.x + G, nx, ny);
+        bf16x8 bh, bm, bl;
+        {
+            float a0[8], a1[8], c0[8];
+            lds8(sA0 + 8 * hl, a0);
+            lds8(sA1 + 8 * hl, a1);
+            lds8(sb0 + 8 * hl, c0);
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                __bf16 a, b, c;
+                split3(in_act<FOUR>(fmaf(cy, a1[jj], cx * a0[jj]) + c0[jj], scale), a, b, c);
+                bh[jj] = a;
+                bm[jj] = b;
+                bl[jj] = c;
+            }
+        }
+        for (int64_t tile = blockIdx.x; g0 + tile * TP < npts; tile += G) {
+            float fx, fy;
+            point(tile + 2 * G, fx, fy);
+            f32x16 acc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll 1
+            for (int s = 0; s < NKB; ++s) {
+                const bool last = s == NKB - 1;
+                const int sn = last ? 0 : s + 1;
+                const float qx = last ? nx : cx, qy = last ? ny : cy;
+                float a0[8], a1[8], c0[8];
+                const int kn = 16 * sn + 8 * hl;
+                lds8(sA0 + kn, a0);
+                lds8(sA1 + kn, a1);
+                lds8(sb0 + kn, c0);
+                bf16x8 nh, nm, nl;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const __bf16* rowp = sWp + (size_t)(t * 32 + il) * RS + 16 * s + 8 * hl;
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
+                    const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
+                    acc[t] = mfma6(ah, am, al, bh, bm, bl, acc[t]);
+#pragma unroll
+                    for (int u = 0; u < EPT; ++u) {
+                        const int jj = t * EPT + u;
+                        __bf16 a, b, c;
+                        split3(in_act<FOUR>(fmaf(qy, a1[jj], qx * a0[jj]) + c0[jj], scale), a, b, c);
+                        nh[jj] = a;
+                        nm[jj] = b;
+                        nl[jj] = c;
+                    }
+                }
+                bh = nh;
+                bm = nm;
+                bl = nl;
+            }
+            float fpart = 0.f;
+            uint64_t mk = 0;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int j = t * 32 + acc_row(r, hl);
+                    const float v = acc[t][r] + sb[j];
+                    const int on = min(max(__float_as_int(v), 0), 1);
+                    fpart = fmaf(sw[j], fmaxf(v, 0.f), fpart);
+                    mk |= (uint64_t)on << (t * 16 + r);
+                }
+            const float fw = fpart + __shfl_xor(fpart, 32) + w.b_out;
+            const int64_t gi = g0 + tile * TP + wave * 32 + il;
+            if (gi < npts) {
+                const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
+                if (hl == 0) out.val[pi * out.sv] = fw;
+                if (out.mask) {
+                    out.mask[(2 * hl) * out.mask_plane + pi] = (uint32_t)mk;
+                    out.mask[(2 * hl + 1) * out.mask_plane + pi] = (uint32_t)(mk >> 32);
+                }
+            }
+            cx = nx;
+            cy = ny;
+            nx = fx;
+            ny = fy;
+        }
+        return;
+    }
 
     // A block's tiles are tile0, tile0 + G, ...: each tile's inputs (point, the reuse source and, one tile later,
     // the source's trial point / value / ReLU pattern) are loaded ahead, so the dependent global round trips of a
@@ -624,62 +726,51 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
             }
         } else {
             // ---------------- reverse sweep: G = W^T e, e = lam * w_out .* mask ----------------
+            // e is split once into the B fragments of all 2 NT k-steps (blk = 2 tj + sl: accumulator registers
+            // 8 sl .. 8 sl + 7 of output tile tj, permuted k order; 3 NT x 2 x 4 VGPRs); then output tile tk of
+            // G = W^T e accumulates over the k-steps while the contraction of tile tk - 1 (whose accumulator is
+            // complete) runs between its MFMAs: 2 of its 16 rows per k-step
             const float lm = lam ? (valid ? lam[pi] : 0.f) : 1.f;
-            f32x16 g[NT];
+            constexpr int NB = 2 * NT;
+            bf16x8 Bh[NB], Bm[NB], Bl[NB];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) g[t] = f32x16{};
-#pragma unroll 1
-            for (int tj = 0; tj < NT; ++tj)
-#pragma unroll 1
-                for (int sl = 0; sl < 2; ++sl) {
-                    // e split straight into the B fragment of k-step (tj, sl): element jj = accumulator
-                    // register 8 sl + jj (permuted k order)
-                    bf16x8 bh, bm, bl;
+            for (int blk = 0; blk < NB; ++blk) {
+                const int tj = blk >> 1, sl = blk & 1;
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) {
-                        const int r = 8 * sl + jj;
-                        const float e = ((mask >> (tj * 16 + r)) & 1) ? lm * sw[tj * 32 + acc_row(r, hl)] : 0.f;
-                        __bf16 a, b, c;
-                        split3(e, a, b, c);
-                        bh[jj] = a;
-                        bm[jj] = b;
-                        bl[jj] = c;
-                    }
-                    const int jbase = 32 * tj + 16 * sl;
-#pragma unroll
-                    for (int tk = 0; tk < NT; ++tk) {
-                        const bf16x8 ah = wt_frag<RS>(sWp, jbase, 32 * tk, lane);
-                        const bf16x8 am = wt_frag<RS>(sWp + (size_t)H * RS, jbase, 32 * tk, lane);
-                        const bf16x8 al = wt_frag<RS>(sWp + (size_t)2 * H * RS, jbase, 32 * tk, lane);
-                        g[tk] = mfma6(ah, am, al, bh, bm, bl, g[tk]);
-                    }
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int r = 8 * sl + jj;
+                    const float e = ((mask >> (tj * 16 + r)) & 1) ? lm * sw[tj * 32 + acc_row(r, hl)] : 0.f;
+                    __bf16 a, b, c;
+                    split3(e, a, b, c);
+                    Bh[blk][jj] = a;
+                    Bm[blk][jj] = b;
+                    Bl[blk][jj] = c;
                 }
-            // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point); the
-            // four rows of a register quad are consecutive k: one 16-byte read per input-layer vector
+            }
+            // g = df/dh0 (x lam): contract with the input layer's derivatives (lane: k rows, point); the four rows
+            // of a register quad are consecutive k: one 16-byte read per input-layer vector
             float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
             const int zo = opaque_zero();
+            auto contract2 = [&](const f32x16& gp, int tp, int r0) {  // rows r0, r0 + 1 of output tile tp
+                const int r4 = r0 >> 2, rr0 = r0 & 3;
+                const int k0 = tp * 32 + 8 * r4 + 4 * hl + zo;
+                const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
+                const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
+                const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
+                float4 Q0, Q1, Q2;  // A0^2, A0 A1, A1^2 (staged once per block)
+                if constexpr (FOUR) {
+                    Q0 = *reinterpret_cast<const float4*>(sq + k0);
+                    Q1 = *reinterpret_cast<const float4*>(sq + H + k0);
+                    Q2 = *reinterpret_cast<const float4*>(sq + 2 * H + k0);
+                }
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int r4 = 0; r4 < 4; ++r4) {
-                    const int k0 = t * 32 + 8 * r4 + 4 * hl + zo;
-                    const float4 A0 = *reinterpret_cast<const float4*>(sA0 + k0);
-                    const float4 A1 = *reinterpret_cast<const float4*>(sA1 + k0);
-                    const float4 B0 = *reinterpret_cast<const float4*>(sb0 + k0);
-                    float4 Q0, Q1, Q2;  // A0^2, A0 A1, A1^2 (staged once per block)
-                    if constexpr (FOUR) {
-                        Q0 = *reinterpret_cast<const float4*>(sq + k0);
-                        Q1 = *reinterpret_cast<const float4*>(sq + H + k0);
-                        Q2 = *reinterpret_cast<const float4*>(sq + 2 * H + k0);
-                    }
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int r = 4 * r4 + rr;
+                for (int u = 0; u < 2; ++u) {
+                    const int rr = rr0 + u;
                     const float ax = rr == 0 ? A0.x : rr == 1 ? A0.y : rr == 2 ? A0.z : A0.w;
                     const float ay = rr == 0 ? A1.x : rr == 1 ? A1.y : rr == 2 ? A1.z : A1.w;
                     const float bz = rr == 0 ? B0.x : rr == 1 ? B0.y : rr == 2 ? B0.z : B0.w;
                     const float z = fmaf(py, ay, px * ax) + bz;
-                    const float d = g[t][r];
+                    const float d = gp[r0 + u];
                     if constexpr (FOUR) {  // the factor -scale is applied to the sums
                         const float qxx = rr == 0 ? Q0.x : rr == 1 ? Q0.y : rr == 2 ? Q0.z : Q0.w;
                         const float qxy = rr == 0 ? Q1.x : rr == 1 ? Q1.y : rr == 2 ? Q1.z : Q1.w;
@@ -698,7 +789,25 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                         gy = fmaf(ay, dz, gy);
                     }
                 }
+            };
+            static_assert(NB == 8, "2 contraction rows per k-step cover a 16-row output tile");
+            f32x16 gprev = f32x16{};
+#pragma unroll
+            for (int tk = 0; tk < NT; ++tk) {
+                f32x16 g = f32x16{};
+#pragma unroll
+                for (int blk = 0; blk < NB; ++blk) {
+                    const int jbase = 16 * blk;  // 32 tj + 16 sl
+                    const bf16x8 ah = wt_frag<RS>(sWp, jbase, 32 * tk, lane);
+                    const bf16x8 am = wt_frag<RS>(sWp + (size_t)H * RS, jbase, 32 * tk, lane);
+                    const bf16x8 al = wt_frag<RS>(sWp + (size_t)2 * H * RS, jbase, 32 * tk, lane);
+                    g = mfma6(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g);
+                    if (tk > 0) contract2(gprev, tk - 1, 2 * blk);
                 }
+                gprev = g;
+            }
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += 2) contract2(gprev, NT - 1, r0);
             const float sg = FOUR ? -scale : 1.f;
             gx = sg * (gx + __shfl_xor(gx, 32));
             gy = sg * (gy + __shfl_xor(gy, 32));
