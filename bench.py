@@ -68,9 +68,9 @@ def parse():
                          "8192 = 65536 over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="instances for the CPU baseline on all threads (0 = skip; default 40 metric / 32 b6 / 16 stress)")
+                    help="instances for the CPU baseline on all threads (0 = skip; default 32; 16 stress)")
     ap.add_argument("--cpu-sample-1core", type=int, default=None,
-                    help="instances for the single-core CPU baseline (default 2; 1 stress)")
+                    help="at least this many instances for the single-core CPU baseline, one at a time until ~8 s (default 2; 1 stress)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the host's CPU share: min(affinity, cgroup cpu.max quota))")
     ap.add_argument("--cpu-overlap", choices=["on", "off"], default="on",
@@ -151,7 +151,7 @@ def main():
     if a.batch is None:
         a.batch = 8192 if stress else 16384 if b6 else 32768
     if a.cpu_sample is None:  # about 10-30 s of oracle work on the box's 16 threads (metric: inside the warm-up)
-        a.cpu_sample = 16 if stress else 32 if b6 else 40
+        a.cpu_sample = 16 if stress else 32
     if a.cpu_sample_1core is None:
         a.cpu_sample_1core = 1 if stress else 2
     prob = STRESS_PROBLEM if stress else B6_PROBLEM if b6 else METRIC_PROBLEM
@@ -555,7 +555,21 @@ def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu
                          f"{per_it * 1e3:.1f} ms per instance-iteration; value = 1 / (that x the GPU run's "
                          f"{gpu_iters_per_solved:.1f} iterations per solved instance)"}
     if n_one > 0:
-        ns1, dt1, sc1, it1 = run(n_one, 1)
+        # single core: instances one at a time on one thread until about 8 s of work (a fixed count of 2-3 instances
+        # drew anything from 17 to 2,000 instance-iterations), at least n_one of them
+        ns1 = dt1 = it1 = 0
+        sc1 = [0] * 7
+        n1 = 0
+        while n1 < len(x0) and (n1 < n_one or dt1 < 8.0):
+            t = time.perf_counter()
+            r1 = O.solve_batch(prob, x0[n1:n1 + 1], xg[n1:n1 + 1], hm, opt=run_opt, threads=1)
+            dt1 += time.perf_counter() - t
+            ns1 += int(r1["status"][0] == 0)
+            sc1[int(r1["status"][0])] += 1
+            it1 += int(r1["iters"][0])
+            n1 += 1
+        n_one = n1
+        print(f"[bench] cpu baseline: {n1} instances on 1 thread, {dt1:.1f} s", file=sys.stderr, flush=True)
         ips1 = it1 / dt1
         out["parallel_efficiency"] = ips / (threads * ips1)
         out["efficiency_note"] = (f"instance-iterations/s: {ips:.1f} on {threads} threads vs {ips1:.2f} on 1 thread")

@@ -216,9 +216,21 @@ static void oracle_mlp_point_smooth(const NlotMlpDesc* m, float px, float py, fl
     for (int c = 1; c < 6; ++c) out[c] = want ? lam * o[c] : 0.f;
 }
 
+/* NLOT_ORACLE_MLP_REV=1 (test infrastructure, tests/outcomes.py): every fp32 dot product of the ReLU net (hidden
+ * layers, output layer, reverse sweep, input-layer contraction) accumulates in the reverse index order.  The result
+ * differs from the default only by fp32 rounding: the same kind of difference the GPU's split-bf16 MFMA sums make, so
+ * a solve whose outcome changes under it is not reproducible at the GPU's arithmetic.  Read per call (toggled
+ * between whole batches by the Python side). */
+static int mlp_rev(void) {
+    const char* e = getenv("NLOT_ORACLE_MLP_REV");
+    return e && e[0] == '1';
+}
+
 void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
     enum { HM = 256, LM = 8 };
     const int H = m->hidden;
+    const int rv = mlp_rev();
+#define RIX(i) (rv ? H - 1 - (i) : (i))
     if (m->act != NLOT_ACT_RELU) {
         oracle_mlp_point_smooth(m, px, py, lam, want, out);
         return;
@@ -242,7 +254,10 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
         const float* b = m->b + (size_t)l * H;
         for (int j = 0; j < H; ++j) {
             float a = 0.f;
-            for (int k = 0; k < H; ++k) a = fmaf(W[(size_t)j * H + k], h[k], a);
+            for (int kq = 0; kq < H; ++kq) {
+                const int k = RIX(kq);
+                a = fmaf(W[(size_t)j * H + k], h[k], a);
+            }
             a += b[j];
             mask[l + 1][j] = a > 0.f;
             hn[j] = a > 0.f ? a : 0.f;
@@ -250,7 +265,7 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
         memcpy(h, hn, sizeof(float) * H);
     }
     float f = 0.f;
-    for (int j = 0; j < H; ++j) f = fmaf(m->w_out[j], h[j], f);
+    for (int jq = 0; jq < H; ++jq) f = fmaf(m->w_out[RIX(jq)], h[RIX(jq)], f);
     out[0] = f + m->b_out;
     out[1] = out[2] = out[3] = out[4] = out[5] = 0.f;
     if (!want) return;
@@ -261,12 +276,15 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
         const float* W = m->W + (size_t)l * H * H;
         for (int j = 0; j < H; ++j) d[j] = mask[l + 1][j] ? d[j] : 0.f;
         for (int k = 0; k < H; ++k) dn[k] = 0.f;
-        for (int j = 0; j < H; ++j)
+        for (int jq = 0; jq < H; ++jq) {
+            const int j = RIX(jq);
             for (int k = 0; k < H; ++k) dn[k] = fmaf(W[(size_t)j * H + k], d[j], dn[k]);
+        }
         memcpy(d, dn, sizeof(float) * H);
     }
     float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
-    for (int k = 0; k < H; ++k) {
+    for (int kq = 0; kq < H; ++kq) {
+        const int k = RIX(kq);
         float ax = m->A[k], ay = m->A[H + k], dz, c2;
         if (m->in_kind == NLOT_MLP_IN_FOURIER) {
             dz = d[k] * (-m->fourier_scale * sinf(z0[k]));
@@ -286,6 +304,7 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
     out[3] = hxx;
     out[4] = hxy;
     out[5] = hyy;
+#undef RIX
 }
 
 /* Batched form of the nn_sdf family (same argument meaning as nlot_sdf_mlp_eval, host buffers). */

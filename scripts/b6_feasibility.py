@@ -15,7 +15,10 @@ feasible when the maximum violation max(|c_eq|, max(0, -c_in)) it reaches is <= 
 instance.  The instances are tests/golden/oracle_outcomes.npz's b6 set when present (their RRT guesses are stored
 there), else 12 seeded ones built here.
 
-    python scripts/b6_feasibility.py [--n 12] [--out profiles/r04/b6_feasibility.json]
+    [B6_SOFTPLUS=1] python scripts/b6_feasibility.py [--n 12] [--out profiles/r04/b6_feasibility.json]
+
+B6_SOFTPLUS=1 also runs the oracle's IPOPT restatement with the net's ReLUs replaced by softplus(beta = 1000) (the
+kink diagnostic of DESIGN.md §4b) from the same RRT guess and reports its status.
 
 CPU only; test infrastructure (uses the oracle)."""
 import argparse
@@ -67,7 +70,17 @@ def phase1(args):
     t = time.time()
     r = least_squares(res, z0, jac=jac, bounds=(lo, hi), method="trf", xtol=1e-15, ftol=1e-15, gtol=1e-15,
                       max_nfev=3000)
-    out = {"instance": i, "violation_at_rrt_guess": viol(z0), "min_violation_reached": viol(r.x),
+    smooth = None
+    if os.environ.get("B6_SOFTPLUS"):  # the same restatement with the net's ReLUs smoothed (oracle-only diagnostic)
+        from nlotrajectories_amd import _abi
+
+        os.environ["NLOT_ORACLE_SOFTPLUS_BETA"] = "1000"
+        hs = O.HostMlp(MlpWeights.load(W6))
+        hs.desc.act = 90  # ORACLE_ACT_SOFTPLUS
+        rs = O.solve_one(B6_PROBLEM, np.asarray(x0, float), np.asarray(xg, float), hs, opt=_abi.default_options(),
+                         X_init=Xi)
+        smooth = {"status": _abi.STATUS_NAMES[rs["status"]], "iters": rs["iters"], "cost": rs["cost"]}
+    out = {"instance": i, "softplus_1000_restatement": smooth, "violation_at_rrt_guess": viol(z0), "min_violation_reached": viol(r.x),
            "equality_violation": float(np.abs(r.fun[:ne]).max()), "corner_sdf_violation": float(np.abs(r.fun[ne:]).max()),
            "feasible_1e-6": bool(viol(r.x) <= 1e-6), "nfev": int(r.nfev), "status": int(r.status),
            "message": r.message, "seconds": time.time() - t, "oracle_status": oracle_status}
@@ -103,6 +116,7 @@ def main():
     doc = {"generator": "scripts/b6_feasibility.py", "instances_from": src, "n": n,
            "method": "scipy least_squares trf on [c_eq; min(0, c_in)] with the control bounds, from the RRT guess",
            "feasible (violation <= 1e-6)": len(feas),
+           "softplus_1000_solved": sum(1 for r in rows if (r["softplus_1000_restatement"] or {}).get("status") == "solved"),
            "max violation reached (median)": float(np.median([r["min_violation_reached"] for r in rows])),
            "instances": rows}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

@@ -4,7 +4,8 @@
     python tests/golden/make_oracle_outcomes.py [--threads 8]   ->  tests/golden/oracle_outcomes.npz
 
 For each case it stores the instances (x0, xg, and the initial guesses where the case has its own) and the CPU
-oracle's status / final cost / iterations at x0 and at x0 +- 1e-13 (tests/outcomes.py), with IPOPT's settings
+oracle's status / final cost / iterations under tests/outcomes.PERTURBATIONS (x0, x0 +- 1e-13 e_x, x0 +- 1e-13 e_y, and
+the net summed in reverse order), with IPOPT's settings
 (default_options: max_iter 1000, tol 1e-4, adaptive mu, restoration on):
 
   metric: 128 seeded instances of the headline workload (unicycle_2nd, b3 body, N = 50, artefact FourierMLP; the
@@ -83,20 +84,24 @@ def main():
         hm6 = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")))
         from concurrent.futures import ThreadPoolExecutor
 
-        def one(args):  # the three perturbations of one instance (ctypes releases the GIL)
-            i, d = args
+        from outcomes import PERTURBATIONS, mlp_order
+
+        def one(args):  # one perturbation of one instance (ctypes releases the GIL)
+            i, (c, d, _) = args
             x = X0[i].copy()
-            x[0] += d
+            x[c] += d
             r = O.solve_one(B6_PROBLEM, x, XG[i], hm6, opt=opt, X_init=Xi[i])
             return r["status"], r["cost"], r["iters"]
 
-        jobs = [(i, d) for d in (0.0, 1e-13, -1e-13) for i in range(len(X0))]
+        res = []
         with ThreadPoolExecutor(a.threads) as ex:
-            res = list(ex.map(one, jobs))
-        n = len(X0)
-        out = {"status": np.array([r[0] for r in res], np.int32).reshape(3, n),
-               "cost": np.array([r[1] for r in res], float).reshape(3, n),
-               "iters": np.array([r[2] for r in res], np.int32).reshape(3, n)}
+            for pd in PERTURBATIONS:  # one batch per perturbation: the net's summation order is process-wide
+                with mlp_order(pd[2]):
+                    res += list(ex.map(one, [(i, pd) for i in range(len(X0))]))
+        n, m = len(X0), len(PERTURBATIONS)
+        out = {"status": np.array([r[0] for r in res], np.int32).reshape(m, n),
+               "cost": np.array([r[1] for r in res], float).reshape(m, n),
+               "iters": np.array([r[2] for r in res], np.int32).reshape(m, n)}
         data.update({"b6_x0": X0, "b6_xg": XG, "b6_xinit": Xi, **{f"b6_{k}": v for k, v in out.items()}})
         print(f"b6: {time.time() - t:.0f} s, statuses {np.bincount(out['status'][0], minlength=7).tolist()}",
               flush=True)

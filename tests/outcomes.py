@@ -3,45 +3,81 @@
 Under IPOPT's settings many instances are chaotic: a 1e-13 change of the start changes the oracle's own status or
 final cost (ReLU kinks, discrete filter / watchdog / mode decisions).  A batch is therefore split:
 
-  * reproducible: the oracle at x0, x0 + 1e-13 e_x and x0 - 1e-13 e_x ends with the same status and final costs
-    within 1e-8 relative.  The GPU must give the identical status and a final cost within 1e-4 relative
-    (BASELINE.json north_star) on 100 % of them;
+  * reproducible: the oracle at x0, at the four starts x0 +- 1e-13 e_x, x0 +- 1e-13 e_y, and at x0 with every fp32
+    dot product of the SDF net summed in reverse order (NLOT_ORACLE_MLP_REV, oracle/nlot_oracle.c: a rounding-level
+    change of the net's outputs, the kind the GPU's split-bf16 MFMA sums make) ends with the same status and, if
+    solved, final costs within 1e-8 relative (a failed run's final cost is where it stopped, not compared).  Perturbing one start coordinate only missed instances that flip under the other (b2
+    instances 20 and 34 of the seeded batch); start perturbations alone missed b6 instances that flip under the net's
+    rounding (5, 14, 18, 19 of the fixture set).  The GPU must give the identical status, and on the solved ones a final cost
+    within 1e-4 relative (BASELINE.json north_star), on 100 % of them;
   * chaotic: the rest.  There the bar is the oracle's own spread: status agreement with the unperturbed oracle at
     least as high as the perturbed oracles' (less two instances of sampling slack), and jointly solved final costs
     within 3x the oracle's own run-to-run envelope (quartile and maximum) or 1e-4.
 
 Test infrastructure only (imports nothing from the product package)."""
+import contextlib
+import os
+
 import numpy as np
 
 PERTURB = 1e-13
+# (start coordinate, offset, net summed in reverse order)
+PERTURBATIONS = ((0, 0.0, False), (0, PERTURB, False), (0, -PERTURB, False), (1, PERTURB, False),
+                 (1, -PERTURB, False), (0, 0.0, True))
 COST_REPRO = 1e-8
 
 
+@contextlib.contextmanager
+def mlp_order(rev):
+    """The oracle's net summation order for the runs inside (process-wide: run batches, not instances, under it)."""
+    old = os.environ.get("NLOT_ORACLE_MLP_REV")
+    if rev:
+        os.environ["NLOT_ORACLE_MLP_REV"] = "1"
+    else:
+        os.environ.pop("NLOT_ORACLE_MLP_REV", None)
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("NLOT_ORACLE_MLP_REV", None)
+        else:
+            os.environ["NLOT_ORACLE_MLP_REV"] = old
+
+
 def oracle_outcomes(O, prob, X0, XG, hm=None, opt=None, X_init=None, threads=16):
-    """Oracle status / cost / iterations at x0 and at x0 +- 1e-13 (x coordinate): arrays [3, B]."""
+    """Oracle status / cost / iterations under each of PERTURBATIONS: arrays [6, B].  Without a net (hm None) the
+    reverse-order run is the unperturbed run and is copied from it."""
     out = {"status": [], "cost": [], "iters": []}
-    for d in (0.0, PERTURB, -PERTURB):
+    for coord, d, rev in PERTURBATIONS:
+        if rev and hm is None:
+            for k in out:
+                out[k].append(out[k][0].copy())
+            continue
         x = np.array(X0, float, copy=True)
-        x[:, 0] += d
-        if X_init is None:
-            r = O.solve_batch(prob, x, XG, hm, opt=opt, threads=threads)
-            st, c, it = r["status"], r["cost"], r["iters"]
-        else:  # per-instance initial guesses
-            rs = [O.solve_one(prob, x[i], XG[i], hm, opt=opt, X_init=X_init[i]) for i in range(len(x))]
-            st = np.array([r["status"] for r in rs])
-            c = np.array([r["cost"] for r in rs])
-            it = np.array([r["iters"] for r in rs])
+        x[:, coord] += d
+        with mlp_order(rev):
+            if X_init is None:
+                r = O.solve_batch(prob, x, XG, hm, opt=opt, threads=threads)
+                st, cost, it = r["status"], r["cost"], r["iters"]
+            else:  # per-instance initial guesses
+                rs = [O.solve_one(prob, x[i], XG[i], hm, opt=opt, X_init=X_init[i]) for i in range(len(x))]
+                st = np.array([r["status"] for r in rs])
+                cost = np.array([r["cost"] for r in rs])
+                it = np.array([r["iters"] for r in rs])
         out["status"].append(np.asarray(st, np.int32))
-        out["cost"].append(np.asarray(c, float))
+        out["cost"].append(np.asarray(cost, float))
         out["iters"].append(np.asarray(it, np.int32))
     return {k: np.stack(v) for k, v in out.items()}
 
 
 def reproducible(out):
+    """Same status under every perturbation and, for solved instances, final costs within COST_REPRO.  The final
+    cost of a failed run (max_iter, restoration failed) is wherever the iteration stopped, not an optimum: it is not
+    compared."""
     st, c = out["status"], out["cost"]
     same = (st == st[0]).all(0)
     rel = np.abs(c - c[0]).max(0) / np.maximum(np.abs(c[0]), 1e-300)
-    return same & (rel <= COST_REPRO)
+    return same & ((st[0] != 0) | (rel <= COST_REPRO))
 
 
 def check_outcome_parity(label, sg, cg, out, min_reproducible=0):
@@ -53,19 +89,20 @@ def check_outcome_parity(label, sg, cg, out, min_reproducible=0):
     C = ~R
     rel = np.abs(cg - co) / np.maximum(np.abs(co), 1e-300)
     bad_status = R & (sg != so)
-    bad_cost = R & (rel > 1e-4)
+    bad_cost = R & (so == 0) & (rel > 1e-4)
     info = {"n": len(sg), "reproducible": int(R.sum()), "chaotic": int(C.sum()),
             "repro_status_mismatch": int(bad_status.sum()), "repro_cost_gt_1e-4": int(bad_cost.sum()),
-            "repro_max_rel_cost": float(rel[R].max()) if R.any() else 0.0,
+            "repro_max_rel_cost": float(rel[R & (so == 0)].max()) if (R & (so == 0)).any() else 0.0,
             "repro_status_counts": np.bincount(so[R], minlength=7).tolist()}
     if C.any():
         gpu_agree = float((sg[C] == so[C]).mean())
-        self_agree = float(min((out["status"][k][C] == so[C]).mean() for k in (1, 2)))
+        nrun = out["status"].shape[0]
+        self_agree = float(min((out["status"][k][C] == so[C]).mean() for k in range(1, nrun)))
         info.update(chaotic_gpu_status_agree=gpu_agree, chaotic_oracle_self_agree=self_agree)
         both = C & (sg == 0) & (so == 0)
         if both.any():
             env = np.concatenate([np.abs(out["cost"][k] - co)[both & (out["status"][k] == 0)] /
-                                  np.abs(co[both & (out["status"][k] == 0)]) for k in (1, 2)])
+                                  np.abs(co[both & (out["status"][k] == 0)]) for k in range(1, nrun)])
             q_self = float(np.quantile(env, 0.75)) if len(env) else 0.0
             m_self = float(env.max()) if len(env) else 0.0
             info.update(chaotic_joint_solved=int(both.sum()), chaotic_gpu_rel_q75=float(np.quantile(rel[both], 0.75)),

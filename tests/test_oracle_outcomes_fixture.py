@@ -1,7 +1,7 @@
 """tests/golden/oracle_outcomes.npz still describes this oracle (CPU): the GPU parity tests compare against its stored
 oracle outcomes (tests/outcomes.py), so a change of the oracle's arithmetic must regenerate it
-(tests/golden/make_oracle_outcomes.py).  Re-runs the fixture's quickest instances (fewest iterations) at x0 and
-x0 + 1e-13 and asks for bitwise the same status, iterations and final cost."""
+(tests/golden/make_oracle_outcomes.py).  Re-runs the fixture's quickest instances (fewest iterations) at x0,
+two perturbed starts and the reverse-order net and asks for bitwise the same status, iterations and final cost."""
 import os
 
 import numpy as np
@@ -16,8 +16,8 @@ def _fixture():
 def test_fixture_layout():
     f = _fixture()
     for case, n in (("metric", 128), ("b6", 24)):
-        assert f[f"{case}_x0"].shape[0] == n and f[f"{case}_status"].shape == (3, n)
-        assert f[f"{case}_cost"].shape == (3, n) and f[f"{case}_iters"].shape == (3, n)
+        assert f[f"{case}_x0"].shape[0] == n and f[f"{case}_status"].shape == (6, n)
+        assert f[f"{case}_cost"].shape == (6, n) and f[f"{case}_iters"].shape == (6, n)
     assert f["b6_xinit"].shape == (24, 101, 7)
     # the split has both groups on the headline workload (tests/outcomes.py)
     import sys
@@ -40,11 +40,18 @@ def test_fixture_matches_oracle():
     opt = _abi.default_options()
     hm = O.HostMlp(MlpWeights.artefact())
     its = f["metric_iters"][0]
+    import sys
+
+    sys.path.insert(0, HERE)
+    from outcomes import PERTURBATIONS, mlp_order
+
     for i in np.argsort(its, kind="stable")[:4]:
-        for r, d in ((0, 0.0), (1, 1e-13)):
+        for r in (0, 1, 3, 5):
+            coord, d, rev = PERTURBATIONS[r]
             x0 = f["metric_x0"][i].copy()
-            x0[0] += d
-            res = O.solve_one(METRIC_PROBLEM, x0, f["metric_xg"][i], hm, opt=opt)
+            x0[coord] += d
+            with mlp_order(rev):
+                res = O.solve_one(METRIC_PROBLEM, x0, f["metric_xg"][i], hm, opt=opt)
             assert res["status"] == f["metric_status"][r, i] and res["iters"] == f["metric_iters"][r, i], (i, r)
             assert res["cost"] == f["metric_cost"][r, i], (i, r, res["cost"], f["metric_cost"][r, i])
     hm6 = O.HostMlp(MlpWeights.load(os.path.join(os.path.dirname(HERE), "nlotrajectories_amd", "data",

@@ -73,7 +73,7 @@ def _fixture():
 def test_batch_b2_analytic_matches_oracle(strategy):
     """64 seeded b2 instances (analytic SDF).  Monotone mu at tol 1e-4; adaptive mu at tol 1e-8.  Solve-level
     parity split by the oracle's own reproducibility (tests/outcomes.py): on the instances whose oracle outcome is
-    unchanged by +-1e-13 start perturbations the GPU gives the same status and a final cost within 1e-4 on 100 %;
+    unchanged by +-1e-13 perturbations of the start's x and y the GPU gives the same status and a final cost within 1e-4 on 100 %;
     on the rest, agreement at least as good as the oracle's with itself."""
     O = _oracle()
     from outcomes import check_outcome_parity, oracle_outcomes
@@ -90,7 +90,9 @@ def test_batch_b2_analytic_matches_oracle(strategy):
     rg = solve_batch(p, x0, xg, options=opt)
     out = oracle_outcomes(O, p, x0, xg, opt=opt)
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
-    info = check_outcome_parity(f"b2 {strategy}", sg, cg, out, min_reproducible=16)
+    # reproducible instances (5 oracle runs, tests/outcomes.py): 15 of 64 under adaptive mu at tol 1e-8, 4 under
+    # monotone mu at tol 1e-4 (its tol 1e-4 termination point moves the final cost by more than 1e-8)
+    info = check_outcome_parity(f"b2 {strategy}", sg, cg, out, min_reproducible=8 if strategy == "adaptive" else 2)
     assert ((sg == 0) & (out["status"][0] == 0)).sum() >= 0.5 * len(x0), info
 
 
@@ -113,7 +115,7 @@ def test_batch_learned_sdf_matches_oracle(artefact):
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
     print("metric GPU status counts", np.bincount(sg, minlength=7).tolist(), "oracle",
           np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
-    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=32)
+    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=48)
 
 
 def test_safeguards_iterate_parity(artefact):
