@@ -410,6 +410,43 @@ __device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int
     return h;
 }
 
+// Inequality values only at a knot (the line search's trial points, MLP values of the trial list tval): d[j] of
+// knot_eval below with the same arithmetic, without the derivative machinery in the kernels that only need values
+__device__ __forceinline__ void knot_values(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
+                                            const double* xk, double* d, const float* tval) {
+    const double x = xk[0], y = xk[1];
+    if (p.shape == NLOT_SHAPE_DOT) {
+        d[0] = corner_sdf(p, ws, rank, k, x, y, tval).v;
+        return;
+    }
+    double sn, cs;
+    sincos(xk[2], &sn, &cs);
+    double phi[MMAX];
+#pragma unroll
+    for (int i = 0; i < MMAX; ++i) {
+        if (i >= dm.nb) break;
+        const double bx = p.body[i][0], by = p.body[i][1];
+        const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
+        phi[i] = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, tval).v;
+    }
+    if (p.use_slack) {  // soft_min over corners (not max-shifted, as utils.py:30-31)
+        const double al = p.softmin_alpha;
+        double sum = 0;
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i) {
+            if (i >= dm.nb) break;
+            sum += exp(-al * phi[i]);
+        }
+        d[0] = -log(sum) / al;
+    } else {
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i) {
+            if (i >= dm.nb) break;
+            d[i] = phi[i];
+        }
+    }
+}
+
 // Inequality functions at a knot (geometry.py:63-67, 107-117; utils.py:18-33): values d[j]
 // (slack excluded), pose gradients g[j][3], and Hw = sum_j w[j] d2 d_j / dpose2 (if w != null).
 __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
@@ -428,72 +465,75 @@ __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, 
     }
     double sn, cs;
     sincos(xk[2], &sn, &cs);
-    double phi[MMAX], gp[MMAX][3], Hp[MMAX][6];  // Hp: xx xy xt yy yt tt
-#pragma unroll
-    for (int i = 0; i < MMAX; ++i) {
-        if (i >= dm.nb) break;
+    // corner i's pose gradient gp[3] and Hessian Hp[6] (xx xy xt yy yt tt) of its SDF value, computed where they are
+    // used (one corner at a time: holding all corners' 36 doubles pushed k_iter_a over its register budget)
+    auto corner = [&](int i, double* phi, double* gp, double* Hp) {
         const double bx = p.body[i][0], by = p.body[i][1];
         const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
         const double ex = -(cy - y), ey = cx - x;                            // d c / d theta
         HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, tval);
-        phi[i] = f.v;
-        gp[i][0] = f.gx;
-        gp[i][1] = f.gy;
-        gp[i][2] = f.gx * ex + f.gy * ey;
-        Hp[i][0] = f.hxx;
-        Hp[i][1] = f.hxy;
-        Hp[i][2] = f.hxx * ex + f.hxy * ey;
-        Hp[i][3] = f.hyy;
-        Hp[i][4] = f.hxy * ex + f.hyy * ey;
-        Hp[i][5] = ex * (f.hxx * ex + f.hxy * ey) + ey * (f.hxy * ex + f.hyy * ey) - f.gx * (cx - x) - f.gy * (cy - y);
-    }
+        *phi = f.v;
+        if (!gp) return;
+        gp[0] = f.gx;
+        gp[1] = f.gy;
+        gp[2] = f.gx * ex + f.gy * ey;
+        if (!Hp) return;
+        Hp[0] = f.hxx;
+        Hp[1] = f.hxy;
+        Hp[2] = f.hxx * ex + f.hxy * ey;
+        Hp[3] = f.hyy;
+        Hp[4] = f.hxy * ex + f.hyy * ey;
+        Hp[5] = ex * (f.hxx * ex + f.hxy * ey) + ey * (f.hxy * ex + f.hyy * ey) - f.gx * (cx - x) - f.gy * (cy - y);
+    };
     if (p.use_slack) {  // soft_min over corners (not max-shifted, as utils.py:30-31)
         const double al = p.softmin_alpha;
         double e[MMAX], sum = 0;
 #pragma unroll
         for (int i = 0; i < MMAX; ++i) {
             if (i >= dm.nb) break;
-            e[i] = exp(-al * phi[i]);
+            double phi;
+            corner(i, &phi, nullptr, nullptr);
+            e[i] = exp(-al * phi);
             sum += e[i];
         }
         d[0] = -log(sum) / al;
+        if (!g && !Hw) return;
         double gd[3] = {0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < MMAX; ++i)
-            if (i < dm.nb)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[i][a];
-        if (g)
-            for (int a = 0; a < 3; ++a) g[0][a] = gd[a];
-        if (Hw) {
-            double H[6] = {0, 0, 0, 0, 0, 0};
-            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-            for (int i = 0; i < MMAX; ++i) {
-                if (i >= dm.nb) break;
-                const double wi = e[i] / sum;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) H[q] += wi * (Hp[i][q] - al * gp[i][ia[q]] * gp[i][ib[q]]);
-            }
-            for (int q = 0; q < 6; ++q) Hw[q] = w[0] * (H[q] + al * gd[ia[q]] * gd[ib[q]]);
-        }
-    } else {
+        double H[6] = {0, 0, 0, 0, 0, 0};
+        const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
         for (int i = 0; i < MMAX; ++i) {
             if (i >= dm.nb) break;
-            d[i] = phi[i];
-            if (g)
+            double phi, gp[3], Hp[6];
+            corner(i, &phi, gp, Hw ? Hp : nullptr);
 #pragma unroll
-                for (int a = 0; a < 3; ++a) g[i][a] = gp[i][a];
+            for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[a];
+            if (Hw) {
+                const double wi = e[i] / sum;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) H[q] += wi * (Hp[q] - al * gp[ia[q]] * gp[ib[q]]);
+            }
         }
-        if (Hw) {
+        if (g)
+            for (int a = 0; a < 3; ++a) g[0][a] = gd[a];
+        if (Hw)
+            for (int q = 0; q < 6; ++q) Hw[q] = w[0] * (H[q] + al * gd[ia[q]] * gd[ib[q]]);
+    } else {
+        if (Hw)
 #pragma unroll
             for (int q = 0; q < 6; ++q) Hw[q] = 0;
 #pragma unroll
-            for (int i = 0; i < MMAX; ++i)
-                if (i < dm.nb)
+        for (int i = 0; i < MMAX; ++i) {
+            if (i >= dm.nb) break;
+            double phi, gp[3], Hp[6];
+            corner(i, &phi, (g || Hw) ? gp : nullptr, Hw ? Hp : nullptr);
+            d[i] = phi;
+            if (g)
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[i][q];
+                for (int a = 0; a < 3; ++a) g[i][a] = gp[a];
+            if (Hw)
+#pragma unroll
+                for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[q];
         }
     }
 }
@@ -3021,32 +3061,58 @@ __device__ inline double objective_w(const NlotProblem& p, const Dims& dm, const
     return wsum(f) + p.slack_penalty * wsum(sq) + p.smooth_weight * wsum(uq);
 }
 
-// IPOPT filter augmentation (lane 0): drop the entries the new one dominates, append it (the oldest entry is
-// forgotten at capacity).  filt: the original problem's filter (count SC_NFILT) or the restoration's (SC_RNFILT).
-__device__ inline void filter_add(const Ws& ws, int b, double* filt, int sc_n, double theta, double phi, int* cs) {
-    const double gt = 1e-5, gp = 1e-8, ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
+// A filter update by the whole wave (uniform control flow, every lane calls): drop the entries (ft, fp) with
+// ft >= a && fp >= c (the new entry dominates them), keep the rest in order, append (a, c), forgetting the oldest entry
+// at capacity; the filter's count lives in SC(sc_n).  The kept entries of each 64-entry chunk move down in one
+// ballot-compacted store (destinations never pass the chunk's own entries, so a chunk's loads complete before any store
+// reaches them; later chunks are not touched), instead of lane 0's serial load -> store chain (one memory round trip
+// per entry).  cs (may be null): the step's counter set — [11] peak size, [12] entries forgotten.  Returns the new count.
+__device__ inline int filter_update(const Ws& ws, int b, double* filt, int sc_n, double a, double c, int* cs, int lane) {
     const int nfc = (int)SC(sc_n);
     int w = 0;
-    for (int i = 0; i < nfc; ++i) {
-        const double ft = filt[2 * i], fp = filt[2 * i + 1];
-        if (!(ft >= ntv && fp >= npv)) {
-            filt[2 * w] = ft;
-            filt[2 * w + 1] = fp;
-            ++w;
+    for (int base = 0; base < nfc; base += 64) {
+        const int i = base + lane;
+        double ft = 0.0, fp = 0.0;
+        bool keep = false;
+        if (i < nfc) {
+            ft = filt[2 * i];
+            fp = filt[2 * i + 1];
+            keep = !(ft >= a && fp >= c);
         }
-    }
-    if (w == FILT_MAX) {
-        for (int i = 0; i + 1 < FILT_MAX; ++i) {
-            filt[2 * i] = filt[2 * (i + 1)];
-            filt[2 * i + 1] = filt[2 * (i + 1) + 1];
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const int d = w + __popcll(m & ((1ull << lane) - 1ull));
+            filt[2 * d] = ft;
+            filt[2 * d + 1] = fp;
         }
-        w--;
-        if (cs) atomicAdd(cs + 12, 1);
+        w += __popcll(m);
     }
-    filt[2 * w] = ntv;
-    filt[2 * w + 1] = npv;
-    SC(sc_n) = w + 1;
-    if (cs) atomicMax(cs + 11, w + 1);
+    wsync();
+    if (lane == 0) {
+        if (w == FILT_MAX) {  // never reached on the bench workloads (NlotSolveStats.filter_forgotten)
+            for (int i = 0; i + 1 < FILT_MAX; ++i) {
+                filt[2 * i] = filt[2 * (i + 1)];
+                filt[2 * i + 1] = filt[2 * (i + 1) + 1];
+            }
+            w--;
+            if (cs) atomicAdd(cs + 12, 1);
+        }
+        filt[2 * w] = a;
+        filt[2 * w + 1] = c;
+        SC(sc_n) = w + 1;
+        if (cs) atomicMax(cs + 11, w + 1);
+    }
+    if (w == FILT_MAX) w--;
+    wsync();
+    return w + 1;
+}
+
+// IPOPT filter augmentation with the iterate's (theta, phi): margins gamma_theta = 1e-5, gamma_phi = 1e-8.  filt: the
+// original problem's filter (count SC_NFILT) or the restoration's (SC_RNFILT).  Whole wave.
+__device__ inline void filter_add(const Ws& ws, int b, double* filt, int sc_n, double theta, double phi, int* cs,
+                                  int lane) {
+    const double gt = 1e-5, gp = 1e-8, ntv = (1.0 - gt) * theta, npv = phi - gp * theta;
+    filter_update(ws, b, filt, sc_n, ntv, npv, cs, lane);
 }
 
 // The line search of the original problem failed and the soft restoration did not help: IPOPT's feasibility
@@ -3067,8 +3133,8 @@ __device__ int resto_enter(const NlotSolverOptions& o, const NlotProblem& p, con
         wsync();
         return PH_DONE;
     }
+    filter_add(ws, b, &AT(filt, 0), SC_NFILT, th, SC(SC_PHI), cnt_next, lane);
     if (lane == 0) {
-        filter_add(ws, b, &AT(filt, 0), SC_NFILT, th, SC(SC_PHI), cnt_next);
         SC(SC_RESTO) = 1;
         SC(SC_PHASE) = PH_RINIT;
         SC(SC_ACCSLOT) = -1;
@@ -3496,11 +3562,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
         double th_c, ph_c, f_c;
         theta_phi(mu0, &th_c, &ph_c, &f_c);
-        auto af_ok = [&]() {  // obj-constr progress filter (margin 1e-5 min(1, theta))
+        auto af_ok = [&]() {  // obj-constr progress filter (margin 1e-5 min(1, theta)); entries lane-parallel
             const double m = 1e-5 * fmin(1.0, th_c);
-            for (int i = 0; i < naf; ++i)
-                if (f_c + m >= AT(afilt, 2 * i) && th_c + m >= AT(afilt, 2 * i + 1)) return false;
-            return true;
+            bool bad = false;
+            for (int i = lane; i < naf; i += 64)
+                if (f_c + m >= AT(afilt, 2 * i) && th_c + m >= AT(afilt, 2 * i + 1)) bad = true;
+            return __ballot(bad) == 0ull;
         };
         // fixed mode (IPOPT AdaptiveMuUpdate): back to free mode as soon as the point makes sufficient progress
         // w.r.t. the progress filter (checked every iteration; remembered below), else one Fiacco-McCormick
@@ -3521,33 +3588,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         if (free_) {
             if (af_ok()) {  // remember the point: drop dominated entries, append (oldest forgotten at capacity)
                 const double m = 1e-5 * fmin(1.0, th_c), nf = f_c - m, nt = th_c - m;
-                int w = 0;
-                for (int i = 0; i < naf; ++i)
-                    if (!(AT(afilt, 2 * i) >= nf && AT(afilt, 2 * i + 1) >= nt)) ++w;
-                naf_new = (w == FILT_MAX ? w - 1 : w) + 1;
                 wsync();
-                if (lane == 0) {
-                    w = 0;
-                    for (int i = 0; i < naf; ++i) {
-                        const double fi = AT(afilt, 2 * i), ti = AT(afilt, 2 * i + 1);
-                        if (!(fi >= nf && ti >= nt)) {
-                            AT(afilt, 2 * w) = fi;
-                            AT(afilt, 2 * w + 1) = ti;
-                            ++w;
-                        }
-                    }
-                    if (w == FILT_MAX) {
-                        for (int i = 0; i + 1 < FILT_MAX; ++i) {
-                            AT(afilt, 2 * i) = AT(afilt, 2 * i + 2);
-                            AT(afilt, 2 * i + 1) = AT(afilt, 2 * i + 3);
-                        }
-                        --w;
-                        atomicAdd(cnt + 12, 1);
-                    }
-                    AT(afilt, 2 * w) = nf;
-                    AT(afilt, 2 * w + 1) = nt;
-                    atomicMax(cnt + 11, w + 1);
-                }
+                if (lane == 0) SC(SC_NAF) = naf;  // the count filter_update reads (the iteration-0 reset included)
+                wsync();
+                naf_new = filter_update(ws, b, &AT(afilt, 0), SC_NAF, nf, nt, cnt, lane);
             } else {  // insufficient progress: fixed mode at 0.8 x average complementarity
                 free_ = false;
                 mu = fmin(fmax(0.8 * avg, kMuMin), mu_max);
@@ -4167,7 +4211,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
                 }
                 double d[MMAX];
-                knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
+                knot_values(p, dm, ws, rank, k, xk, d, tval);
                 const double sk = AT(S, k) + al * AT(dS, k);
                 for (int j = 0; j < M; ++j) {
                     const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
@@ -4403,7 +4447,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     SC(SC_NFREJ) = 0;
                 }
             }
-            if (!tiny && !fa && lane == 0) filter_add(ws, b, &AT(filt, 0), SC_NFILT, theta, phi, cnt);
+            wsync();  // lane 0's filter reset above
+            if (!tiny && !fa) filter_add(ws, b, &AT(filt, 0), SC_NFILT, theta, phi, cnt, lane);
             // accept: primal and multipliers with alpha, bound multipliers with alpha_z + safeguard
             accept_point(al, SC(SC_AZ));
             const bool stop_tiny = tiny && SC(SC_TINYLAST) != 0.0;  // IPOPT STOP_AT_TINY_STEP
@@ -5074,7 +5119,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                 for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
             }
             double d[MMAX];
-            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
+            knot_values(p, dm, ws, rank, k, xk, d, tval);
             const double sk = AT(S, k) + al * AT(dS, k);
             for (int j = 0; j < M; ++j) {
                 const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
@@ -5142,7 +5187,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
         if (!(na < SC(SC_AMIN))) emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
         return;
     }
-    if (!fa && lane == 0) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, nullptr);  // no statistics here
+    if (!fa) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, nullptr, lane);  // no statistics here
     // accept: primal, p, n and equality multipliers with alpha; bound multipliers (z_p, z_n included) with alpha_z
     const double az = SC(SC_AZ), ks = 1e10;
     auto zupd = [&](double z, double dz, double sl) {
