@@ -91,7 +91,7 @@ def main():
             x = X0[i].copy()
             x[c] += d
             r = O.solve_one(B6_PROBLEM, x, XG[i], hm6, opt=opt, X_init=Xi[i])
-            return r["status"], r["cost"], r["iters"]
+            return r["status"], r["cost"], r["iters"], np.concatenate([np.ravel(r["X"]), np.ravel(r["U"])])
 
         res = []
         with ThreadPoolExecutor(a.threads) as ex:
@@ -99,9 +99,11 @@ def main():
                 with mlp_order(pd[2]):
                     res += list(ex.map(one, [(i, pd) for i in range(len(X0))]))
         n, m = len(X0), len(PERTURBATIONS)
+        XU = np.stack([r[3] for r in res]).reshape(m, n, -1)
         out = {"status": np.array([r[0] for r in res], np.int32).reshape(m, n),
                "cost": np.array([r[1] for r in res], float).reshape(m, n),
-               "iters": np.array([r[2] for r in res], np.int32).reshape(m, n)}
+               "iters": np.array([r[2] for r in res], np.int32).reshape(m, n),
+               "xdev": np.abs(XU - XU[0]).max(2)}
         data.update({"b6_x0": X0, "b6_xg": XG, "b6_xinit": Xi, **{f"b6_{k}": v for k, v in out.items()}})
         print(f"b6: {time.time() - t:.0f} s, statuses {np.bincount(out['status'][0], minlength=7).tolist()}",
               flush=True)

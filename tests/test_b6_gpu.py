@@ -60,7 +60,7 @@ def test_b6_batch_matches_oracle():
 
     f = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_outcomes.npz")))
     X0, XG, Xi = f["b6_x0"], f["b6_xg"], f["b6_xinit"]
-    out = {k: f[f"b6_{k}"] for k in ("status", "cost", "iters")}
+    out = {k: f[f"b6_{k}"] for k in ("status", "cost", "iters", "xdev")}
     r = solve_batch(prob, X0, XG, mlp=mlp, X_init=Xi, options=_abi.default_options())
     st, cost = r["status"].cpu().numpy(), r["cost"].cpu().numpy()
     print("b6 batch statuses gpu", st.tolist(), "oracle", out["status"].tolist(), flush=True)

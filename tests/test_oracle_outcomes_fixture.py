@@ -18,6 +18,7 @@ def test_fixture_layout():
     for case, n in (("metric", 128), ("b6", 24)):
         assert f[f"{case}_x0"].shape[0] == n and f[f"{case}_status"].shape == (6, n)
         assert f[f"{case}_cost"].shape == (6, n) and f[f"{case}_iters"].shape == (6, n)
+        assert f[f"{case}_xdev"].shape == (6, n) and (f[f"{case}_xdev"][0] == 0).all()
     assert f["b6_xinit"].shape == (24, 101, 7)
     # the split has both groups on the headline workload (tests/outcomes.py)
     import sys
@@ -25,7 +26,7 @@ def test_fixture_layout():
     sys.path.insert(0, HERE)
     from outcomes import reproducible
 
-    R = reproducible({k: f[f"metric_{k}"] for k in ("status", "cost")})
+    R = reproducible({k: f[f"metric_{k}"] for k in ("status", "cost", "xdev")})
     print("metric fixture: reproducible", int(R.sum()), "of", len(R))
     assert 0 < R.sum() < len(R)
 
