@@ -115,7 +115,7 @@ def test_batch_learned_sdf_matches_oracle(artefact):
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
     print("metric GPU status counts", np.bincount(sg, minlength=7).tolist(), "oracle",
           np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
-    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=48)
+    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=24)
 
 
 def test_safeguards_iterate_parity(artefact):
