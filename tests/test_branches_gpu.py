@@ -105,7 +105,11 @@ def test_iterates_match_oracle(name):
 @pytest.mark.parametrize("name", ["b1_dot_point2nd", "b5_ackermann2nd_squares", "b2_no_slack", "b2_smooth",
                                   "b2_enforce_heading", "b6_settings_N100", "b4_polygon", "discr_s_trapezoid"])
 def test_full_solves_match_oracle(name):
+    """12 perturbed start/goal pairs per branch case, split parity (tests/outcomes.py): identical status and (solved)
+    final cost within 1e-4 on every oracle-reproducible instance, the oracle's own spread on the chaotic ones."""
     import oracle as O
+    from outcomes import check_outcome_parity, oracle_outcomes
+    from nlotrajectories_amd import _abi
     from nlotrajectories_amd.solver import solve_batch
 
     prob, x0, xg = _cases()[name]
@@ -116,13 +120,10 @@ def test_full_solves_match_oracle(name):
     X0[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
     XG[:, :2] += rng.uniform(-0.05, 0.05, (B, 2))
     rg = solve_batch(prob, X0, XG)
-    rc = O.solve_batch(prob, X0, XG, opt=__import__("nlotrajectories_amd._abi", fromlist=["x"]).gpu_options(), threads=8)
+    out = oracle_outcomes(O, prob, X0, XG, opt=_abi.gpu_options(), threads=8)
     sg = rg["status"].cpu().numpy()
-    agree = (sg == rc["status"]).mean()
-    both = (sg == 0) & (rc["status"] == 0)
-    rel = np.abs(rg["cost"].cpu().numpy() - rc["cost"]) / np.abs(rc["cost"])
-    print(name, "gpu", sg.tolist(), "oracle", rc["status"].tolist(), "rel cost", np.round(rel[both], 8).tolist())
-    assert agree >= 0.75, (name, agree)
+    print(name, "gpu", sg.tolist(), "oracle", out["status"][0].tolist(), flush=True)
+    check_outcome_parity(name, sg, rg["cost"].cpu().numpy(), out)
     # GPU-solved trajectories satisfy the start / terminal / dynamics equalities and the bounds
     X, U = rg["X"].cpu().numpy(), rg["U"].cpu().numpy()
     term = [i for i in range(prob.nx) if prob.enforce_heading or i != 2]
