@@ -410,43 +410,6 @@ __device__ __forceinline__ HD corner_sdf(const NlotProblem& p, const Ws& ws, int
     return h;
 }
 
-// Inequality values only at a knot (the line search's trial points, MLP values of the trial list tval): d[j] of
-// knot_eval below with the same arithmetic, without the derivative machinery in the kernels that only need values
-__device__ __forceinline__ void knot_values(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
-                                            const double* xk, double* d, const float* tval) {
-    const double x = xk[0], y = xk[1];
-    if (p.shape == NLOT_SHAPE_DOT) {
-        d[0] = corner_sdf(p, ws, rank, k, x, y, tval).v;
-        return;
-    }
-    double sn, cs;
-    sincos(xk[2], &sn, &cs);
-    double phi[MMAX];
-#pragma unroll
-    for (int i = 0; i < MMAX; ++i) {
-        if (i >= dm.nb) break;
-        const double bx = p.body[i][0], by = p.body[i][1];
-        const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
-        phi[i] = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, tval).v;
-    }
-    if (p.use_slack) {  // soft_min over corners (not max-shifted, as utils.py:30-31)
-        const double al = p.softmin_alpha;
-        double sum = 0;
-#pragma unroll
-        for (int i = 0; i < MMAX; ++i) {
-            if (i >= dm.nb) break;
-            sum += exp(-al * phi[i]);
-        }
-        d[0] = -log(sum) / al;
-    } else {
-#pragma unroll
-        for (int i = 0; i < MMAX; ++i) {
-            if (i >= dm.nb) break;
-            d[i] = phi[i];
-        }
-    }
-}
-
 // Inequality functions at a knot (geometry.py:63-67, 107-117; utils.py:18-33): values d[j]
 // (slack excluded), pose gradients g[j][3], and Hw = sum_j w[j] d2 d_j / dpose2 (if w != null).
 __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, const Ws& ws, int rank, int k,
@@ -465,75 +428,72 @@ __device__ __forceinline__ void knot_eval(const NlotProblem& p, const Dims& dm, 
     }
     double sn, cs;
     sincos(xk[2], &sn, &cs);
-    // corner i's pose gradient gp[3] and Hessian Hp[6] (xx xy xt yy yt tt) of its SDF value, computed where they are
-    // used (one corner at a time: holding all corners' 36 doubles pushed k_iter_a over its register budget)
-    auto corner = [&](int i, double* phi, double* gp, double* Hp) {
+    double phi[MMAX], gp[MMAX][3], Hp[MMAX][6];  // Hp: xx xy xt yy yt tt
+#pragma unroll
+    for (int i = 0; i < MMAX; ++i) {
+        if (i >= dm.nb) break;
         const double bx = p.body[i][0], by = p.body[i][1];
         const double cx = x + cs * bx - sn * by, cy = y + sn * bx + cs * by;  // geometry.py:78-83
         const double ex = -(cy - y), ey = cx - x;                            // d c / d theta
         HD f = corner_sdf(p, ws, rank, k * dm.nb + i, cx, cy, tval);
-        *phi = f.v;
-        if (!gp) return;
-        gp[0] = f.gx;
-        gp[1] = f.gy;
-        gp[2] = f.gx * ex + f.gy * ey;
-        if (!Hp) return;
-        Hp[0] = f.hxx;
-        Hp[1] = f.hxy;
-        Hp[2] = f.hxx * ex + f.hxy * ey;
-        Hp[3] = f.hyy;
-        Hp[4] = f.hxy * ex + f.hyy * ey;
-        Hp[5] = ex * (f.hxx * ex + f.hxy * ey) + ey * (f.hxy * ex + f.hyy * ey) - f.gx * (cx - x) - f.gy * (cy - y);
-    };
+        phi[i] = f.v;
+        gp[i][0] = f.gx;
+        gp[i][1] = f.gy;
+        gp[i][2] = f.gx * ex + f.gy * ey;
+        Hp[i][0] = f.hxx;
+        Hp[i][1] = f.hxy;
+        Hp[i][2] = f.hxx * ex + f.hxy * ey;
+        Hp[i][3] = f.hyy;
+        Hp[i][4] = f.hxy * ex + f.hyy * ey;
+        Hp[i][5] = ex * (f.hxx * ex + f.hxy * ey) + ey * (f.hxy * ex + f.hyy * ey) - f.gx * (cx - x) - f.gy * (cy - y);
+    }
     if (p.use_slack) {  // soft_min over corners (not max-shifted, as utils.py:30-31)
         const double al = p.softmin_alpha;
         double e[MMAX], sum = 0;
 #pragma unroll
         for (int i = 0; i < MMAX; ++i) {
             if (i >= dm.nb) break;
-            double phi;
-            corner(i, &phi, nullptr, nullptr);
-            e[i] = exp(-al * phi);
+            e[i] = exp(-al * phi[i]);
             sum += e[i];
         }
         d[0] = -log(sum) / al;
-        if (!g && !Hw) return;
         double gd[3] = {0, 0, 0};
-        double H[6] = {0, 0, 0, 0, 0, 0};
-        const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+        for (int i = 0; i < MMAX; ++i)
+            if (i < dm.nb)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[i][a];
+        if (g)
+            for (int a = 0; a < 3; ++a) g[0][a] = gd[a];
+        if (Hw) {
+            double H[6] = {0, 0, 0, 0, 0, 0};
+            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+            for (int i = 0; i < MMAX; ++i) {
+                if (i >= dm.nb) break;
+                const double wi = e[i] / sum;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) H[q] += wi * (Hp[i][q] - al * gp[i][ia[q]] * gp[i][ib[q]]);
+            }
+            for (int q = 0; q < 6; ++q) Hw[q] = w[0] * (H[q] + al * gd[ia[q]] * gd[ib[q]]);
+        }
+    } else {
 #pragma unroll
         for (int i = 0; i < MMAX; ++i) {
             if (i >= dm.nb) break;
-            double phi, gp[3], Hp[6];
-            corner(i, &phi, gp, Hw ? Hp : nullptr);
+            d[i] = phi[i];
+            if (g)
 #pragma unroll
-            for (int a = 0; a < 3; ++a) gd[a] += (e[i] / sum) * gp[a];
-            if (Hw) {
-                const double wi = e[i] / sum;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) H[q] += wi * (Hp[q] - al * gp[ia[q]] * gp[ib[q]]);
-            }
+                for (int a = 0; a < 3; ++a) g[i][a] = gp[i][a];
         }
-        if (g)
-            for (int a = 0; a < 3; ++a) g[0][a] = gd[a];
-        if (Hw)
-            for (int q = 0; q < 6; ++q) Hw[q] = w[0] * (H[q] + al * gd[ia[q]] * gd[ib[q]]);
-    } else {
-        if (Hw)
+        if (Hw) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) Hw[q] = 0;
 #pragma unroll
-        for (int i = 0; i < MMAX; ++i) {
-            if (i >= dm.nb) break;
-            double phi, gp[3], Hp[6];
-            corner(i, &phi, (g || Hw) ? gp : nullptr, Hw ? Hp : nullptr);
-            d[i] = phi;
-            if (g)
+            for (int i = 0; i < MMAX; ++i)
+                if (i < dm.nb)
 #pragma unroll
-                for (int a = 0; a < 3; ++a) g[i][a] = gp[a];
-            if (Hw)
-#pragma unroll
-                for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[q];
+                    for (int q = 0; q < 6; ++q) Hw[q] += w[i] * Hp[i][q];
         }
     }
 }
@@ -4211,7 +4171,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
                 }
                 double d[MMAX];
-                knot_values(p, dm, ws, rank, k, xk, d, tval);
+                knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
                 const double sk = AT(S, k) + al * AT(dS, k);
                 for (int j = 0; j < M; ++j) {
                     const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);
@@ -5119,7 +5079,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                 for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
             }
             double d[MMAX];
-            knot_values(p, dm, ws, rank, k, xk, d, tval);
+            knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
             const double sk = AT(S, k) + al * AT(dS, k);
             for (int j = 0; j < M; ++j) {
                 const double t = AT(T, k * M + j) + al * AT(dT, k * M + j);

@@ -12,8 +12,9 @@ final cost (ReLU kinks, discrete filter / watchdog / mode decisions; DESIGN.md Â
     rounding (5, 14, 18, 19 of the fixture set).  The GPU must give the identical status, and on the solved ones a final cost
     within 1e-4 relative (BASELINE.json north_star), on 100 % of them;
   * chaotic: the rest.  There the bar is the oracle's own spread: status agreement with the unperturbed oracle at
-    least as high as the perturbed oracles' (less two instances of sampling slack), and jointly solved final costs
-    within 3x the oracle's own run-to-run envelope (quartile and maximum) or 1e-4.
+    least as high as the perturbed oracles' (less two instances of sampling slack); among the jointly solved, the
+    share whose final cost differs by more than 1e-4 (another local optimum) at most the perturbed oracles' share
+    (plus two instances), and no difference beyond 3x the oracle's own largest (or 1e-4).
 
 Test infrastructure only (imports nothing from the product package)."""
 import contextlib
@@ -111,12 +112,18 @@ def check_outcome_parity(label, sg, cg, out, min_reproducible=0):
         info.update(chaotic_gpu_status_agree=gpu_agree, chaotic_oracle_self_agree=self_agree)
         both = C & (sg == 0) & (so == 0)
         if both.any():
-            env = np.concatenate([np.abs(out["cost"][k] - co)[both & (out["status"][k] == 0)] /
-                                  np.abs(co[both & (out["status"][k] == 0)]) for k in range(1, nrun)])
-            q_self = float(np.quantile(env, 0.75)) if len(env) else 0.0
+            env, far_self = [], 0.0
+            for k in range(1, nrun):
+                jk = C & (so == 0) & (out["status"][k] == 0)
+                if jk.any():
+                    rk = np.abs(out["cost"][k] - co)[jk] / np.abs(co[jk])
+                    env.append(rk)
+                    far_self = max(far_self, float((rk > 1e-4).mean()))
+            env = np.concatenate(env) if env else np.zeros(0)
             m_self = float(env.max()) if len(env) else 0.0
-            info.update(chaotic_joint_solved=int(both.sum()), chaotic_gpu_rel_q75=float(np.quantile(rel[both], 0.75)),
-                        chaotic_gpu_rel_max=float(rel[both].max()), chaotic_self_q75=q_self, chaotic_self_max=m_self)
+            info.update(chaotic_joint_solved=int(both.sum()), chaotic_gpu_far_frac=float((rel[both] > 1e-4).mean()),
+                        chaotic_self_far_frac=far_self, chaotic_gpu_rel_max=float(rel[both].max()),
+                        chaotic_self_max=m_self)
     print(f"[parity] {label}: {info}", flush=True)
     assert R.sum() >= min_reproducible, (label, "reproducible group too small", info)
     assert not bad_status.any(), (label, "status differs on oracle-reproducible instances",
@@ -127,6 +134,10 @@ def check_outcome_parity(label, sg, cg, out, min_reproducible=0):
         slack = 2.0 / C.sum()
         assert info["chaotic_gpu_status_agree"] >= info["chaotic_oracle_self_agree"] - slack, (label, info)
         if "chaotic_joint_solved" in info:
-            assert (info["chaotic_gpu_rel_q75"] <= 3 * max(1e-4, info["chaotic_self_q75"]) and
-                    info["chaotic_gpu_rel_max"] <= 3 * max(1e-4, info["chaotic_self_max"])), (label, info)
+            # the share of jointly solved chaotic instances whose cost moves beyond 1e-4 (another local optimum) is at
+            # most the perturbed oracles' share plus two instances of sampling slack; no difference beyond 3x the
+            # oracle's own largest
+            nj = info["chaotic_joint_solved"]
+            assert info["chaotic_gpu_far_frac"] <= info["chaotic_self_far_frac"] + 2.0 / nj, (label, info)
+            assert info["chaotic_gpu_rel_max"] <= 3 * max(1e-4, info["chaotic_self_max"]), (label, info)
     return info
