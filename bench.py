@@ -344,6 +344,16 @@ def main():
         else:
             cpu = cpu_baseline(prob, w, x0.cpu().numpy(), xg.cpu().numpy(), a.cpu_sample, a.cpu_sample_1core,
                                a.cpu_threads, opt)
+    if cpu and "ips" in cpu and not cpu.get("estimate"):
+        # the sample's traj/s depends on which statuses its few instances draw (a 32-instance sample holds 10-20
+        # solved ones): also the measured instance-iteration rate over the GPU run's instance-iterations per solved
+        # instance, i.e. the CPU time of this run's whole status mix (an estimate, reported beside the value)
+        tot_it = sum(int(x["iters"].sum().item()) for x in results)
+        n_solved = max(sum(int((x["status"] == 0).sum().item()) for x in results), 1)
+        cpu["full_mix_estimate"] = {
+            "value": cpu["ips"] / (tot_it / n_solved), "unit": "trajectories/s", "cores": cpu["cores"],
+            "note": f"{cpu['ips']:.1f} instance-iterations/s (the sample) / {tot_it / n_solved:.0f} instance-iterations "
+                    f"per solved instance over rank 0's {len(results)} timed call(s)"}
 
     if rank == 0:
         B_all = a.batch * world
@@ -543,7 +553,7 @@ def cpu_baseline(prob, w, x0, xg, n_all, n_one, threads, opt, iter_cap=None, gpu
     ns, dt, sc, it = run(n_all, threads)
     ips = it / dt  # instance-iterations per second
     if iter_cap is None:
-        out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port",
+        out = {"value": ns / dt, "unit": "trajectories/s", "cores": threads, "kind": "port", "ips": ips,
                "sample": f"first {n_all} instances of rank 0's first timed batch: {ns} solved (status counts {sc}), "
                          f"{it} instance-iterations in {dt:.1f} s on {threads} OpenMP threads (host: {host})"}
     else:
