@@ -5350,7 +5350,11 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     NLOT_HIP_CHECK(hipEventCreateWithFlags(&res.e_v1, hipEventDisableTiming));
     NLOT_HIP_CHECK(hipStreamCreateWithFlags(&res.s4, hipStreamNonBlocking));
     hipStream_t s2 = res.s2, s3 = res.s3, s4 = res.s4;
-    int soc_fork = 0, early_value = 0;  // A/B knobs of the step's stream layout (NLOT_SOC_FORK, NLOT_EARLY_VALUE)
+    // stream layout of the step (A/B knobs NLOT_SOC_FORK, NLOT_EARLY_VALUE).  The early value launch (the previous
+    // step's line-search candidates evaluated on a fourth stream while this step's evaluations and Newton solves run)
+    // is on by default since round 4: +1.3 % at the bench's scheduling with the round-4 MLP kernels (bitwise-equal
+    // results, scripts/gpu_r04q.sh; neutral in round 3 when the full MLP launch held one 512-VGPR wave per SIMD)
+    int soc_fork = 0, early_value = 1;
     if (const char* e = getenv("NLOT_SOC_FORK")) soc_fork = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("NLOT_EARLY_VALUE")) early_value = atoi(e) != 0;
     if (g_timing)
