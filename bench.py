@@ -422,6 +422,14 @@ def main():
             "avg_launch_ms": v_avg_ms,
             "launches": agg["mlp_value_launches"],
         }
+        if os.environ.get("NLOT_EARLY_VALUE", "1") != "0" and not streaming:
+            note = ("per step, the value launch runs in two parts, the first on a fourth stream concurrently with the "
+                    "step's evaluations and Newton solves (NLOT_EARLY_VALUE, default since round 4: +1.3 %% traj/s); "
+                    "avg_launch_ms sums both parts' event-timed durations, which include that overlap, so frac is a "
+                    "lower bound on the kernel's own (0.479 on standalone 3.3 M-point launches, scripts/mlp_bench.py)")
+            mlp_value["overlap_note"] = note.replace("%%", "%")
+            mlp_full["overlap_note"] = ("the full launch shares the CUs with the early value launch of the previous "
+                                        "step's candidates (fourth stream); its event-timed duration includes that")
         # the dominant kernel by device time: k_ric on the metric workload, the SDF-MLP on the stress workload
         if stress:
             rooflines = {"roofline": mlp_full, "roofline_mlp_value": mlp_value, "roofline_ric": ric}
