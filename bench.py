@@ -310,8 +310,11 @@ def main():
     alg_bytes = 2 * 4 * (nvar + ncon)
     ric_alg = ric_solves_per_launch * alg_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     ric_traffic = None
-    # PMC at bench size (B = 65536): scripts/pmc_r03.sh -> profiles/r03/pmc_traffic_r03m_B65536.json
-    tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_r03m_B65536.json")
+    # PMC at bench size (B = 65536): scripts/pmc_traffic.sh + scripts/pmc_traffic.py -> profiles/r04/ (round 3's file
+    # as the fallback)
+    tf = os.path.join(ROOT, "profiles", "r04", "pmc_traffic_r04_B65536.json")
+    if not os.path.exists(tf):
+        tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_r03m_B65536.json")
     pmc = None
     if os.path.exists(tf):
         with open(tf) as f:
@@ -382,10 +385,11 @@ def main():
                     "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline.  The "
                     "second-order corrections (substitution with the stored factors, k_ric<DYN, false, true>) and the "
                     "restoration solves run on a side stream and are not counted in this launch's solves",
-            "pmc_note": "traffic = HBM bytes per solve from profiles/r03/pmc_traffic_r03m_B65536.json (FETCH_SIZE x2 + "
-                        "WRITE_SIZE at B = 65536: 1.85x the algorithmic bytes) x solves per launch; phase timers "
-                        "(profiles/r03/kric_phase_timers_r03n.log): one solve takes ~160 us alone, ~400 us at B = 65536 "
-                        "(the forward sweep's memory passes 4x slower under load)",
+            "pmc_note": (f"traffic = HBM bytes per solve from {os.path.relpath(tf, ROOT)} (FETCH_SIZE x2 + WRITE_SIZE "
+                         f"at B = 65536: {pmc['k_ric']['ratio_to_algorithmic']:.2f}x the algorithmic bytes) x solves per "
+                         "launch; phase timers (profiles/r03/kric_phase_timers_r03n.log): one solve takes ~160 us alone, "
+                         "~400 us at B = 65536 (the forward sweep's memory passes 4x slower under load)")
+                        if pmc else "no PMC traffic file",
         }
         mlp_full = {
             "kernel": kname % "full" + ": SDF-MLP value + gradient + Hessian",
@@ -405,10 +409,12 @@ def main():
             "points_per_launch": agg["mlp_points_full"] / n_l,
             "avg_launch_ms": avg_ms,
             "launches": agg["mlp_full_launches"],
-            "traffic_note": "HBM bytes per point in the solve at B = 65536 (profiles/r03/pmc_traffic_r03m_B65536.json): "
-                            "53.2 B/point = 1.07x the algorithmic 49.8 B/point with forward reuse (coordinates, the "
-                            "trial's value and ReLU pattern in, value + gradient + Hessian out), 1.66x the 32 B/point "
-                            "of a launch without reuse",
+            "traffic_note": (f"HBM bytes per point in the solve at B = 65536 ({os.path.relpath(tf, ROOT)}): "
+                             f"{pmc['mlp_full']['hbm_bytes_per_point']:.1f} B/point = "
+                             f"{pmc['mlp_full']['ratio_to_algorithmic_with_reuse']:.2f}x the algorithmic "
+                             f"{pmc['mlp_full']['algorithmic_bytes_per_point_with_reuse']:.1f} B/point with forward reuse "
+                             "(coordinates, the trial's coordinates, value and ReLU pattern in; value + gradient + "
+                             "Hessian out)") if pmc else "no PMC traffic file",
         }
         mlp_value = {
             "kernel": kname % "value" + ": line-search trial points, value only",
