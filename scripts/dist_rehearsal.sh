@@ -1,7 +1,7 @@
 #!/bin/bash
 # bench.py's multi-rank path with the real solver on a 1-GPU box: 2 ranks share cuda:0 over gloo
 # (NLOT_DIST_BACKEND=gloo); sharded seeded instances, barriers, max-over-ranks clock, gather to rank 0.
-OUT=gpurun_out/r02r
+OUT=${OUT:-gpurun_out/r02r}
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p $OUT
 export TMPDIR=/tmp
