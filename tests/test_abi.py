@@ -69,3 +69,36 @@ def test_workspace_holds_the_slots_only():
     assert workspace_bytes(METRIC_PROBLEM, 4096, 4096) == full
     assert workspace_bytes(METRIC_PROBLEM, 1 << 20, 4096) == full
     assert workspace_bytes(METRIC_PROBLEM, 4096, 512) == workspace_bytes(METRIC_PROBLEM, 512) < full
+
+
+def test_solve_batch_refuses_bad_arguments_before_the_device():
+    """nlot_solve_batch validates on the host and fails loudly (NLOT_ERR_INVALID + nlot_last_error) before any device
+    call, so these run without a GPU: an empty or oversized batch, the CPU-only general_bounds option, an unknown
+    mu_strategy, a learned-SDF problem without a net, null output pointers."""
+    import ctypes as C
+
+    from nlotrajectories_amd import _abi, _lib
+    from nlotrajectories_amd.problem import BENCHMARKS, METRIC_PROBLEM
+
+    L = _lib.lib()
+    pc = BENCHMARKS["b2"]["problem"].to_c()
+
+    def call(opt, B, prob=pc):
+        rc = L.nlot_solve_batch(C.byref(prob), C.byref(opt), None, None, None, None, None, None, None, None, None,
+                                None, B, None, 0, None)
+        return rc, L.nlot_last_error().decode()
+
+    base = _abi.gpu_options()
+    assert call(base, 0) == (-1, "B out of range")
+    assert call(base, (1 << 26) + 1) == (-1, "B out of range")
+    rc, msg = call(base, 4)
+    assert rc == -1 and msg == "nlot_solve_batch: null pointer"
+    o = _abi.gpu_options()
+    o.general_bounds = 1
+    rc, msg = call(o, 4)
+    assert rc == -1 and "CPU restatement only" in msg
+    o = _abi.gpu_options()
+    o.mu_strategy = 2
+    assert call(o, 4)[0] == -1 and "mu_strategy" in call(o, 4)[1]
+    rc, msg = call(base, 4, METRIC_PROBLEM.to_c())
+    assert rc == -1 and "requires an NlotMlp" in msg
