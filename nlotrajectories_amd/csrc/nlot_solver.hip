@@ -73,6 +73,16 @@ enum IterPass { PASS_ALL = 0, PASS_INIT = 1, PASS_SOC = 2, PASS_EVAL = 3 };
 #ifndef NLOT_RIC_RING
 #define NLOT_RIC_RING 2
 #endif
+// the restoration phases run few wavefronts (the instances in restoration), so their latency, not residency, counts
+#ifndef NLOT_WPE_RA
+#define NLOT_WPE_RA NLOT_WPE_A  // k_resto_a
+#endif
+#ifndef NLOT_WPE_RLS
+#define NLOT_WPE_RLS NLOT_WPE_ACC  // k_resto_ls
+#endif
+#ifndef NLOT_WPE_RRIC
+#define NLOT_WPE_RRIC NLOT_WPE_RIC  // k_ric<DYN, true>
+#endif
 #if !defined(NLOT_RIC_FENCED) && !defined(NLOT_RIC_INORDER)
 #define NLOT_RIC_INORDER
 #endif
@@ -1002,10 +1012,12 @@ __device__ __forceinline__ void ric_sync_reads() {
 // Newton (or least-squares) solve of the instances whose stage matrices k_iter_a built (SC_RIC = 1),
 // with IPOPT's inertia correction: on a wrong inertia the group rebuilds its stages with the next
 // delta_w and factorises again.  Outputs: dX dU dS yi_n yk_n yt_n (and the second right-hand side).
-// waves per SIMD of k_ric: NLOT_WPE_RIC, except ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
-template <int DYN, bool SOC = false>
+// waves per SIMD of k_ric: NLOT_WPE_RIC (restoration: NLOT_WPE_RRIC; corrections: NLOT_WPE_SOC), except
+// ackermann_2nd (nx = 7), whose larger stage spills 384 B/lane at 2
+template <int DYN, bool RESTO, bool SOC>
 struct RicWpe {
-    static constexpr int value = SOC ? NLOT_WPE_SOC : DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1 : NLOT_WPE_RIC;
+    static constexpr int value = SOC ? NLOT_WPE_SOC : DYN % NLOT_RK4_BIAS == NLOT_ACKERMANN_2ND ? 1
+                                                  : RESTO ? NLOT_WPE_RRIC : NLOT_WPE_RIC;
 };
 // RESTO = true: the restoration problem's Newton solve (instances with SC_RESTO = 1, list ws.actr): every
 // equality row is soft (p, n eliminated, oracle soft_transform): before stage k uses the value function of
@@ -1015,7 +1027,7 @@ struct RicWpe {
 // SOC = true: the second-order corrections (SC_RICFIX >= 0) by substitution with the stored factors; the SOC = false
 // launch skips them (separate instantiations: the substitution's registers stay out of the factorising sweep's).
 template <int DYN, bool RESTO, bool SOC = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, SOC>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, RESTO, SOC>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
                                             const int* __restrict__ nact, int mode, int* __restrict__ diag,
                                             int max_tries) {
@@ -4497,7 +4509,7 @@ struct Resto {
 };
 
 template <int DYN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_resto_a(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA))) void k_resto_a(
     const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
     const int* __restrict__ actr, const double* __restrict__ x0, const double* __restrict__ xg, int* cnt) {
     const NlotProblem& p = *pp_;
@@ -5033,7 +5045,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
 }
 
 template <int DYN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC))) void k_resto_ls(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS))) void k_resto_ls(
     const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
     const int* __restrict__ actr, const double* __restrict__ x0, const double* __restrict__ xg, int* cnt,
     int* cnt_next, float* tp_next, const float* tval, int nspec_next) {
