@@ -5624,10 +5624,11 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         if (n_resto > 0) NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_r, 0));
         if (ev[4]) (void)hipEventRecord(ev[5], st);
         if (use_mlp) {
+            // the wait for the early part comes before the timing event: ev[2]..ev[3] is the second part's own time
+            if (early_value) NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_v1, 0));
             if (ev[0]) (void)hipEventRecord(ev[2], st);
             MlpReuse vb{};
             vb.base = C + 14;
-            if (early_value) NLOT_HIP_CHECK(hipStreamWaitEvent(st, res.e_v1, 0));
             rc = launch_mlp_strided(mlp->dev, ws.tpts[q], (int64_t)n_active * NSPEC, C + 1, (int)P, 0, nullptr,
                                     mo_t[q], false, st, early_value ? &vb : nullptr);
             if (rc) break;
