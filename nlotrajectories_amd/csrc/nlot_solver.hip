@@ -357,6 +357,22 @@ __device__ inline void res_io(const Ws& ws, int64_t b, int lane, double* buf, bo
 }
 #undef NLOT_IO
 
+// lane-strided update of n workspace elements in chunks of CH elements per lane: a chunk's NV loads per element are
+// all issued before its stores (the compiler may not move a load above a store into the same workspace), so an array
+// costs one memory round trip per chunk instead of one per 64 elements; ld(i, v) loads, st(i, v) computes and stores
+template <int CH, int NV, class Ld, class St>
+__device__ __forceinline__ void chunked_update(int n, int lane, Ld&& ld, St&& st) {
+    for (int i0 = lane; i0 < n; i0 += 64 * CH) {
+        double v[CH][NV];
+#pragma unroll
+        for (int r = 0; r < CH; ++r)
+            if (i0 + 64 * r < n) ld(i0 + 64 * r, v[r]);
+#pragma unroll
+        for (int r = 0; r < CH; ++r)
+            if (i0 + 64 * r < n) st(i0 + 64 * r, v[r]);
+    }
+}
+
 // ---- wave-level helpers (64 lanes; results broadcast from lane 0 so every lane branches alike) ----
 __device__ inline double wsum(double v) {
 #pragma unroll
@@ -3927,12 +3943,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         mu = fmin(fmax(sig * avg, kMuMin), mu_max);
         sig = mu / avg;
         tau = fmax(0.99, 1.0 - mu);
-        for (int i = lane; i < (N + 1) * NX; i += 64) AT(dX, i) = qa_[i] + sig * qc_[i];
-        for (int i = lane; i < N * NU; i += 64) AT(dU, i) = qa_[oU + i] + sig * qc_[oU + i];
-        for (int i = lane; i <= N; i += 64) AT(dS, i) = qa_[oS + i] + sig * qc_[oS + i];
-        for (int i = lane; i < NX; i += 64) AT(yi_n, i) = qa_[oyi + i] + sig * qc_[oyi + i];
-        for (int i = lane; i < N * NX; i += 64) AT(yk_n, i) = qa_[oyk + i] + sig * qc_[oyk + i];
-        for (int i = lane; i < 8; i += 64) AT(yt_n, i) = qa_[oyt + i] + sig * qc_[oyt + i];
+        // the step for the chosen sigma: affine + sigma centering (chunked: loads before stores)
+        auto comb = [&](int n, int oa, double* dst) {
+            chunked_update<4, 2>(n, lane, [&](int i, double* v) { v[0] = qa_[oa + i]; v[1] = qc_[oa + i]; },
+                                 [&](int i, const double* v) { dst[i] = v[0] + sig * v[1]; });
+        };
+        comb((N + 1) * NX, 0, &AT(dX, 0));
+        comb(N * NU, oU, &AT(dU, 0));
+        comb(N + 1, oS, &AT(dS, 0));
+        comb(NX, oyi, &AT(yi_n, 0));
+        comb(N * NX, oyk, &AT(yk_n, 0));
+        comb(8, oyt, &AT(yt_n, 0));
         wsync();
         if (lane == 0) {  // a new barrier problem: BacktrackingLineSearch::Reset (filter, soft restoration, watchdog)
             SC(SC_MU) = mu;
@@ -4242,28 +4263,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                 const double zn = z + az * dz;
                 return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
             };
-            for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
-            for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e) + al * AT(dU, e);
-                AT(U, e) = u;
-                AT(zl, e) = zupd(AT(zl, e), AT(dzl, e), u - p.umin[e % NU]);
-                AT(zu, e) = zupd(AT(zu, e), AT(dzu, e), p.umax[e % NU] - u);
-            }
-            for (int k = lane; k <= N; k += 64)
-                if (dm.ns) {
-                    const double s_ = AT(S, k) + al * AT(dS, k);
-                    AT(S, k) = s_;
-                    AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s_);
-                }
-            for (int q = lane; q < (N + 1) * M; q += 64) {
-                const double t = AT(T, q) + al * AT(dT, q);
-                AT(T, q) = t;
-                AT(vt, q) = zupd(AT(vt, q), AT(dvt, q), t);
-                AT(yd, q) += al * (AT(yd_n, q) - AT(yd, q));
-            }
-            for (int i = lane; i < NX; i += 64) AT(yi, i) += al * (AT(yi_n, i) - AT(yi, i));
-            for (int i = lane; i < N * NX; i += 64) AT(yk, i) += al * (AT(yk_n, i) - AT(yk, i));
-            for (int i = lane; i < nc; i += 64) AT(yt, i) += al * (AT(yt_n, i) - AT(yt, i));
+            chunked_update<4, 2>((N + 1) * NX, lane, [&](int i, double* v) { v[0] = AT(X, i); v[1] = AT(dX, i); },
+                   [&](int i, const double* v) { AT(X, i) = v[0] + al * v[1]; });
+            chunked_update<4, 6>(N * NU, lane,
+                   [&](int e, double* v) {
+                       v[0] = AT(U, e); v[1] = AT(dU, e); v[2] = AT(zl, e); v[3] = AT(dzl, e); v[4] = AT(zu, e);
+                       v[5] = AT(dzu, e);
+                   },
+                   [&](int e, const double* v) {
+                       const double u = v[0] + al * v[1];
+                       AT(U, e) = u;
+                       AT(zl, e) = zupd(v[2], v[3], u - p.umin[e % NU]);
+                       AT(zu, e) = zupd(v[4], v[5], p.umax[e % NU] - u);
+                   });
+            if (dm.ns)
+                chunked_update<4, 4>(N + 1, lane, [&](int k, double* v) { v[0] = AT(S, k); v[1] = AT(dS, k); v[2] = AT(zs, k); v[3] = AT(dzs, k); },
+                       [&](int k, const double* v) {
+                           const double s_ = v[0] + al * v[1];
+                           AT(S, k) = s_;
+                           AT(zs, k) = zupd(v[2], v[3], s_);
+                       });
+            chunked_update<4, 6>((N + 1) * M, lane,
+                   [&](int q, double* v) {
+                       v[0] = AT(T, q); v[1] = AT(dT, q); v[2] = AT(vt, q); v[3] = AT(dvt, q); v[4] = AT(yd, q);
+                       v[5] = AT(yd_n, q);
+                   },
+                   [&](int q, const double* v) {
+                       const double t = v[0] + al * v[1];
+                       AT(T, q) = t;
+                       AT(vt, q) = zupd(v[2], v[3], t);
+                       AT(yd, q) = v[4] + al * (v[5] - v[4]);
+                   });
+            chunked_update<4, 2>(NX, lane, [&](int i, double* v) { v[0] = AT(yi, i); v[1] = AT(yi_n, i); },
+                   [&](int i, const double* v) { AT(yi, i) = v[0] + al * (v[1] - v[0]); });
+            chunked_update<4, 2>(N * NX, lane, [&](int i, double* v) { v[0] = AT(yk, i); v[1] = AT(yk_n, i); },
+                   [&](int i, const double* v) { AT(yk, i) = v[0] + al * (v[1] - v[0]); });
+            chunked_update<4, 2>(nc, lane, [&](int i, double* v) { v[0] = AT(yt, i); v[1] = AT(yt_n, i); },
+                   [&](int i, const double* v) { AT(yt, i) = v[0] + al * (v[1] - v[0]); });
         };
         if (ph == PH_SOFT1) {
             // IPOPT TrySoftRestoStep: the step a = min(alpha_max, alpha_z) for primal and dual variables is taken if
