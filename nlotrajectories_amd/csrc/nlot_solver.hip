@@ -3292,28 +3292,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
 #pragma unroll
         for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
     }
-    for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) = AT(dv, q) - AT(T, q);
+    chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(dv, q); v[1] = AT(T, q); },
+                         [&](int q, const double* v) { AT(rcq, q) = v[0] - v[1]; });
     wsync();
 
+    // the lane-strided sums below run through chunked_update (loads of 4 rows first, then the same per-lane order)
     auto theta_phi = [&](double mu, double* th, double* phv, double* fout = nullptr) {
         double t = 0, bar = 0, lin = 0;
-        for (int i = lane; i < NX; i += 64) t += fabs(AT(rci, i));
-        for (int i = lane; i < nc; i += 64) t += fabs(AT(rct, i));
-        for (int i = lane; i < N * NX; i += 64) t += fabs(AT(rcd, i));
-        for (int q = lane; q < (N + 1) * M; q += 64) {
-            t += fabs(AT(rcq, q));
-            bar += log(AT(T, q));
-            lin += AT(T, q);
-        }
-        for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
-            bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
-        }
+        auto tsum = [&](int, const double* v) { t += fabs(v[0]); };
+        chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(rci, i); }, tsum);
+        chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(rct, i); }, tsum);
+        chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(rcd, i); }, tsum);
+        chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(rcq, q); v[1] = AT(T, q); },
+                             [&](int, const double* v) {
+                                 t += fabs(v[0]);
+                                 bar += log(v[1]);
+                                 lin += v[1];
+                             });
+        chunked_update<4, 1>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); },
+                             [&](int e, const double* v) {
+                                 const double u = v[0];
+                                 bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
+                             });
         if (dm.ns)
-            for (int k = lane; k <= N; k += 64) {
-                bar += log(AT(S, k));
-                lin += AT(S, k);
-            }
+            chunked_update<4, 1>(N + 1, lane, [&](int k, double* v) { v[0] = AT(S, k); },
+                                 [&](int, const double* v) {
+                                     bar += log(v[0]);
+                                     lin += v[0];
+                                 });
         *th = wsum(t);
         const double fo = objective_w(p, dm, ws, b, lane, 0.0);
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
@@ -3412,14 +3418,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         psq += v * v;
         p1 += fabs(v);
     };
-    for (int i = lane; i < NX; i += 64) pri_(AT(rci, i));
-    for (int i = lane; i < nc; i += 64) pri_(AT(rct, i));
-    for (int i = lane; i < N * NX; i += 64) pri_(AT(rcd, i));
+    auto pri1 = [&](int, const double* v) { pri_(v[0]); };
+    chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(rci, i); }, pri1);
+    chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(rct, i); }, pri1);
+    chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(rcd, i); }, pri1);
     cviol = wmax(primal);
-    for (int q = lane; q < (N + 1) * M; q += 64) {
-        pri_(AT(rcq, q));
-        cviol = fmax(cviol, fmax(0.0, -AT(dv, q)));
-    }
+    chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(rcq, q); v[1] = AT(dv, q); },
+                         [&](int, const double* v) {
+                             pri_(v[0]);
+                             cviol = fmax(cviol, fmax(0.0, -v[1]));
+                         });
     auto compl_ = [&](double z, double s) {
         c0 = fmax(c0, fabs(z * s));
         cmu = fmax(cmu, fabs(z * s - mu0));
@@ -3427,18 +3435,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         zsum += fabs(z);
         nzc += 1;
     };
-    for (int e = lane; e < N * NU; e += 64) {
-        const double u = AT(U, e);
-        compl_(AT(zl, e), u - p.umin[e % NU]);
-        compl_(AT(zu, e), p.umax[e % NU] - u);
-    }
-    if (dm.ns)
-        for (int k = lane; k <= N; k += 64) compl_(AT(zs, k), AT(S, k));
-    for (int q = lane; q < (N + 1) * M; q += 64) compl_(AT(vt, q), AT(T, q));
-    for (int i = lane; i < NX; i += 64) ysum += fabs(AT(yi, i));
-    for (int i = lane; i < N * NX; i += 64) ysum += fabs(AT(yk, i));
-    for (int i = lane; i < nc; i += 64) ysum += fabs(AT(yt, i));
-    for (int q = lane; q < (N + 1) * M; q += 64) ysum += fabs(AT(yd, q));
+    chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
+                         [&](int e, const double* v) {
+                             compl_(v[1], v[0] - p.umin[e % NU]);
+                             compl_(v[2], p.umax[e % NU] - v[0]);
+                         });
+    auto compl2 = [&](int, const double* v) { compl_(v[0], v[1]); };
+    if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = AT(S, k); }, compl2);
+    chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); }, compl2);
+    auto ysum1 = [&](int, const double* v) { ysum += fabs(v[0]); };
+    chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(yi, i); }, ysum1);
+    chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(yk, i); }, ysum1);
+    chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(yt, i); }, ysum1);
+    chunked_update<4, 1>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(yd, q); }, ysum1);
     dual = wmax(dual);
     primal = wmax(primal);
     cviol = wmax(cviol);
@@ -3511,14 +3520,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     bool reset_filter = false;
     auto compl_mu = [&](double m) {
         double cm = 0;
-        for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
-            cm = fmax(cm, fabs(AT(zl, e) * (u - p.umin[e % NU]) - m));
-            cm = fmax(cm, fabs(AT(zu, e) * (p.umax[e % NU] - u) - m));
-        }
-        if (dm.ns)
-            for (int k = lane; k <= N; k += 64) cm = fmax(cm, fabs(AT(zs, k) * AT(S, k) - m));
-        for (int q = lane; q < (N + 1) * M; q += 64) cm = fmax(cm, fabs(AT(vt, q) * AT(T, q) - m));
+        chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
+                             [&](int e, const double* v) {
+                                 cm = fmax(cm, fabs(v[1] * (v[0] - p.umin[e % NU]) - m));
+                                 cm = fmax(cm, fabs(v[2] * (p.umax[e % NU] - v[0]) - m));
+                             });
+        auto cm2 = [&](int, const double* v) { cm = fmax(cm, fabs(v[0] * v[1] - m)); };
+        if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = AT(S, k); }, cm2);
+        chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); }, cm2);
         return wmax(cm);
     };
     bool tiny_last = o.mu_strategy == 0 && SC(SC_TINYLAST) != 0.0;  // a tiny step forces a decrease
