@@ -67,9 +67,6 @@ enum IterPass { PASS_ALL = 0, PASS_INIT = 1, PASS_SOC = 2, PASS_EVAL = 3 };
 #ifndef NLOT_WPE_SOC
 #define NLOT_WPE_SOC 2  // the correction (substitution) instantiation of k_ric
 #endif
-#ifndef NLOT_WPE_TPI
-#define NLOT_WPE_TPI 1  // k_ric_tpi: one instance per lane, the 512-register file (AGPRs as spill space)
-#endif
 #ifndef NLOT_RIC_RING
 #define NLOT_RIC_RING 2
 #endif
@@ -2079,782 +2076,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Thread-per-instance Newton solve (k_ric_tpi): the factorising solves of k_ric<DYN, false> (MODE_NEWTON and the
-// INIT least-squares solve) with one instance per lane, 64 instances per wavefront.  The lane-group kernel above
-// spreads one instance's stage over 16 lanes and hands columns over through LDS: about 2,200 instructions per
-// stage for 4 instances, a quarter of the cycles issuing.  Here each lane runs the oracle's dense
-// recursion (oracle/nlot_oracle.c riccati()) on its own instance in registers: ~1,500 fp64 instructions per stage
-// for 64 instances, no LDS, no hand-offs.  Inputs and outputs are k_ric's, in the same layouts (hg, the slot's
-// [A B 0 | c] | M, gains, vf, qfac, tfac, phi, the steps and multipliers of both right-hand sides), so the
-// second-order corrections (k_ric<DYN, false, true>) and the restoration solves (k_ric<DYN, true>) run unchanged.
-// NCR = the number of terminal equalities (nc, compile time: nx - 1 without enforced heading, nx with it).
-// One wave per SIMD: the recursion's live set (value function, stage block, gains) is ~150 doubles per lane.
-// ---------------------------------------------------------------------------------------------
-template <int DYN, int NCR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_TPI))) void k_ric_tpi(
-    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, const Ws* __restrict__ ws_,
-    const int* __restrict__ active, int n_active, const int* __restrict__ nact, int mode, int* __restrict__ diag,
-    int max_tries) {
-    using SV = Solver<DYN>;
-    constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NCOL = SV::NCOL, NAB = SV::NAB;
-    constexpr int NZA = NX + NU;  // columns of [A B]: the slack column of the dynamics is zero
-    constexpr int SLOT = SV::SLOT, HG = SV::HG, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
-    constexpr int QFL = ldl_len(NV), PR = NX + 2, HW = NZ + 2;
-    static_assert(NCR <= NX && NCR >= 1, "terminal equalities");
-    const Dims& dm = *dd_;
-    const Ws& ws = *ws_;
-    const int si = (int)(blockIdx.x * 64 + threadIdx.x);
-    const int nlist = std::min(n_active, *nact);
-    if (si >= nlist) return;
-    const int b = active[si];
-    if ((int)SC(SC_RIC) != 1 || SC(SC_RESTO) != 0.0 || SC(SC_RICFIX) >= 0.0) return;
-    if (mode == MODE_LSQ && (int)SC(SC_PHASE) != PH_INIT) return;
-    const int N = dm.N, ns = dm.ns, nr = (int)SC(SC_RNR);
-    const double last_dw = SC(SC_DWLAST);
-    double* SL = &AT(stg, 0);
-    const bool newton = mode == MODE_NEWTON;
-    double nu_[2][NCR];
-
-    // backward sweep + terminal multipliers (oracle riccati()); 0, or 1 on a wrong inertia / singular block
-    auto backward = [&]() -> int {
-        double P[NX][NX], pv[2][NX], G[NX][NCR], Psi[NCR][NCR], psi[2][NCR];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-#pragma unroll
-            for (int j = 0; j < NX; ++j) P[i][j] = 0.0;
-            pv[0][i] = pv[1][i] = 0.0;
-#pragma unroll
-            for (int c = 0; c < NCR; ++c) G[i][c] = 0.0;
-        }
-#pragma unroll
-        for (int a = 0; a < NCR; ++a) {
-            psi[0][a] = psi[1][a] = 0.0;
-#pragma unroll
-            for (int c = 0; c < NCR; ++c) Psi[a][c] = 0.0;
-        }
-        int negsum = 0;
-        if (newton) SC(SC_DC) = 0.0;
-#pragma unroll 1
-        for (int k = N; k >= 0; --k) {
-            const int nv = (k < N ? NU : 0) + ns;
-            const double* hgk = &AT(hg, k * HG);
-            const double* sk = SL + (size_t)k * SLOT;
-            double c[NX], Mk[2][2];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) c[i] = sk[sAB + i * NAB + NZ];
-            Mk[0][0] = sk[sM];
-            Mk[0][1] = sk[sM + 1];
-            Mk[1][0] = sk[sM + 2];
-            Mk[1][1] = sk[sM + 3];
-            // psi_r += G' c (the value function of stage k + 1), P c + p_r
-            double Pc[2][NX];
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) {
-                double t = 0;
-#pragma unroll
-                for (int r = 0; r < NX; ++r) t += G[r][a] * c[r];
-                psi[0][a] += t;
-                psi[1][a] += t;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double t = 0;
-#pragma unroll
-                for (int j = 0; j < NX; ++j) t += P[i][j] * c[j];
-                Pc[0][i] = t + pv[0][i];
-                Pc[1][i] = t + pv[1][i];
-            }
-            // [A B] of the stage; QN = AB' G (the controls' rows; the slack row of the dynamics is zero)
-            double AB[NX][NZA];
-#pragma unroll
-            for (int r = 0; r < NX; ++r)
-#pragma unroll
-                for (int j = 0; j < NZA; ++j) AB[r][j] = sk[sAB + r * NAB + j];
-            double QNx[NX][NCR], QNv[NU][NCR];
-#pragma unroll
-            for (int i = 0; i < NZA; ++i)
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) {
-                    double t = 0;
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += AB[r][i] * G[r][a];
-                    if (i < NX) QNx[i][a] = t;
-                    else QNv[i - NX][a] = t;
-                }
-            // Q = H + AB' P AB + cross terms (M couples the positions of x_k and x_{k+1}), in the blocks the recursion
-            // uses: Q_xx (upper triangle), Q_xv[i][v] = Q[i][NX + v], Q_vv; q_r = g_r + AB' (P c + p_r) (+ M c)
-            auto Hij = [&](int i, int j) { return hgk[i * HW + j]; };
-            double Qxx[NX][NX], Qxv[NX][NV], Qvv[NV][NV], qx[2][NX], qv[2][NV];
-            {
-                double W[NX][NZA];  // P AB
-#pragma unroll
-                for (int r = 0; r < NX; ++r)
-#pragma unroll
-                    for (int j = 0; j < NZA; ++j) {
-                        double t = 0;
-#pragma unroll
-                        for (int q = 0; q < NX; ++q) t += P[r][q] * AB[q][j];
-                        W[r][j] = t;
-                    }
-                auto qe = [&](int i, int j) {  // Q[i][j], i <= j or (i < NX <= j)
-                    double t = Hij(j, i);
-                    if (i < NZA && j < NZA) {
-#pragma unroll
-                        for (int r = 0; r < NX; ++r) t += AB[r][i] * W[r][j];
-                    }
-                    if (i < 2 && j < NZA) t += Mk[i][0] * AB[0][j] + Mk[i][1] * AB[1][j];
-                    if (j < 2 && i < NZA) t += Mk[j][0] * AB[0][i] + Mk[j][1] * AB[1][i];
-                    return t;
-                };
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int j = i; j < NX; ++j) Qxx[i][j] = qe(i, j);
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) Qxv[i][v] = qe(i, NX + v);
-#pragma unroll
-                for (int a = 0; a < NV; ++a)
-#pragma unroll
-                    for (int v = a; v < NV; ++v) Qvv[a][v] = Qvv[v][a] = qe(NX + a, NX + v);
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-                    for (int i = 0; i < NZ; ++i) {
-                        double t = rr < nr ? Hij(i, NZ + rr) : 0.0;
-                        if (i < NZA) {
-#pragma unroll
-                            for (int r = 0; r < NX; ++r) t += AB[r][i] * Pc[rr][r];
-                        }
-                        if (i < 2) t += Mk[i][0] * c[0] + Mk[i][1] * c[1];
-                        if (i < NX) qx[rr][i] = t;
-                        else qv[rr][i - NX] = t;
-                    }
-            }
-            // factor Q_vv (pivoted LDL^T, the inertia count), gains K = -Q_vv^-1 Q_vx, k_r, Kn
-            double Kg[NV][NX], kg[2][NV], Kn[NV][NCR];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-#pragma unroll
-                for (int j = 0; j < NX; ++j) Kg[v][j] = 0.0;
-                kg[0][v] = kg[1][v] = 0.0;
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) Kn[v][a] = 0.0;
-            }
-            if (nv > 0) {
-                double L[NV][NV];
-                int perm[NV], nneg;
-#pragma unroll
-                for (int a = 0; a < NV; ++a)
-#pragma unroll
-                    for (int cc = 0; cc < NV; ++cc) L[a][cc] = (a < nv && cc < nv) ? Qvv[a][cc] : 0.0;
-                if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
-                negsum += nneg;
-                if (negsum > NCR) return 1;
-                if (newton) {
-                    double* qf = &AT(qfac, k * QFL);
-#pragma unroll
-                    for (int a = 0; a < NV; ++a) {
-#pragma unroll
-                        for (int cc = 0; cc < NV; ++cc) qf[a * NV + cc] = L[a][cc];
-                        qf[NV * NV + a] = (double)perm[a];
-                    }
-                }
-                double col[NV];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) {
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? -Qxv[j][v] : 0.0;
-                    ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) Kg[v][j] = v < nv ? col[v] : 0.0;
-                }
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr) {
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = v < nv ? -qv[rr][v] : 0.0;
-                    ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) kg[rr][v] = v < nv ? col[v] : 0.0;
-                }
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) {
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) col[v] = (v < nv && v < NU) ? -QNv[v < NU ? v : 0][a] : 0.0;
-                    ldl_solve1<NV>(L, nv, perm, col);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) Kn[v][a] = v < nv ? col[v] : 0.0;
-                }
-            }
-            // gains to the slot (GN[c][v]: K' | k_0 | k_1 | Kn'), the forward sweep's and the corrections' input
-            {
-                double* GN = SL + (size_t)k * SLOT + sGN;
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) GN[j * NV + v] = Kg[v][j];
-                    GN[NX * NV + v] = kg[0][v];
-                    GN[(NX + 1) * NV + v] = kg[1][v];
-#pragma unroll
-                    for (int a = 0; a < NX; ++a) GN[(NX + 2 + a) * NV + v] = a < NCR ? Kn[v][a < NCR ? a : 0] : 0.0;
-                }
-            }
-            // terminal system: Psi += QN_v' Kn, psi_r += QN_v' k_r (QN's slack row is zero)
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) {
-#pragma unroll
-                for (int cc = 0; cc < NCR; ++cc) {
-                    double t = 0;
-#pragma unroll
-                    for (int v = 0; v < NU; ++v) t += QNv[v][a] * Kn[v][cc];
-                    Psi[a][cc] += t;
-                }
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr) {
-                    double t = 0;
-#pragma unroll
-                    for (int v = 0; v < NU; ++v) t += QNv[v][a] * kg[rr][v];
-                    psi[rr][a] += t;
-                }
-            }
-            // value function of stage k: P = Q_xx + Q_xv K (symmetrised), p_r = q_x + Q_xv k_r, G = QN_x + Q_xv Kn
-            double* vfk = &AT(vf, k * VF);
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int j = 0; j < NX; ++j) {
-                    double t = i <= j ? Qxx[i][j] : Qxx[j][i];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += Qxv[i][v] * Kg[v][j];
-                    P[i][j] = t;
-                }
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int j = 0; j < i; ++j) {
-                    const double a = 0.5 * (P[i][j] + P[j][i]);
-                    P[i][j] = P[j][i] = a;
-                }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr) {
-                    double t = qx[rr][i];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += Qxv[i][v] * kg[rr][v];
-                    pv[rr][i] = t;
-                }
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) {
-                    double t = QNx[i][a];
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) t += Qxv[i][v] * Kn[v][a];
-                    G[i][a] = t;
-                }
-            }
-            if (k == N) {  // the terminal equalities C x_N = xg enter here
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int a = 0; a < NCR; ++a) G[i][a] = dm.tidx[a] == i ? 1.0 : 0.0;
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) psi[0][a] = psi[1][a] = newton ? AT(rct, a) : 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-#pragma unroll
-                for (int j = 0; j < NX; ++j) vfk[i * NCOL + j] = P[i][j];
-                vfk[i * NCOL + NX] = pv[0][i];
-                vfk[i * NCOL + NX + 1] = pv[1][i];
-#pragma unroll
-                for (int a = 0; a < NX; ++a) vfk[i * NCOL + NX + 2 + a] = a < NCR ? G[i][a] : 0.0;
-            }
-        }
-        // terminal multipliers: -Psi nu_r = G_0' dx0 + psi_r (delta_c on the terminal block when singular / inertia)
-        double dx0[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dx0[i] = newton ? -AT(rci, i) : 0.0;
-        double L[NCR][NCR];
-        int perm[NCR], nneg;
-#pragma unroll
-        for (int i = 0; i < NCR; ++i)
-#pragma unroll
-            for (int cc = 0; cc < NCR; ++cc) L[i][cc] = -Psi[i][cc];
-        const int f = ldl_factor<NCR>(L, NCR, perm, &nneg);
-        if (f == 2 || nneg != negsum) {
-            const double dc = 1e-8 * pow(SC(SC_MU), 0.25);
-#pragma unroll
-            for (int i = 0; i < NCR; ++i)
-#pragma unroll
-                for (int cc = 0; cc < NCR; ++cc) L[i][cc] = -Psi[i][cc] + (i == cc ? dc : 0.0);
-            if (ldl_factor<NCR>(L, NCR, perm, &nneg)) return 1;
-            if (nneg != negsum) return 1;
-            SC(SC_DC) = dc;
-        }
-        if (newton) {  // tfac in the NX x NX layout of k_ric (the corrections read it)
-            double* tf = &AT(tfac, 0);
-#pragma unroll
-            for (int a = 0; a < NX; ++a) {
-#pragma unroll
-                for (int cc = 0; cc < NX; ++cc) tf[a * NX + cc] = (a < NCR && cc < NCR) ? L[a < NCR ? a : 0][cc < NCR ? cc : 0] : 0.0;
-                tf[NX * NX + a] = a < NCR ? (double)perm[a < NCR ? a : 0] : (double)a;
-            }
-        }
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            if (rr >= nr) {  // k_ric leaves the unused right-hand side's multipliers at 0
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) nu_[rr][a] = 0.0;
-                continue;
-            }
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) {
-                double t = psi[rr][a];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) t += G[r][a] * dx0[r];
-                nu_[rr][a] = t;
-            }
-            ldl_solve1<NCR>(L, NCR, perm, nu_[rr]);
-        }
-        return 0;
-    };
-
-    // delta_w enters the stage matrices linearly (k_ric's add_dw): H += ddw (I_nz + sum_q J_q J_q'), g += ddw sum_q J_q c_q
-    auto add_dw = [&](double ddw) {
-        const int M = dm.M, sd = dm.sd;
-#pragma unroll 1
-        for (int k = 0; k <= N; ++k) {
-            double* o = &AT(hg, k * HG);
-            const int is = k < N ? NX + NU : NX, nz = is + (ns ? 1 : 0);
-            for (int i = 0; i < nz; ++i) o[i * HW + i] += ddw;
-            for (int qq = 0; qq < M; ++qq) {
-                double J[3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) J[a] = AT(Jd, (k * M + qq) * 3 + a);
-                const double r = ddw * AT(rcq, k * M + qq);
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) o[a * HW + cc] += ddw * J[a] * J[cc];
-                    o[a * HW + NZ] += J[a] * r;
-                    if (nr > 1) o[a * HW + NZ + 1] += J[a] * r;
-                    if (sd) {
-                        o[is * HW + a] += ddw * J[a];
-                        o[a * HW + is] += ddw * J[a];
-                    }
-                }
-                if (sd) {
-                    o[is * HW + is] += ddw;
-                    o[is * HW + NZ] += r;
-                    if (nr > 1) o[is * HW + NZ + 1] += r;
-                }
-            }
-        }
-    };
-
-    // inertia correction (IPOPT): delta_w = 0, then 1e-4 (or last / 3), x100 (x8 once one was used); an attempt cap
-    // defers the rest of the sequence to the next global step (same sequence, k_ric's SC_RETRY / SC_DWHG)
-    double dw = 0.0, dw_in_hg = 0.0;
-    const bool resume = newton && SC(SC_RETRY) >= 0.0;
-    if (resume) {
-        dw = SC(SC_RETRY);
-        dw_in_hg = SC(SC_DWHG);
-    }
-    int fail = 0, n_tries = 0;
-    bool deferred = false;
-#pragma unroll 1
-    for (int attempt = resume ? 1 : 0;; ++attempt) {
-        ++n_tries;
-        if (attempt > 0) {
-            add_dw(dw - dw_in_hg);
-            dw_in_hg = dw;
-        }
-        fail = backward();
-        if (!fail || !newton) break;
-        dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
-        if (dw > 1e40) break;
-        if (n_tries >= max_tries && (int)SC(SC_PHASE) == PH_EVAL) {
-            deferred = true;
-            break;
-        }
-    }
-    if (diag && newton) {
-        atomicAdd(diag, n_tries);
-        atomicMax(diag + 1, n_tries);
-        if (n_tries > 1) atomicAdd(diag + 2, 1);
-    }
-    if (deferred) {
-        SC(SC_RETRY) = dw;
-        SC(SC_DWHG) = dw_in_hg;
-        return;
-    }
-    if (fail) {
-        if (newton) {
-            SC(SC_STATUS) = NLOT_NUMERIC;
-            SC(SC_PHASE) = PH_DONE;
-            SC(SC_RIC) = 0;
-        } else {
-            SC(SC_RIC) = 3;
-        }
-        return;
-    }
-
-    // the forward sweep runs in k_ric_tpi_fwd (its own register budget): nu_r in yt_n / yt2, SC_RIC = 5
-#pragma unroll
-    for (int a = 0; a < NCR; ++a) {
-        AT(yt_n, a) = nu_[0][a];
-        AT(yt2, a) = nu_[1][a];
-    }
-    if (dw > 0.0 && newton) SC(SC_DWLAST) = dw;
-    SC(SC_RETRY) = -1.0;
-    SC(SC_DW) = dw;
-    SC(SC_RIC) = 5;
-}
-
-// Forward sweep of k_ric_tpi (instances with SC_RIC = 5): its own kernel, so the backward sweep's register budget
-// does not bound it.  Reads the gains, vf and the slots' [A B 0 | c] | M, nu_r from yt_n / yt2.
-template <int DYN, int NCR>
-__global__ __launch_bounds__(64) void k_ric_tpi_fwd(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
-                                                    const Ws* __restrict__ ws_, const int* __restrict__ active,
-                                                    int n_active, const int* __restrict__ nact, int mode, int write_phi) {
-    using SV = Solver<DYN>;
-    constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NCOL = SV::NCOL, NAB = SV::NAB;
-    constexpr int SLOT = SV::SLOT, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
-    constexpr int PR = NX + 2;
-    const Dims& dm = *dd_;
-    const Ws& ws = *ws_;
-    const int si = (int)(blockIdx.x * 64 + threadIdx.x);
-    const int nlist = std::min(n_active, *nact);
-    if (si >= nlist) return;
-    const int b = active[si];
-    if ((int)SC(SC_RIC) != 5) return;
-    const int N = dm.N, ns = dm.ns, nr = (int)SC(SC_RNR);
-    const bool newton = mode == MODE_NEWTON;
-    double* SL = &AT(stg, 0);
-    double nu_[2][NCR];
-#pragma unroll
-    for (int a = 0; a < NCR; ++a) {
-        nu_[0][a] = AT(yt_n, a);
-        nu_[1][a] = AT(yt2, a);
-    }
-    // forward sweep: dv_k = k_r + K dx_k + Kn nu_r; the closed-loop map Phi = A + B K and offsets off_r = c + B (k_r +
-    // Kn nu_r) go to phi (the corrections reuse Phi); dx_{k+1} = Phi dx_k + off_r; multipliers y_k = -grad V_{k+1}(dx_{k+1})
-    // - M_k' dx_k, y_init = -grad V_0(dx_0), y_term = nu
-    double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
-    double* dUo[2] = {&AT(dU, 0), &AT(dU2, 0)};
-    double* dSo[2] = {&AT(dS, 0), &AT(dS2, 0)};
-    double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
-    double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
-    double x[2][NX], xp[2][NX], Mp[2][2] = {{0, 0}, {0, 0}};
-#pragma unroll
-    for (int i = 0; i < NX; ++i) x[0][i] = x[1][i] = newton ? -AT(rci, i) : 0.0;
-#pragma unroll 1
-    for (int k = 0; k <= N; ++k) {
-        const double* sk = SL + (size_t)k * SLOT;
-        const double* GN = sk + sGN;
-        const double* vfk = &AT(vf, k * VF);
-        double Kt[NV][NX], dvn[2][NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-#pragma unroll
-            for (int j = 0; j < NX; ++j) Kt[v][j] = GN[j * NV + v];
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                double t = GN[(NX + rr) * NV + v];
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) t += GN[(NX + 2 + a) * NV + v] * nu_[rr][a];
-                dvn[rr][v] = t;
-            }
-        }
-        // this knot's step and the multiplier of the constraint ending here (V_k at dx_k)
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            if (rr >= nr) break;
-            double dv[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                double t = dvn[rr][v];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) t += Kt[v][j] * x[rr][j];
-                dv[v] = t;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) dXo[rr][k * NX + i] = x[rr][i];
-            if (k < N)
-#pragma unroll
-                for (int v = 0; v < NU; ++v) dUo[rr][k * NU + v] = dv[v];
-            if (ns) dSo[rr][k] = k < N ? dv[NU] : dv[0];
-            double mx[2] = {0.0, 0.0};
-            if (k > 0) {
-                mx[0] = Mp[0][0] * xp[rr][0] + Mp[1][0] * xp[rr][1];
-                mx[1] = Mp[0][1] * xp[rr][0] + Mp[1][1] * xp[rr][1];
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double t = vfk[i * NCOL + NX + rr];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) t += vfk[i * NCOL + j] * x[rr][j];
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) t += vfk[i * NCOL + NX + 2 + a] * nu_[rr][a];
-                if (k == 0) yio[rr][i] = -t;
-                else yko[rr][(k - 1) * NX + i] = -t - (i < 2 ? mx[i] : 0.0);
-            }
-        }
-        if (k == N) break;
-        double* ph = write_phi ? &AT(phi, (size_t)k * NX * PR) : nullptr;
-        double xn[2][NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double Bi[NU];
-#pragma unroll
-            for (int v = 0; v < NU; ++v) Bi[v] = sk[sAB + i * NAB + NX + v];
-            double o0 = sk[sAB + i * NAB + NZ], o1 = o0;
-#pragma unroll
-            for (int v = 0; v < NU; ++v) {
-                o0 += Bi[v] * dvn[0][v];
-                o1 += Bi[v] * dvn[1][v];
-            }
-            double t0 = o0, t1 = o1;
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-                double f = sk[sAB + i * NAB + j];
-#pragma unroll
-                for (int v = 0; v < NU; ++v) f += Bi[v] * Kt[v][j];
-                if (ph) ph[i * PR + j] = f;
-                t0 += f * x[0][j];
-                t1 += f * x[1][j];
-            }
-            if (ph) {
-                ph[i * PR + NX] = o0;
-                ph[i * PR + NX + 1] = o1;
-            }
-            xn[0][i] = t0;
-            xn[1][i] = t1;
-        }
-        Mp[0][0] = sk[sM];
-        Mp[0][1] = sk[sM + 1];
-        Mp[1][0] = sk[sM + 2];
-        Mp[1][1] = sk[sM + 3];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            xp[0][i] = x[0][i];
-            xp[1][i] = x[1][i];
-            x[0][i] = xn[0][i];
-            x[1][i] = xn[1][i];
-        }
-    }
-    SC(SC_RIC) = 2;
-}
-
-// Second-order corrections, thread-per-instance (k_soc_tpi): the substitution of k_ric<DYN, false, true> (same
-// recursion: w = P' c + p', q = g + M c + AB' w, k = -Q_vv^-1 q_v with the stored factor, p = q_x + K' q_v, psi +=
-// Gamma'(c + B k), nu from the stored terminal factor; then the forward sweep) with one instance per lane.  Reads
-// what the iteration's Newton solve stored (gains, vf, qfac, tfac) and k_iter_a's corrected g and c; writes k_0 into
-// the gains and p_0 into vf, the step and the multipliers.  The closed-loop maps are recomputed from A, B and K.
-template <int DYN, int NCR>
-__global__ __launch_bounds__(64) 
-void k_soc_tpi(
-    const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, const Ws* __restrict__ ws_,
-    const int* __restrict__ active, int n_active, const int* __restrict__ nact) {
-    using SV = Solver<DYN>;
-    constexpr int NX = SV::NX, NU = SV::NU, NV = SV::NV, NZ = SV::NZ, NCOL = SV::NCOL, NAB = SV::NAB;
-    constexpr int NZA = NX + NU;
-    constexpr int SLOT = SV::SLOT, HG = SV::HG, VF = SV::VF, sAB = SV::sAB, sM = SV::sM, sGN = SV::sGN;
-    constexpr int QFL = ldl_len(NV), HW = NZ + 2;
-    const Dims& dm = *dd_;
-    const Ws& ws = *ws_;
-    if (ws.prio) __builtin_amdgcn_s_setprio(2);  // NLOT_SETPRIO (see k_ric)
-    const int si = (int)(blockIdx.x * 64 + threadIdx.x);
-    const int nlist = std::min(n_active, *nact);
-    if (si >= nlist) return;
-    const int b = active[si];
-    if ((int)SC(SC_RIC) != 1 || SC(SC_RESTO) != 0.0 || SC(SC_RICFIX) < 0.0) return;
-    const int N = dm.N, ns = dm.ns;
-    double* SL = &AT(stg, 0);
-    // backward substitution
-    double pn[NX], psi[NCR];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) pn[i] = 0.0;
-#pragma unroll
-    for (int a = 0; a < NCR; ++a) psi[a] = 0.0;
-#pragma unroll 1
-    for (int k = N; k >= 0; --k) {
-        const int nv = (k < N ? NU : 0) + ns;
-        const bool kn = k < N;
-        const double* sk = SL + (size_t)k * SLOT;
-        double* GN = SL + (size_t)k * SLOT + sGN;
-        const double* hgk = &AT(hg, k * HG);
-        const double* vn = &AT(vf, (kn ? k + 1 : N) * VF);
-        double c[NX], w[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) c[i] = kn ? sk[sAB + i * NAB + NZ] : 0.0;
-        // w = P' c + p' (the value function of stage k + 1; zero beyond the horizon)
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double t = pn[i];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) t += vn[i * NCOL + j] * c[j];
-            w[i] = kn ? t : 0.0;
-        }
-        double q[NZ];
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) {
-            double t = hgk[i * HW + NZ];
-            if (kn) {
-                if (i < 2) t += sk[sM + 2 * i] * c[0] + sk[sM + 2 * i + 1] * c[1];
-                if (i < NZA) {
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) t += sk[sAB + r * NAB + i] * w[r];
-                }
-            }
-            q[i] = t;
-        }
-        double kv[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) kv[v] = v < nv ? -q[NX + v] : 0.0;
-        if (nv > 0) {
-            double L[NV][NV];
-            int perm[NV];
-            const double* f = &AT(qfac, k * QFL);
-#pragma unroll
-            for (int a = 0; a < NV; ++a) {
-#pragma unroll
-                for (int cc = 0; cc < NV; ++cc) L[a][cc] = f[a * NV + cc];
-                perm[a] = (int)f[NV * NV + a];
-            }
-            ldl_solve1<NV>(L, nv, perm, kv);
-        }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) GN[NX * NV + v] = kv[v];  // k_0
-        // p = q_x + K' q_v (K' q_v = Q_xv k), e = c + B k, psi += Gamma' e (at N: psi = the terminal residuals)
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double t = q[i];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) t += GN[i * NV + v] * q[NX + v];
-            pn[i] = t;
-            AT(vf, k * VF + i * NCOL + NX) = t;  // p_0
-        }
-        if (!kn) {
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) psi[a] = AT(rct, a);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double e = c[i];
-#pragma unroll
-                for (int v = 0; v < NU; ++v) e += sk[sAB + i * NAB + NX + v] * kv[v];
-#pragma unroll
-                for (int a = 0; a < NCR; ++a) psi[a] += vn[i * NCOL + NX + 2 + a] * e;
-            }
-        }
-    }
-    // terminal multiplier: (-Psi + delta_c) nu = psi + Gamma_0' dx0 with the Newton solve's stored factor
-    double dx0[NX], nu[NCR];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) dx0[i] = -AT(rci, i);
-    {
-        const double* v0 = &AT(vf, 0);
-#pragma unroll
-        for (int a = 0; a < NCR; ++a) {
-            double t = psi[a];
-#pragma unroll
-            for (int r = 0; r < NX; ++r) t += v0[r * NCOL + NX + 2 + a] * dx0[r];
-            nu[a] = t;
-        }
-        double L[NCR][NCR];
-        int perm[NCR];
-        const double* f = &AT(tfac, 0);
-#pragma unroll
-        for (int a = 0; a < NCR; ++a) {
-#pragma unroll
-            for (int cc = 0; cc < NCR; ++cc) L[a][cc] = f[a * NX + cc];
-            perm[a] = (int)f[NX * NX + a];
-        }
-        ldl_solve1<NCR>(L, NCR, perm, nu);
-    }
-    // forward sweep (one right-hand side): dv_k = k_0 + K dx_k + Kn nu, dx_{k+1} = A dx_k + B dv_k + c_k, multipliers
-    double x[NX], xp[NX], Mp[2][2] = {{0, 0}, {0, 0}};
-#pragma unroll
-    for (int i = 0; i < NX; ++i) x[i] = dx0[i];
-#pragma unroll 1
-    for (int k = 0; k <= N; ++k) {
-        const double* sk = SL + (size_t)k * SLOT;
-        const double* GN = sk + sGN;
-        const double* vfk = &AT(vf, k * VF);
-        double dv[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            double t = GN[NX * NV + v];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) t += GN[j * NV + v] * x[j];
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) t += GN[(NX + 2 + a) * NV + v] * nu[a];
-            dv[v] = t;
-        }
-#pragma unroll
-        for (int i = 0; i < NX; ++i) AT(dX, k * NX + i) = x[i];
-        if (k < N)
-#pragma unroll
-            for (int v = 0; v < NU; ++v) AT(dU, k * NU + v) = dv[v];
-        if (ns) AT(dS, k) = k < N ? dv[NU] : dv[0];
-        double mx[2] = {0.0, 0.0};
-        if (k > 0) {
-            mx[0] = Mp[0][0] * xp[0] + Mp[1][0] * xp[1];
-            mx[1] = Mp[0][1] * xp[0] + Mp[1][1] * xp[1];
-        }
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double t = vfk[i * NCOL + NX];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) t += vfk[i * NCOL + j] * x[j];
-#pragma unroll
-            for (int a = 0; a < NCR; ++a) t += vfk[i * NCOL + NX + 2 + a] * nu[a];
-            if (k == 0) AT(yi_n, i) = -t;
-            else AT(yk_n, (k - 1) * NX + i) = -t - (i < 2 ? mx[i] : 0.0);
-        }
-        if (k == N) break;
-        double xn[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double t = sk[sAB + i * NAB + NZ];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) t += sk[sAB + i * NAB + j] * x[j];
-#pragma unroll
-            for (int v = 0; v < NU; ++v) t += sk[sAB + i * NAB + NX + v] * dv[v];
-            xn[i] = t;
-        }
-        Mp[0][0] = sk[sM];
-        Mp[0][1] = sk[sM + 1];
-        Mp[1][0] = sk[sM + 2];
-        Mp[1][1] = sk[sM + 3];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            xp[i] = x[i];
-            x[i] = xn[i];
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < NCR; ++a) AT(yt_n, a) = nu[a];
-    SC(SC_RETRY) = -1.0;
-    SC(SC_DW) = SC(SC_RICFIX);
-    SC(SC_RIC) = 2;
-}
-
-// ---------------------------------------------------------------------------------------------
 // kernels (one 64-lane workgroup = one instance; grid = active instances)
 // ---------------------------------------------------------------------------------------------
 static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, Ws ws,
                                                    const double* __restrict__ x0, const double* __restrict__ xg,
                                                    const double* __restrict__ Xinit, const int* __restrict__ adm,
-                                                   const int* __restrict__ adm_base) {
+                                                   const int* __restrict__ cadm) {
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
     const int lane = threadIdx.x;
     // the first fill (adm = NULL): slot i holds instance i; an admission: the slots k_admit appended to the next
-    // active list at adm[*adm_base ..], holding the instances k_admit assigned (ws.sinst)
-    const int b = adm ? adm[*adm_base + (int)blockIdx.x] : (int)blockIdx.x;
+    // active list at adm[cadm[13] ..], holding the instances k_admit assigned (ws.sinst).  k_admit admitted
+    // cadm[2] - cadm[13] of them (fewer than the host's grid on a shortfall, which it flags): blocks past that exit
+    if (adm && (int)blockIdx.x >= cadm[2] - cadm[13]) return;
+    const int b = adm ? adm[cadm[13] + (int)blockIdx.x] : (int)blockIdx.x;
     const int64_t inst = adm ? ws.sinst[b] : b;
     const int N = dm.N, nx = dm.nx, nu = dm.nu, M = dm.M;
     const double k1 = o.bound_push, k2 = o.bound_frac;
@@ -5204,7 +4439,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
         if (!(na < SC(SC_AMIN))) emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
         return;
     }
-    if (!fa) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, nullptr, lane);  // no statistics here
+    if (!fa) filter_add(ws, b, &AT(rfilt, 0), SC_RNFILT, rth, rph, cnt, lane);  // peak / forgotten statistics too
     // accept: primal, p, n and equality multipliers with alpha; bound multipliers (z_p, z_n included) with alpha_z
     const double az = SC(SC_AZ), ks = 1e10;
     auto zupd = [&](double z, double dz, double sl) {
@@ -5539,33 +4774,10 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         }
         synced = last + 1;
     };
-    // the factorising Newton solves (main stream): the lane-group k_ric, or thread-per-instance (k_ric_tpi, opt-in
-    // NLOT_RIC_TPI=1, nx <= 5: measured slower in round 4, kept for the A/B); k_ric_tpi is instantiated for nc = nx - 1
-    // (free terminal heading) and nc = nx
-    const bool ric_tpi = getenv("NLOT_RIC_TPI") && atoi(getenv("NLOT_RIC_TPI")) != 0 && Dyn<DYN>::NX <= 5 &&
-                         (dm.nc == Dyn<DYN>::NX || dm.nc == Dyn<DYN>::NX - 1);
+    // the factorising Newton solves (main stream): the lane-group k_ric
     auto launch_ric = [&](const int* list, const int* count, int mode, int* diag, int tries) {
-        if (ric_tpi) {
-            const dim3 grid((n_active + 63) / 64);
-            constexpr int NXD = Dyn<DYN>::NX, NXM = NXD > 1 ? NXD - 1 : 1;
-            // phi (closed-loop maps) only for the lane-group corrections (NLOT_RIC_TPI=0 for them is not offered:
-            // both paths switch together), so the thread-per-instance forward sweep skips it
-            const int write_phi = 0;
-            if (dm.nc == NXD) {
-                hipLaunchKernelGGL((k_ric_tpi<DYN, NXD>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count, mode,
-                                   diag, tries);
-                hipLaunchKernelGGL((k_ric_tpi_fwd<DYN, NXD>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count,
-                                   mode, write_phi);
-            } else {
-                hipLaunchKernelGGL((k_ric_tpi<DYN, NXM>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count, mode,
-                                   diag, tries);
-                hipLaunchKernelGGL((k_ric_tpi_fwd<DYN, NXM>), grid, dim3(64), 0, st, dP, dD, dW, list, n_active, count,
-                                   mode, write_phi);
-            }
-        } else {
-            hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
-                               st, dP, dD, dW, list, n_active, count, mode, diag, tries);
-        }
+        hipLaunchKernelGGL((k_ric<DYN, false>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0,
+                           st, dP, dD, dW, list, n_active, count, mode, diag, tries);
     };
     for (step = 0; step < max_steps && n_active > 0; ++step) {
         const int* act = ws.act[cur];
@@ -5590,18 +4802,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             if (with_pass)
                 hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, s2, dP, dD, o, dW, act, ws.x0s, ws.xgs,
                                    (int)PASS_SOC, C, Cn);
-            if (ric_tpi) {
-                const dim3 grid((n_active + 63) / 64);
-                if (dm.nc == Dyn<DYN>::NX)
-                    hipLaunchKernelGGL((k_soc_tpi<DYN, Dyn<DYN>::NX>), grid, dim3(64), 0, s2, dP, dD, dW, ws.socl,
-                                       n_active, C + 6);
-                else
-                    hipLaunchKernelGGL((k_soc_tpi<DYN, (Dyn<DYN>::NX > 1 ? Dyn<DYN>::NX - 1 : 1)>), grid, dim3(64), 0, s2,
-                                       dP, dD, dW, ws.socl, n_active, C + 6);
-            } else {
-                hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per),
-                                   dim3(64), 0, s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
-            }
+            hipLaunchKernelGGL((k_ric<DYN, false, true>), dim3((n_active + ric_blocks_per - 1) / ric_blocks_per),
+                               dim3(64), 0, s2, dP, dD, dW, ws.socl, n_active, C + 6, (int)MODE_NEWTON, nullptr, 1 << 30);
             NLOT_HIP_CHECK(hipEventRecord(res.e_soc, s2));
             return NLOT_OK;
         };
@@ -5722,7 +4924,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             hipLaunchKernelGGL(k_admit, dim3(1), dim3(1024), 0, st, ws.act[cur], Cadm, ws.sinst, ws.freel,
                                ws.cnt + 2 * CSET, next_admit, n_new);
             hipLaunchKernelGGL(k_init_state, dim3(n_new), dim3(64), 0, st, dP, dD, o, ws, x0, xg, Xinit, ws.act[cur],
-                               Cadm + 13);
+                               Cadm);
             NLOT_HIP_CHECK(hipGetLastError());
             next_admit += n_new;
             n_active += n_new;

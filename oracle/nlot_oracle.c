@@ -18,9 +18,11 @@
  *   - analytic SDFs (circle, smooth square, union)              core/sdf/casadi.py:33-41,69-118,385-386
  *   - learned SDF (FourierMLP / naive MLP, fp32 like libtorch)  core/nn_architectures.py:30-72; gen/nn_sdf.cpp:57-104
  *   - IPOPT (external dependency, CasADi 3.7.0's bundled IPOPT, poetry.lock:90-91) is restated from its
- *     published algorithm (Waechter & Biegler 2006): primal-dual barrier method, monotone mu update,
- *     fraction-to-boundary rule, inertia-corrected Newton step, filter line search.  Deviations are
- *     listed in DESIGN.md §4 (no SOC / restoration / adaptive mu oracle).
+ *     published algorithm (Waechter & Biegler 2006): primal-dual barrier method, monotone and adaptive
+ *     (quality-function oracle) mu updates, fraction-to-boundary rule, inertia-corrected Newton step, filter
+ *     line search with second-order corrections, watchdog, tiny-step rule, filter reset, soft restoration and
+ *     the feasibility restoration phase (MinC_1Nrm); the bounds as Opti's constraint rows (general_bounds,
+ *     runner.py:67-69,101-103) or as variable bounds.  Deviations are listed in DESIGN.md §4.
  *
  * Derivatives use a small second-order forward-mode "jet" (value, gradient, Hessian), so this file is
  * an independent derivation from the hand-written derivatives of the HIP kernels.
