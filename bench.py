@@ -86,6 +86,10 @@ def parse():
                          "workspace holds the slots' state only, ABI v10)")
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
+    ap.add_argument("--bounds", choices=["rows", "variable"], default="rows",
+                    help="rows = the reference's NLP: the control bounds and slack >= 0 as constraint rows, the form "
+                         "CasADi's Opti hands IPOPT (runner.py:67-69,101-103; NlotSolverOptions.general_bounds = 1); "
+                         "variable = the same bounds as variable bounds (the GPU's form before round 5)")
     return ap.parse_args()
 
 
@@ -182,6 +186,7 @@ def main():
     x0, xg = batches[a.warmup]  # the first timed batch (CPU baseline sample)
     opt = _abi.gpu_options() if a.mu_strategy == "adaptive" else \
         _abi.gpu_options(mu_strategy=0, barrier_tol_factor=10.0)
+    opt.general_bounds = 1 if a.bounds == "rows" else 0
 
     from nlotrajectories_amd.solver import workspace_bytes
 
@@ -292,6 +297,7 @@ def main():
     iters_solved = [x["iters"][x["status"] == 0].float().mean().item() for x in results if (x["status"] == 0).any()]
     # pooled over the K distinct timed batches of rank 0
     status_counts = torch.bincount(st_all, minlength=len(_abi.STATUS_NAMES)).cpu().numpy().tolist()
+    inst_iters = float(it_all.sum().item())  # rank 0's instance-iterations in the timed region
     q = torch.quantile(it_all, torch.tensor([0.5, 0.99], dtype=torch.float64, device=it_all.device)).cpu().tolist()
     rank_rows = gather_rank_rows([rank, t_solve["s"], q[0], q[1], float(it_all.max().item())] + status_counts, dev)
 
@@ -472,6 +478,9 @@ def main():
                             "metric NLP: unicycle_2nd, rect 0.2x0.08, N=50, rho=10, bounds +-1, "
                             "learned SDF FourierMLP 2-128-128-1 (artefact), linear init, IPOPT tol 1e-4",
                 "mu_strategy": a.mu_strategy,
+                "bounds": ("constraint rows (general_bounds = 1): opti.bounded(umin, U, umax) and slack >= 0 as IPOPT "
+                           "sees them from CasADi's Opti (runner.py:67-69,101-103), U and S free"
+                           if opt.general_bounds else "variable bounds on U and S (general_bounds = 0)"),
                 "instances_per_gpu": a.batch,
                 "global_batch": B_all,
                 "knots": prob.N + 1,
@@ -503,10 +512,24 @@ def main():
                 "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
                 "ric_ms_per_step": agg["ric_ms"] / max(a.steps, 1),
                 "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) / max(a.steps, 1),
+                "instance_iterations_rank0": inst_iters,
+                # SDF-MLP work per instance-iteration (DESIGN.md §8f cost model): points the value launches (line-search
+                # candidates, speculative ones included) and the full launches evaluate per accepted iteration
+                "value_mlp_points_per_instance_iteration": agg["mlp_points_value"] / max(inst_iters, 1.0),
+                "full_mlp_points_per_instance_iteration": agg["mlp_points_full"] / max(inst_iters, 1.0),
             },
             **rooflines,
             "cpu_baseline": cpu,
         }
+        if opt.general_bounds and not (stress or b6):  # the variable-bound form's figures, measured on the same tree
+            vf = os.path.join(ROOT, "profiles", "r05", "bench_varbounds.json")
+            if os.path.exists(vf):
+                with open(vf) as f:
+                    v = json.load(f)
+                line["config"]["variable_bounds_reference"] = {
+                    "value": v["value"], "status_counts_rank0": v["config"]["status_counts_rank0"],
+                    "mean_iters_solved": v["config"]["mean_iters_solved"], "source": os.path.relpath(vf, ROOT),
+                    "note": "the same command with --bounds variable (committed measurement, not this run)"}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

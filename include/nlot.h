@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 11
+#define NLOT_ABI_VERSION 12
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -159,9 +159,9 @@ typedef struct NlotSolverOptions {
     double resto_proximity_weight;           /* zeta = weight * sqrt(mu), weight 1 */
     double bound_mult_reset_threshold;       /* 1000 */
     double resto_failure_feasibility_threshold; /* 0 means 1e2 * tol (IPOPT default) */
-    int32_t general_bounds;      /* 1: the control bounds and slack >= 0 as constraint rows g(x) = U, g(x) = S with
-                                    bounded IPOPT slacks (CasADi Opti's form, runner.py:67-69,100-104); 0: variable
-                                    bounds.  CPU restatement only so far (oracle/); the GPU solver refuses 1 */
+    int32_t general_bounds;      /* 1 (default since ABI v12): the control bounds and slack >= 0 as constraint rows
+                                    g(x) = U, g(x) = S with bounded IPOPT slacks, U and S free — the NLP CasADi Opti
+                                    hands IPOPT (runner.py:67-69,101-103); 0: the same bounds as variable bounds */
     int32_t pad_gb_;
 } NlotSolverOptions;
 

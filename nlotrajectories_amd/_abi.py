@@ -94,7 +94,8 @@ def default_options(**kw) -> NlotSolverOptions:
                           tiny_step_tol=10 * 2.220446049250313e-16, tiny_step_y_tol=1e-2,
                           soft_resto_pderror_reduction_factor=0.9999, required_infeasibility_reduction=0.9,
                           resto_penalty_parameter=1000.0, resto_proximity_weight=1.0,
-                          bound_mult_reset_threshold=1000.0, resto_failure_feasibility_threshold=0.0)
+                          bound_mult_reset_threshold=1000.0, resto_failure_feasibility_threshold=0.0,
+                          general_bounds=1)
     for k, v in kw.items():
         setattr(o, k, v)
     return o

@@ -77,7 +77,7 @@ def lib():
     L.nlot_rrt_init.restype = C.c_int32
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 11:
+    if L.nlot_abi_version() != 12:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

@@ -44,6 +44,7 @@ extern "C" void nlot_default_options(NlotSolverOptions* o) {
     o->resto_proximity_weight = 1.0;
     o->bound_mult_reset_threshold = 1000.0;
     o->resto_failure_feasibility_threshold = 0.0;
+    o->general_bounds = 1;  // opti.bounded / subject_to(slack >= 0) as constraint rows (runner.py:67-69,101-103)
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -133,6 +133,10 @@ struct Dims {
     int N, nx, nu, ns, M, nc, nb, nv, sd;  // nv = nu + ns (stage k < N)
     int tidx[8];
     int ppk;  // SDF points per knot (corners, or 1 for a dot)
+    // general bounds (NlotSolverOptions.general_bounds): the control bounds and slack >= 0 as constraint rows, the way
+    // CasADi's Opti hands them to IPOPT (runner.py:67-69,101-103).  ngb = bound rows N nu + ns (N + 1) (the workspace
+    // always holds their arrays: the workspace size does not depend on the options); gcb = 1 selects the form
+    int ngb, gcb;
 };
 
 static Dims make_dims(const NlotProblem& p) {
@@ -149,6 +153,8 @@ static Dims make_dims(const NlotProblem& p) {
     for (int i = 0; i < p.nx; ++i)
         if (p.enforce_heading || i != 2) d.tidx[d.nc++] = i;
     d.ppk = d.nb;
+    d.ngb = p.N * p.nu + d.ns * (p.N + 1);
+    d.gcb = 0;  // run() sets it from the options
     return d;
 }
 
@@ -169,20 +175,21 @@ __host__ __device__ constexpr int slot_len(int nx, int nu) {
 }
 __host__ __device__ constexpr int hg_len(int nx, int nu) { return (nx + nu + 1) * (nx + nu + 3); }
 __host__ __device__ constexpr int vf_len(int nx, int nu) { return nx * (nx + 2 + nx); }
-// quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt
-__host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M) {
-    return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M;
+// quality-function oracle step buffers (affine / centering): dX dU dS yi yk yt | dT dzl dzu dzs dvt | dsb (the
+// bound rows' slack step, general bounds)
+__host__ __device__ constexpr int qf_len(int N, int nx, int nu, int M, int ngb) {
+    return (N + 1) * nx + N * nu + (N + 1) + nx + N * nx + 8 + (N + 1) * M + 2 * N * nu + (N + 1) + (N + 1) * M + ngb;
 }
 
-// an iterate (X U S T yi yk yt yd zl zu zs vt) or a step (dX dU dS dT yi_n yk_n yt_n yd_n dzl dzu dzs dvt):
-// the save areas of the second-order correction and the watchdog
-__host__ __device__ constexpr int it_len(int N, int nx, int nu, int M) {
-    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + 8;
+// an iterate (X U S T yi yk yt yd zl zu zs vt sb yb) or a step (dX dU dS dT yi_n yk_n yt_n yd_n dzl dzu dzs dvt dsb
+// yb_n): the save areas of the second-order correction and the watchdog
+__host__ __device__ constexpr int it_len(int N, int nx, int nu, int M, int ngb) {
+    return (N + 1) * nx + 3 * N * nu + 2 * (N + 1) + 3 * (N + 1) * M + nx + N * nx + 8 + 2 * ngb;
 }
 
-// restoration rows (oracle Sol::rp ...): [initial state nx][dynamics N nx][terminal nc][inequalities (N+1) M],
-// allocated with the terminal block padded to 8
-__host__ __device__ constexpr int ne_len(int N, int nx, int M) { return nx + N * nx + 8 + (N + 1) * M; }
+// restoration rows (oracle Sol::rp ...): [initial state nx][dynamics N nx][terminal nc][inequalities (N+1) M]
+// [bound rows ngb (general bounds)], allocated with the terminal block padded to 8
+__host__ __device__ constexpr int ne_len(int N, int nx, int M, int ngb) { return nx + N * nx + 8 + (N + 1) * M + ngb; }
 
 // a stored pivoted LDL^T factor of an n x n block (ldl_factor's in-place form, then the permutation): the Q_vv
 // factor of every stage and the terminal block's, kept by each Newton solve for the second-order corrections
@@ -196,14 +203,17 @@ __host__ __device__ constexpr int ldl_len(int n) { return n * n + n; }
     X_(rct, 8) X_(rcq, (N + 1) * M) X_(dX, (N + 1) * nx) X_(dU, N * nu) X_(dS, N + 1)                  \
     X_(dT, (N + 1) * M) X_(yi_n, nx) X_(yk_n, N * nx) X_(yt_n, 8) X_(yd_n, (N + 1) * M)                \
     X_(dzl, N * nu) X_(dzu, N * nu) X_(dzs, N + 1) X_(dvt, (N + 1) * M) X_(sc, SC_COUNT)               \
-    X_(filt, 2 * FILT_MAX) X_(afilt, 2 * FILT_MAX) X_(qa, qf_len(N, nx, nu, M)) X_(qc, qf_len(N, nx, nu, M))  \
+    X_(filt, 2 * FILT_MAX) X_(afilt, 2 * FILT_MAX) X_(qa, qf_len(N, nx, nu, M, ngb)) X_(qc, qf_len(N, nx, nu, M, ngb)) \
     X_(stg, (N + 1) * slot_len(nx, nu)) X_(hg, (N + 1) * hg_len(nx, nu)) X_(vf, (N + 1) * vf_len(nx, nu))   \
     X_(dX2, (N + 1) * nx) X_(dU2, N * nu) X_(dS2, N + 1) X_(yi2, nx) X_(yk2, N * nx) X_(yt2, 8)         \
-    X_(sts, it_len(N, nx, nu, M)) X_(rcs, nx + N * nx + 8 + (N + 1) * M) X_(wdi, it_len(N, nx, nu, M))       \
-    X_(wdd, it_len(N, nx, nu, M)) X_(rp, ne_len(N, nx, M)) X_(rn, ne_len(N, nx, M)) X_(rzp, ne_len(N, nx, M))     \
-    X_(rzn, ne_len(N, nx, M)) X_(rdp, ne_len(N, nx, M)) X_(rdn, ne_len(N, nx, M)) X_(rdzp, ne_len(N, nx, M))      \
-    X_(rdzn, ne_len(N, nx, M)) X_(dsoft, ne_len(N, nx, M)) X_(esoft, ne_len(N, nx, M)) X_(rfilt, 2 * FILT_MAX)   \
-    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx)) X_(x0s, nx) X_(xgs, nx) X_(phi, N * nx * (nx + 2))
+    X_(sts, it_len(N, nx, nu, M, ngb)) X_(rcs, nx + N * nx + 8 + (N + 1) * M + ngb)                     \
+    X_(wdi, it_len(N, nx, nu, M, ngb)) X_(wdd, it_len(N, nx, nu, M, ngb))                               \
+    X_(rp, ne_len(N, nx, M, ngb)) X_(rn, ne_len(N, nx, M, ngb)) X_(rzp, ne_len(N, nx, M, ngb))           \
+    X_(rzn, ne_len(N, nx, M, ngb)) X_(rdp, ne_len(N, nx, M, ngb)) X_(rdn, ne_len(N, nx, M, ngb))         \
+    X_(rdzp, ne_len(N, nx, M, ngb)) X_(rdzn, ne_len(N, nx, M, ngb)) X_(dsoft, ne_len(N, nx, M, ngb))     \
+    X_(esoft, ne_len(N, nx, M, ngb)) X_(rfilt, 2 * FILT_MAX)                                            \
+    X_(qfac, (N + 1) * ldl_len(nu + 1)) X_(tfac, ldl_len(nx)) X_(x0s, nx) X_(xgs, nx) X_(phi, N * nx * (nx + 2)) \
+    X_(sb, ngb) X_(yb, ngb) X_(rcb, ngb) X_(dsb, ngb) X_(yb_n, ngb)
 
 struct Ws {
 #define NLOT_DECL(name, cnt) \
@@ -242,7 +252,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // doubles of all instance-major arrays for B instances, each array rounded up to 256 bytes
 static size_t ws_doubles(const Dims& d, int64_t B) {
-    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M;
+    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M, ngb = d.ngb;
     size_t n = 0;
 #define NLOT_CNT(name, cnt) n += ((size_t)(cnt) * (size_t)B + 31) & ~(size_t)31;
     NLOT_WS_ARRAYS(NLOT_CNT)
@@ -277,7 +287,7 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
     Ws w{};
     w.cap = B;
     w.ppk = d.ppk;
-    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M;
+    const int N = d.N, nx = d.nx, nu = d.nu, M = d.M, ngb = d.ngb;
     base = (char*)base + kHdr;
     double* q = (double*)base;
 #define NLOT_TAKE(name, cnt)          \
@@ -325,11 +335,21 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
 // element i of instance b's array (instance-major)
 #define AT(arr, i) (ws.arr[(size_t)b * ws.L_##arr + (i)])
 #define SC(i) AT(sc, i)
+// General bounds (Dims::gcb; oracle Sol::gcb): CasADi's Opti passes opti.bounded(umin, U, umax) and slack >= 0
+// (runner.py:67-69,101-103) to IPOPT as constraint rows d(x) = U_ki, d(x) = S_k, i.e. rows d(x) - sb = 0 whose slack
+// sb carries the bounds, with U and S free.  Bound row q: control q = k nu + i, then slack rows N nu + k.  The bounded
+// quantity of a row is sb (general bounds) or the variable itself (variable bounds); its bound multipliers live in
+// zl / zu (controls) and zs (slacks) in both forms.  BVU / BVS: the bounded value, BDU / BDS: its step.
+#define BVU(e) (dm.gcb ? AT(sb, (e)) : AT(U, (e)))
+#define BVS(k) (dm.gcb ? AT(sb, dm.N * dm.nu + (k)) : AT(S, (k)))
+#define BDU(e) (dm.gcb ? AT(dsb, (e)) : AT(dU, (e)))
+#define BDS(k) (dm.gcb ? AT(dsb, dm.N * dm.nu + (k)) : AT(dS, (k)))
 
 // save (to buf) or load (from buf) an iterate, a step, or the residual rows, lane-strided
-#define NLOT_ITER_ARRAYS(F_) F_(X) F_(U) F_(S) F_(T) F_(yi) F_(yk) F_(yt) F_(yd) F_(zl) F_(zu) F_(zs) F_(vt)
-#define NLOT_STEP_ARRAYS(F_) F_(dX) F_(dU) F_(dS) F_(dT) F_(yi_n) F_(yk_n) F_(yt_n) F_(yd_n) F_(dzl) F_(dzu) F_(dzs) F_(dvt)
-#define NLOT_RES_ARRAYS(F_) F_(rci) F_(rcd) F_(rct) F_(rcq)
+#define NLOT_ITER_ARRAYS(F_) F_(X) F_(U) F_(S) F_(T) F_(yi) F_(yk) F_(yt) F_(yd) F_(zl) F_(zu) F_(zs) F_(vt) F_(sb) F_(yb)
+#define NLOT_STEP_ARRAYS(F_) \
+    F_(dX) F_(dU) F_(dS) F_(dT) F_(yi_n) F_(yk_n) F_(yt_n) F_(yd_n) F_(dzl) F_(dzu) F_(dzs) F_(dvt) F_(dsb) F_(yb_n)
+#define NLOT_RES_ARRAYS(F_) F_(rci) F_(rcd) F_(rct) F_(rcq) F_(rcb)
 #define NLOT_IO(name)                                                              \
     {                                                                              \
         double* a_ = &AT(name, 0);                                                 \
@@ -615,22 +635,42 @@ struct Solver {
                     if (ia[q] != ib[q]) Pp[ib[q]][ia[q]] += v;
                 }
             }
+            // bound barriers: Sigma on the diagonal, the barrier gradient (affine in mu).  General bounds: the row
+            // d(x) - sb = 0 with sb's barrier eliminated (oracle bound_row): D = Sigma + dw, rhs = D rcb + grad barrier
             if (k < N)
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
-                    const double uv = AT(U, k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
-                    uu[i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
+                    const double uv = BVU(k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
+                    const double sig = AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
+                    if (dm.gcb) {
+                        uu[i] += sig + dw;
+                        gu[i] += (sig + dw) * AT(rcb, k * NU + i);
+                    } else {
+                        uu[i] += sig;
+                    }
                     gum[i] += -1.0 / sl + 1.0 / su;
                 }
             if (dm.ns) {
-                ss += AT(zs, k) / Sk;
-                gsm += -1.0 / Sk + kappa_d;
+                const double sv = BVS(k), sig = AT(zs, k) / sv;
+                if (dm.gcb) {
+                    ss += sig + dw;
+                    gs += (sig + dw) * AT(rcb, N * NU + k);
+                } else {
+                    ss += sig;
+                }
+                gsm += -1.0 / sv + kappa_d;
             }
-        } else {
+        } else {  // least squares: D = 1 on a bound row (general bounds), rhs -(z_L - z_U) either way
             if (k < N)
 #pragma unroll
-                for (int i = 0; i < NU; ++i) gu[i] += -AT(zl, k * NU + i) + AT(zu, k * NU + i);
-            if (dm.ns) gs += -AT(zs, k);
+                for (int i = 0; i < NU; ++i) {
+                    gu[i] += -AT(zl, k * NU + i) + AT(zu, k * NU + i);
+                    if (dm.gcb) uu[i] += 1.0;
+                }
+            if (dm.ns) {
+                gs += -AT(zs, k);
+                if (dm.gcb) ss += 1.0;
+            }
         }
         // eliminated inequality slacks t:  H += J' D J, g += J' rhs, J = (d d_j/d pose, 1 on the slack)
         for (int j = 0; j < M; ++j) {
@@ -843,16 +883,31 @@ struct Solver {
                 if (ia[q] != ib[q]) Pp[ib[q]][ia[q]] += v;
             }
         }
+        // bound barriers; general bounds: the bound row with sb, p and n eliminated (bound_row_resto)
         if (k < N)
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                const double uv = AT(U, k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
-                uu[i] += AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su;
-                gu[i] += -mu / sl + mu / su;
+                const double uv = BVU(k * NU + i), sl = uv - p.umin[i], su = p.umax[i] - uv;
+                const double sig = AT(zl, k * NU + i) / sl + AT(zu, k * NU + i) / su, bg = -mu / sl + mu / su;
+                if (dm.gcb) {
+                    double Db;
+                    gu[i] += bound_row_resto(dm, ws, b, k * NU + i, sig, bg, dw, mu, &Db);
+                    uu[i] += Db;
+                } else {
+                    uu[i] += sig;
+                    gu[i] += bg;
+                }
             }
         if (dm.ns) {
-            ss += AT(zs, k) / Sk;
-            gs += -mu / Sk + kappa_d * mu;
+            const double sv = BVS(k), sig = AT(zs, k) / sv, bg = -mu / sv + kappa_d * mu;
+            if (dm.gcb) {
+                double Db;
+                gs += bound_row_resto(dm, ws, b, N * NU + k, sig, bg, dw, mu, &Db);
+                ss += Db;
+            } else {
+                ss += sig;
+                gs += bg;
+            }
         }
         const int q0 = NX + N * NX + nc;  // first inequality row
         for (int j = 0; j < M; ++j) {
@@ -910,6 +965,21 @@ struct Solver {
         };
         if (k < N) emit(std::true_type{});
         else emit(std::false_type{});
+    }
+
+    // general bounds in the restoration problem (oracle bound_row, resto branch): bound row q with its slack sb (barrier
+    // Hessian sig, gradient bg) and its p, n eliminated like an inequality row's t, p, n: D = 1 / C, rhs = (r - E) / C,
+    // C = 1/(sig + dw) + 1/(zp/p + dw) + 1/(zn/n + dw), r = rcb (c - p + n); returns rhs, D in *Dq
+    __device__ __forceinline__ static double bound_row_resto(const Dims& dm, const Ws& ws, int b, int q, double sig,
+                                                             double bg, double dw, double mu, double* Dq) {
+        const double kappa_d = 1e-5, rho = SC(SC_RHO);
+        const int r = NX + dm.N * NX + dm.nc + (dm.N + 1) * dm.M + q;
+        const double pp = AT(rp, r), nn = AT(rn, r);
+        const double st = sig + dw, sp = AT(rzp, r) / pp + dw, sn = AT(rzn, r) / nn + dw;
+        const double C = 1.0 / st + 1.0 / sp + 1.0 / sn;
+        const double E = -bg / st + (mu / pp - rho - kappa_d * mu) / sp - (mu / nn - rho - kappa_d * mu) / sn;
+        *Dq = 1.0 / C;
+        return (AT(rcb, q) - E) / C;
     }
 
     // the soft equality rows' compliance and offset (oracle build(), resto branch) for delta_w dw, rows lane.. by
@@ -1071,7 +1141,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     if (mode == MODE_LSQ && (int)SC(SC_PHASE) != PH_INIT) return;
     typename R::Sh& sh = shg[grp];
     const int N = dm.N, nc = dm.nc, ns = dm.ns;
-    const double mu0 = SC(SC_RMU0), mu1 = SC(SC_RMU1), last_dw = SC(SC_DWLAST);
+    const double mu0 = SC(SC_RMU0), last_dw = SC(SC_DWLAST);
     const int nr = (int)SC(SC_RNR);
     double* SL = &AT(stg, 0);
     const int j = l;  // QE column of this lane
@@ -1670,7 +1740,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 
     // delta_w enters the stage matrices linearly: H(dw) = H(0) + dw (I_nz + sum_q Jx_q Jx_q'),
     // g(dw) = g(0) + dw sum_q Jx_q c_q, with Jx_q = (d d_q/d pose, 1 on the slack when it enters d_q) and
-    // c_q = rcq (stage(): D_q = v/t + dw).  A retry adds (dw_new - dw_old) times that to hg in place.
+    // c_q = rcq (stage(): D_q = v/t + dw); general bounds add dw e_b e_b' and dw e_b rcb_b per bound row b (D_b = Sigma_b
+    // + dw on the control / slack column).  A retry adds (dw_new - dw_old) times that to hg in place.
     auto add_dw = [&](double ddw) {
         const int M = dm.M, sd = dm.sd;
         const bool hs = ns != 0;
@@ -1678,6 +1749,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             double* o = &AT(hg, k * HG);
             const int is = k < N ? NX + NU : NX, nz = is + (hs ? 1 : 0);
             for (int i = 0; i < nz; ++i) o[i * (NZ + 2) + i] += ddw;
+            if (dm.gcb) {  // bound rows: the control columns (k < N) and the slack column
+                for (int i = NX; i < nz; ++i) {
+                    const int qb = i < is ? k * NU + (i - NX) : N * NU + k;
+                    const double r = ddw * AT(rcb, qb);
+                    o[i * (NZ + 2) + i] += ddw;
+                    o[i * (NZ + 2) + NZ] += r;
+                    if (nr > 1) o[i * (NZ + 2) + NZ + 1] += r;
+                }
+            }
             for (int qq = 0; qq < M; ++qq) {
                 double J[3];
 #pragma unroll
@@ -1746,6 +1826,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 if (sd) {
                     o[is * (NZ + 2) + is] += dD;
                     o[is * (NZ + 2) + NZ] += dg;
+                }
+            }
+            if (dm.gcb) {  // bound rows (sb, p, n eliminated): the differences of D and rhs on their columns
+                for (int i = NX; i < nz; ++i) {
+                    const int qb = i < is ? k * NU + (i - NX) : N * NU + k;
+                    double sig, bg, D0, D1;
+                    if (i < is) {
+                        const double lo = p.umin[i - NX], hi = p.umax[i - NX], uv = BVU(qb);
+                        sig = AT(zl, qb) / (uv - lo) + AT(zu, qb) / (hi - uv);
+                        bg = -mu0 / (uv - lo) + mu0 / (hi - uv);
+                    } else {
+                        const double sv = BVS(k);
+                        sig = AT(zs, k) / sv;
+                        bg = -mu0 / sv + kappa_d * mu0;
+                    }
+                    const double r0 = SV::bound_row_resto(dm, ws, b, qb, sig, bg, dw_old, mu0, &D0);
+                    const double r1 = SV::bound_row_resto(dm, ws, b, qb, sig, bg, dw_new, mu0, &D1);
+                    o[i * (NZ + 2) + i] += D1 - D0;
+                    o[i * (NZ + 2) + NZ] += r1 - r0;
                 }
             }
             if (k < N)
@@ -2109,15 +2208,27 @@ static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __r
         const double lo = p.umin[i], hi = p.umax[i];
         const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
         const double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
-        AT(U, e) = fmin(fmax(0.0, lo + pl), hi - pu);
+        const double pushed = fmin(fmax(0.0, lo + pl), hi - pu);
+        // general bounds: U is free (Opti's initial value 0) and its row slack starts pushed into the bounds
+        AT(U, e) = dm.gcb ? 0.0 : pushed;
         AT(zl, e) = 1.0;
         AT(zu, e) = 1.0;
         AT(dU, e) = 0.0;
+        if (dm.gcb) {
+            AT(sb, e) = pushed;
+            AT(yb, e) = 0.0;
+            AT(dsb, e) = 0.0;
+        }
     }
     for (int k = lane; k <= N; k += 64) {
-        AT(S, k) = dm.ns ? fmax(0.0, k1) : 0.0;
+        AT(S, k) = (dm.ns && !dm.gcb) ? fmax(0.0, k1) : 0.0;
         AT(zs, k) = 1.0;
         AT(dS, k) = 0.0;
+        if (dm.gcb && dm.ns) {  // slack_bound_push of the row d(x0) = S_k = 0
+            AT(sb, N * nu + k) = fmax(0.0, k1);
+            AT(yb, N * nu + k) = 0.0;
+            AT(dsb, N * nu + k) = 0.0;
+        }
     }
     for (int q = lane; q < (N + 1) * M; q += 64) {
         AT(vt, q) = 1.0;
@@ -2464,11 +2575,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
         wsync();
     };
+    const int ngb = dm.gcb ? dm.ngb : 0;  // bound rows (general bounds)
     auto zero_mults = [&]() {
         for (int i = lane; i < NX; i += 64) AT(yi, i) = 0;
         for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0;
         for (int i = lane; i < nc; i += 64) AT(yt, i) = 0;
         for (int q = lane; q < (N + 1) * M; q += 64) AT(yd, q) = 0;
+        for (int q = lane; q < ngb; q += 64) AT(yb, q) = 0;
     };
 
     const double mu0 = SC(SC_MU);
@@ -2504,6 +2617,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
             for (int i = lane; i < NX; i += 64) ymax = fmax(ymax, fabs(AT(yi, i) = AT(yi_n, i)));
             for (int i = lane; i < N * NX; i += 64) ymax = fmax(ymax, fabs(AT(yk, i) = AT(yk_n, i)));
             for (int i = lane; i < nc; i += 64) ymax = fmax(ymax, fabs(AT(yt, i) = AT(yt_n, i)));
+            // bound rows: y = J dz - (z_L - z_U), J the unit vector of the control / slack
+            for (int q = lane; q < ngb; q += 64) {
+                const double v = q < N * NU ? AT(dU, q) - (AT(zl, q) - AT(zu, q)) : AT(dS, q - N * NU) - AT(zs, q - N * NU);
+                AT(yb, q) = v;
+                ymax = fmax(ymax, fabs(v));
+            }
             ymax = wmax(ymax);
             wsync();
             if (ymax > o.constr_mult_init_max) zero_mults();
@@ -2529,6 +2648,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     }
     chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(dv, q); v[1] = AT(T, q); },
                          [&](int q, const double* v) { AT(rcq, q) = v[0] - v[1]; });
+    for (int q = lane; q < ngb; q += 64)  // bound rows U - sb, S - sb
+        AT(rcb, q) = (q < N * NU ? AT(U, q) : AT(S, q - N * NU)) - AT(sb, q);
     wsync();
 
     // the lane-strided sums below run through chunked_update (loads of 4 rows first, then the same per-lane order)
@@ -2544,17 +2665,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                                  bar += log(v[1]);
                                  lin += v[1];
                              });
-        chunked_update<4, 1>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); },
+        chunked_update<4, 1>(N * NU, lane, [&](int e, double* v) { v[0] = BVU(e); },
                              [&](int e, const double* v) {
                                  const double u = v[0];
                                  bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
                              });
         if (dm.ns)
-            chunked_update<4, 1>(N + 1, lane, [&](int k, double* v) { v[0] = AT(S, k); },
+            chunked_update<4, 1>(N + 1, lane, [&](int k, double* v) { v[0] = BVS(k); },
                                  [&](int, const double* v) {
                                      bar += log(v[0]);
                                      lin += v[0];
                                  });
+        chunked_update<4, 1>(ngb, lane, [&](int q, double* v) { v[0] = AT(rcb, q); }, tsum);
         *th = wsum(t);
         const double fo = objective_w(p, dm, ws, b, lane, 0.0);
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
@@ -2624,8 +2746,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
         if (k < N)
 #pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                double t = -AT(zl, k * NU + i) + AT(zu, k * NU + i);
+            for (int i = 0; i < NU; ++i) {  // general bounds: the bound row's multiplier instead of z_L, z_U
+                double t = dm.gcb ? AT(yb, k * NU + i) : -AT(zl, k * NU + i) + AT(zu, k * NU + i);
                 if (p.use_smooth && k < N - 1) t += 2.0 * p.smooth_weight * AT(U, k * NU + i);
 #pragma unroll
                 for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
@@ -2634,7 +2756,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                 d1 += fabs(t);
             }
         if (dm.ns) {
-            double t = 2.0 * p.slack_penalty * AT(S, k) - AT(zs, k);
+            double t = 2.0 * p.slack_penalty * AT(S, k) + (dm.gcb ? AT(yb, N * NU + k) : -AT(zs, k));
             if (dm.sd)
                 for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
             dual = fmax(dual, fabs(t));
@@ -2647,6 +2769,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
             dsq += t * t;
             d1 += fabs(t);
         }
+    }
+    for (int q = lane; q < ngb; q += 64) {  // bound-row slacks: -y - z_L + z_U
+        const double t = q < N * NU ? -AT(yb, q) - AT(zl, q) + AT(zu, q) : -AT(yb, q) - AT(zs, q - N * NU);
+        dual = fmax(dual, fabs(t));
+        dsq += t * t;
+        d1 += fabs(t);
     }
     auto pri_ = [&](double v) {
         primal = fmax(primal, fabs(v));
@@ -2663,6 +2791,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                              pri_(v[0]);
                              cviol = fmax(cviol, fmax(0.0, -v[1]));
                          });
+    for (int q = lane; q < ngb; q += 64) {  // bound rows: d(x) = U or S against its bounds
+        pri_(AT(rcb, q));
+        if (q < N * NU) {
+            const double u = AT(U, q);
+            cviol = fmax(cviol, fmax(0.0, fmax(p.umin[q % NU] - u, u - p.umax[q % NU])));
+        } else {
+            cviol = fmax(cviol, fmax(0.0, -AT(S, q - N * NU)));
+        }
+    }
     auto compl_ = [&](double z, double s) {
         c0 = fmax(c0, fabs(z * s));
         cmu = fmax(cmu, fabs(z * s - mu0));
@@ -2670,19 +2807,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         zsum += fabs(z);
         nzc += 1;
     };
-    chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
+    chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = BVU(e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
                          [&](int e, const double* v) {
                              compl_(v[1], v[0] - p.umin[e % NU]);
                              compl_(v[2], p.umax[e % NU] - v[0]);
                          });
     auto compl2 = [&](int, const double* v) { compl_(v[0], v[1]); };
-    if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = AT(S, k); }, compl2);
+    if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = BVS(k); }, compl2);
     chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); }, compl2);
     auto ysum1 = [&](int, const double* v) { ysum += fabs(v[0]); };
     chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(yi, i); }, ysum1);
     chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(yk, i); }, ysum1);
     chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(yt, i); }, ysum1);
     chunked_update<4, 1>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(yd, q); }, ysum1);
+    chunked_update<4, 1>(ngb, lane, [&](int q, double* v) { v[0] = AT(yb, q); }, ysum1);
     dual = wmax(dual);
     primal = wmax(primal);
     cviol = wmax(cviol);
@@ -2693,22 +2831,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     nzc = wsum(nzc);
     const double csum_w = wsum(csum), dsq_w = wsum(dsq), psq_w = wsum(psq);
     const double d1_w = wsum(d1), p1_w = wsum(p1);
-    const double ny = NX + N * NX + nc + (N + 1) * M;
+    const double ny = NX + N * NX + nc + (N + 1) * M + ngb;
     const double sd = fmax(100.0, (ysum + zsum) / (ny + nzc)) / 100.0;
     const double scc = fmax(100.0, zsum / nzc) / 100.0;
     const double E0 = fmax(fmax(dual / sd, primal), c0 / scc);
     // IPOPT's primal-dual system error at barrier parameter m (soft restoration): sum of the 1-norms of the dual,
     // primal and complementarity residuals over the element count
-    const double n_pd = (double)((N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M) +
-                        (double)(NX + nc + N * NX + (N + 1) * M) + nzc;
+    const double n_pd = (double)((N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M + ngb) +
+                        (double)(NX + nc + N * NX + (N + 1) * M + ngb) + nzc;
     auto pd_error = [&](double m) {
         double c1 = 0;
         for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
+            const double u = BVU(e);
             c1 += fabs(AT(zl, e) * (u - p.umin[e % NU]) - m) + fabs(AT(zu, e) * (p.umax[e % NU] - u) - m);
         }
         if (dm.ns)
-            for (int k = lane; k <= N; k += 64) c1 += fabs(AT(zs, k) * AT(S, k) - m);
+            for (int k = lane; k <= N; k += 64) c1 += fabs(AT(zs, k) * BVS(k) - m);
         for (int q = lane; q < (N + 1) * M; q += 64) c1 += fabs(AT(vt, q) * AT(T, q) - m);
         return (d1_w + p1_w + wsum(c1)) / n_pd;
     };
@@ -2755,13 +2893,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     bool reset_filter = false;
     auto compl_mu = [&](double m) {
         double cm = 0;
-        chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
+        chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = BVU(e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
                              [&](int e, const double* v) {
                                  cm = fmax(cm, fabs(v[1] * (v[0] - p.umin[e % NU]) - m));
                                  cm = fmax(cm, fabs(v[2] * (p.umax[e % NU] - v[0]) - m));
                              });
         auto cm2 = [&](int, const double* v) { cm = fmax(cm, fabs(v[0] * v[1] - m)); };
-        if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = AT(S, k); }, cm2);
+        if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = BVS(k); }, cm2);
         chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); }, cm2);
         return wmax(cm);
     };
@@ -2922,8 +3060,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     const double dw = SC(SC_DW), avg = SC(SC_AVG), dsq_w = SC(SC_DSQ), psq_w = SC(SC_PSQ), nzc = SC(SC_NZC);
     const bool use_qf = SC(SC_USEQF) != 0.0;
     double mu = SC(SC_MU), tau = SC(SC_TAU);
-    const int n_dual_ = (N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M;
-    const int n_pri_ = NX + dm.nc + N * NX + (N + 1) * M;
+    const int ngb = dm.gcb ? dm.ngb : 0;  // bound rows (general bounds)
+    const int n_dual_ = (N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M + ngb;
+    const int n_pri_ = NX + dm.nc + N * NX + (N + 1) * M + ngb;
     const int nc = dm.nc;
     constexpr double kMuMin = 1e-11;
     (void)o;
@@ -2938,14 +3077,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             lin += AT(T, q);
         }
         for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
+            const double u = BVU(e);
             bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
         }
         if (dm.ns)
             for (int k = lane; k <= N; k += 64) {
-                bar += log(AT(S, k));
-                lin += AT(S, k);
+                bar += log(BVS(k));
+                lin += BVS(k);
             }
+        for (int q = lane; q < ngb; q += 64) t += fabs(AT(rcb, q));
         *th = wsum(t);
         const double fo = objective_w(p, dm, ws, b, lane, 0.0);
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
@@ -2955,7 +3095,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     // centering minus affine (qc)
     {
         const int oU = (N + 1) * NX, oS = oU + N * NU, oyi = oS + N + 1, oyk = oyi + NX, oyt = oyk + N * NX,
-                  oT = oyt + 8, ozl = oT + (N + 1) * M, ozu = ozl + N * NU, ozs = ozu + N * NU, ovt = ozs + N + 1;
+                  oT = oyt + 8, ozl = oT + (N + 1) * M, ozu = ozl + N * NU, ozs = ozu + N * NU, ovt = ozs + N + 1,
+                  odb = ovt + (N + 1) * M;
+        // the steps of the bounded quantities: the bound rows' slacks (general bounds) or U and S
+        const int oBU = dm.gcb ? odb : oU, oBS = dm.gcb ? odb + N * NU : oS;
         // store the Riccati outputs and the recovered slack/dual steps at barrier parameter m (cen: minus aff)
         // (cen: the second right-hand side's arrays dX2 ...)
         auto qf_store = [&](double m, bool cen) {
@@ -2984,15 +3127,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
                     put(oT + q, dt_);
                     put(ovt + q, m / t - v - (v / t) * dt_);
                 }
-                if (dm.ns) {
-                    const double sk = AT(S, k);
-                    put(ozs + k, m / sk - AT(zs, k) - (AT(zs, k) / sk) * sS[k]);
+                if (dm.ns) {  // general bounds: the row slack's step d_sb = dS + rcb
+                    const double sk = BVS(k), ds = dm.gcb ? sS[k] + AT(rcb, N * NU + k) : sS[k];
+                    put(ozs + k, m / sk - AT(zs, k) - (AT(zs, k) / sk) * ds);
+                    if (dm.gcb) put(odb + N * NU + k, ds);
                 }
             }
             for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = sU[e];
+                const double u = BVU(e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u;
+                const double du = dm.gcb ? sU[e] + AT(rcb, e) : sU[e];
                 put(ozl + e, m / sl - AT(zl, e) - (AT(zl, e) / sl) * du);
                 put(ozu + e, m / su - AT(zu, e) + (AT(zu, e) / su) * du);
+                if (dm.gcb) put(odb + e, du);
             }
             wsync();
         };
@@ -3028,7 +3174,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             for (int h = 0; h < 2; ++h) {
                 const int e = lane + 64 * h;
                 if (e < N * NU) {
-                    const double u = AT(U, e), da = qa_[oU + e], dc = qc_[oU + e];
+                    const double u = BVU(e), da = qa_[oBU + e], dc = qc_[oBU + e];
                     put(2 * h, u - p.umin[e % NU], da, dc, AT(zl, e), qa_[ozl + e], qc_[ozl + e]);
                     put(2 * h + 1, p.umax[e % NU] - u, -da, -dc, AT(zu, e), qa_[ozu + e], qc_[ozu + e]);
                 } else {
@@ -3036,7 +3182,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
                     none(2 * h + 1);
                 }
             }
-            if (dm.ns && lane <= N) put(4, AT(S, lane), qa_[oS + lane], qc_[oS + lane], AT(zs, lane), qa_[ozs + lane],
+            if (dm.ns && lane <= N) put(4, BVS(lane), qa_[oBS + lane], qc_[oBS + lane], AT(zs, lane), qa_[ozs + lane],
                                         qc_[ozs + lane]);
             else none(4);
             if (lane < (N + 1) * M) put(5, AT(T, lane), qa_[oT + lane], qc_[oT + lane], AT(vt, lane), qa_[ovt + lane],
@@ -3066,7 +3212,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             }
             double ap = 1.0, ad = 1.0;
             for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e), du = qa_[oU + e] + sig * qc_[oU + e];
+                const double u = BVU(e), du = qa_[oBU + e] + sig * qc_[oBU + e];
                 ap = frac_to_bound(u - p.umin[e % NU], du, tq, ap);
                 ap = frac_to_bound(p.umax[e % NU] - u, -du, tq, ap);
                 ad = frac_to_bound(AT(zl, e), qa_[ozl + e] + sig * qc_[ozl + e], tq, ad);
@@ -3074,7 +3220,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             }
             if (dm.ns)
                 for (int k = lane; k <= N; k += 64) {
-                    ap = frac_to_bound(AT(S, k), qa_[oS + k] + sig * qc_[oS + k], tq, ap);
+                    ap = frac_to_bound(BVS(k), qa_[oBS + k] + sig * qc_[oBS + k], tq, ap);
                     ad = frac_to_bound(AT(zs, k), qa_[ozs + k] + sig * qc_[ozs + k], tq, ad);
                 }
             for (int q = lane; q < (N + 1) * M; q += 64) {
@@ -3089,13 +3235,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
                 csq += c * c;
             };
             for (int e = lane; e < N * NU; e += 64) {
-                const double u = AT(U, e), du = qa_[oU + e] + sig * qc_[oU + e];
+                const double u = BVU(e), du = qa_[oBU + e] + sig * qc_[oBU + e];
                 cq(u - p.umin[e % NU], du, AT(zl, e), qa_[ozl + e] + sig * qc_[ozl + e]);
                 cq(p.umax[e % NU] - u, -du, AT(zu, e), qa_[ozu + e] + sig * qc_[ozu + e]);
             }
             if (dm.ns)
                 for (int k = lane; k <= N; k += 64)
-                    cq(AT(S, k), qa_[oS + k] + sig * qc_[oS + k], AT(zs, k), qa_[ozs + k] + sig * qc_[ozs + k]);
+                    cq(BVS(k), qa_[oBS + k] + sig * qc_[oBS + k], AT(zs, k), qa_[ozs + k] + sig * qc_[ozs + k]);
             for (int q = lane; q < (N + 1) * M; q += 64)
                 cq(AT(T, q), qa_[oT + q] + sig * qc_[oT + q], AT(vt, q), qa_[ovt + q] + sig * qc_[ovt + q]);
             csq = wsum(csq);
@@ -3231,12 +3377,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
             gd += (-mu / t + kappa_d * mu) * dt_;
         }
         if (dm.ns) {
-            const double s = AT(S, k), ds = AT(dS, k);
-            const double dzs_ = mu / s - AT(zs, k) - (AT(zs, k) / s) * ds;
-            AT(dzs, k) = dzs_;
-            amax = frac_to_bound(s, ds, tau, amax);
-            az = frac_to_bound(AT(zs, k), dzs_, tau, az);
-            gd += (2.0 * p.slack_penalty * s - mu / s + kappa_d * mu) * ds;
+            if (dm.gcb) {  // the bound row S - sb: sb's step, the row multiplier (oracle recover)
+                const int qb = N * NU + k;
+                const double s = AT(S, k), ds = AT(dS, k), sv = AT(sb, qb), db = ds + AT(rcb, qb);
+                const double sig = AT(zs, k) / sv, bg = -mu / sv + kappa_d * mu;
+                const double dzs_ = mu / sv - AT(zs, k) - sig * db;
+                AT(dsb, qb) = db;
+                AT(yb_n, qb) = (sig + dw) * db + bg;
+                AT(dzs, k) = dzs_;
+                amax = frac_to_bound(sv, db, tau, amax);
+                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                gd += 2.0 * p.slack_penalty * s * ds + bg * db;
+            } else {
+                const double s = AT(S, k), ds = AT(dS, k);
+                const double dzs_ = mu / s - AT(zs, k) - (AT(zs, k) / s) * ds;
+                AT(dzs, k) = dzs_;
+                amax = frac_to_bound(s, ds, tau, amax);
+                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                gd += (2.0 * p.slack_penalty * s - mu / s + kappa_d * mu) * ds;
+            }
         }
         for (int seg = k - 1; seg <= k; ++seg) {  // path-length gradient . dx_k
             if (seg < 0 || seg >= N) continue;
@@ -3249,6 +3408,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     }
     for (int e = lane; e < N * NU; e += 64) {
         const int i = e % NU, k = e / NU;
+        if (dm.gcb) {  // the bound row U - sb: sb's step d_sb = dU + rcb, the row multiplier (oracle recover)
+            const double u = AT(U, e), du = AT(dU, e), bv = AT(sb, e), sl = bv - p.umin[i], su = p.umax[i] - bv;
+            const double db = du + AT(rcb, e);
+            const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * db;
+            const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * db;
+            const double sig = AT(zl, e) / sl + AT(zu, e) / su, bg = -mu / sl + mu / su;
+            AT(dsb, e) = db;
+            AT(yb_n, e) = (sig + dw) * db + bg;
+            AT(dzl, e) = dzl_;
+            AT(dzu, e) = dzu_;
+            amax = frac_to_bound(sl, db, tau, amax);
+            amax = frac_to_bound(su, -db, tau, amax);
+            az = frac_to_bound(AT(zl, e), dzl_, tau, az);
+            az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+            if (p.use_smooth && k < N - 1) gd += 2.0 * p.smooth_weight * u * du;
+            gd += bg * db;
+            continue;
+        }
         const double u = AT(U, e), sl = u - p.umin[i], su = p.umax[i] - u, du = AT(dU, e);
         const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * du;
         const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * du;
@@ -3297,6 +3474,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         if (dm.ns)
             for (int k = lane; k <= N; k += 64) mx = fmax(mx, fabs(AT(dS, k)) / (1.0 + fabs(AT(S, k))));
         for (int q = lane; q < (N + 1) * M; q += 64) mx = fmax(mx, fabs(AT(dT, q)) / (1.0 + fabs(AT(T, q))));
+        for (int q = lane; q < ngb; q += 64) mx = fmax(mx, fabs(AT(dsb, q)) / (1.0 + fabs(AT(sb, q))));
         auto ystep = [&](double yn, double y) {
             my = fmax(my, fabs(yn - y));
             ya = fmax(ya, fabs(y));
@@ -3305,6 +3483,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         for (int i = lane; i < N * NX; i += 64) ystep(AT(yk_n, i), AT(yk, i));
         for (int i = lane; i < nc; i += 64) ystep(AT(yt_n, i), AT(yt, i));
         for (int q = lane; q < (N + 1) * M; q += 64) ystep(AT(yd_n, q), AT(yd, q));
+        for (int q = lane; q < ngb; q += 64) ystep(AT(yb_n, q), AT(yb, q));
         mx = wmax(mx);
         my = wmax(my);
         ya = wmax(ya);
@@ -3444,8 +3623,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                         th += fabs(c);
                         if (store) AT(rcd, k * NX + i) = keep * AT(rcd, k * NX + i) + c;
                     }
+                    if (dm.gcb) {  // bound rows U - sb, the barrier of sb
 #pragma unroll
-                    for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+                        for (int i = 0; i < NU; ++i) {
+                            const int qb = k * NU + i;
+                            const double sv = AT(sb, qb) + al * AT(dsb, qb), c = u[i] - sv;
+                            th += fabs(c);
+                            if (store) AT(rcb, qb) = keep * AT(rcb, qb) + c;
+                            bar += log(sv - p.umin[i]) + log(p.umax[i] - sv);
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+                    }
                 }
                 double d[MMAX];
                 knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
@@ -3459,8 +3649,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                     lin += t;
                 }
                 if (dm.ns) {
-                    bar += log(sk);
-                    lin += sk;
+                    if (dm.gcb) {  // bound row S - sb
+                        const int qb = N * NU + k;
+                        const double sv = AT(sb, qb) + al * AT(dsb, qb), c = sk - sv;
+                        th += fabs(c);
+                        if (store) AT(rcb, qb) = keep * AT(rcb, qb) + c;
+                        bar += log(sv);
+                        lin += sv;
+                    } else {
+                        bar += log(sk);
+                        lin += sk;
+                    }
                 }
             }
             *th_o = wsum(th);
@@ -3509,6 +3708,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             };
             chunked_update<4, 2>((N + 1) * NX, lane, [&](int i, double* v) { v[0] = AT(X, i); v[1] = AT(dX, i); },
                    [&](int i, const double* v) { AT(X, i) = v[0] + al * v[1]; });
+            if (dm.gcb) {  // general bounds: U and S free; the bound rows' slacks carry the bound multipliers
+                chunked_update<4, 2>(N * NU, lane, [&](int e, double* v) { v[0] = AT(U, e); v[1] = AT(dU, e); },
+                       [&](int e, const double* v) { AT(U, e) = v[0] + al * v[1]; });
+                if (dm.ns)
+                    chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(S, k); v[1] = AT(dS, k); },
+                           [&](int k, const double* v) { AT(S, k) = v[0] + al * v[1]; });
+                chunked_update<4, 4>(dm.ngb, lane,
+                       [&](int q, double* v) { v[0] = AT(sb, q); v[1] = AT(dsb, q); v[2] = AT(yb, q); v[3] = AT(yb_n, q); },
+                       [&](int q, const double* v) {
+                           const double sv = v[0] + al * v[1];
+                           AT(sb, q) = sv;
+                           AT(yb, q) = v[2] + al * (v[3] - v[2]);
+                           if (q < N * NU) {
+                               AT(zl, q) = zupd(AT(zl, q), AT(dzl, q), sv - p.umin[q % NU]);
+                               AT(zu, q) = zupd(AT(zu, q), AT(dzu, q), p.umax[q % NU] - sv);
+                           } else {
+                               AT(zs, q - N * NU) = zupd(AT(zs, q - N * NU), AT(dzs, q - N * NU), sv);
+                           }
+                       });
+            } else {
             chunked_update<4, 6>(N * NU, lane,
                    [&](int e, double* v) {
                        v[0] = AT(U, e); v[1] = AT(dU, e); v[2] = AT(zl, e); v[3] = AT(dzl, e); v[4] = AT(zu, e);
@@ -3527,6 +3746,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                            AT(S, k) = s_;
                            AT(zs, k) = zupd(v[2], v[3], s_);
                        });
+            }
             chunked_update<4, 6>((N + 1) * M, lane,
                    [&](int q, double* v) {
                        v[0] = AT(T, q); v[1] = AT(dT, q); v[2] = AT(vt, q); v[3] = AT(dvt, q); v[4] = AT(yd, q);
@@ -3754,14 +3974,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
 template <int DYN>
 struct Resto {
     static constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
+    // restoration rows: every equality row, the bound rows last (general bounds)
+    __device__ static int n_rows(const Dims& dm) {
+        return NX + dm.N * NX + dm.nc + (dm.N + 1) * dm.M + (dm.gcb ? dm.ngb : 0);
+    }
     // multiplier of restoration row i (the row's equality multiplier)
     __device__ static double yrow(const Dims& dm, const Ws& ws, int b, int i) {
-        const int rt = NX + dm.N * NX, rq = rt + dm.nc;
-        return i < NX ? AT(yi, i) : i < rt ? AT(yk, i - NX) : i < rq ? AT(yt, i - rt) : AT(yd, i - rq);
+        const int rt = NX + dm.N * NX, rq = rt + dm.nc, rb = rq + (dm.N + 1) * dm.M;
+        return i < NX ? AT(yi, i) : i < rt ? AT(yk, i - NX) : i < rq ? AT(yt, i - rt) : i < rb ? AT(yd, i - rq)
+                                                                                               : AT(yb, i - rb);
     }
     // sum over the rows of p + n, and of log p + log n (wave-reduced)
     __device__ static void pn_sums(const Dims& dm, const Ws& ws, int b, int lane, double al, double* lin, double* bar) {
-        const int ne = NX + dm.N * NX + dm.nc + (dm.N + 1) * dm.M;
+        const int ne = n_rows(dm);
         double l = 0, g = 0;
         for (int i = lane; i < ne; i += 64) {
             const double pp = AT(rp, i) + al * AT(rdp, i), nn = AT(rn, i) + al * AT(rdn, i);
@@ -3806,14 +4031,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
     if (ph != PH_RINIT && ph != PH_EVAL) return;
     const bool init = ph == PH_RINIT;
     const int N = dm.N, M = dm.M, nc = dm.nc, rank = (int)SC(SC_RANK);
-    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const int rt = NX + N * NX, rq = rt + nc, rb = rq + (N + 1) * M, ne = RS::n_rows(dm), ngb = ne - rb;
     const double kappa_d = 1e-5;
     const double* x0b = x0 + (size_t)b * NX;
     const double* xgb = xg + (size_t)b * NX;
     double* ori = &AT(wdi, 0);
     const int oU = ws.L_X, oS = oU + ws.L_U, oT = oS + ws.L_S, oyi = oT + ws.L_T, oyk = oyi + ws.L_yi,
               oyt = oyk + ws.L_yk, oyd = oyt + ws.L_yt, ozl = oyd + ws.L_yd, ozu = ozl + ws.L_zl, ozs = ozu + ws.L_zu,
-              ovt = ozs + ws.L_zs;
+              ovt = ozs + ws.L_zs, osb = ovt + ws.L_vt;
     (void)oyi; (void)oyk; (void)oyt; (void)oyd;
     // ---- evaluation at X: constraint values and Jacobians; the restoration multipliers weight Hd (0 at PH_RINIT)
     for (int k = lane; k <= N; k += 64) {
@@ -3847,9 +4072,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
         for (int i = 0; i < NX; ++i) AT(rcd, k * NX + i) = AT(X, (k + 1) * NX + i) - (x[i] + p.dt * f[i]);
     }
     for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) = AT(dv, q) - AT(T, q);
+    for (int q = lane; q < ngb; q += 64) AT(rcb, q) = (q < N * NU ? AT(U, q) : AT(S, q - N * NU)) - AT(sb, q);
     wsync();
     auto crow = [&](int i) {  // c of restoration row i
-        return i < NX ? AT(rci, i) : i < rt ? AT(rcd, i - NX) : i < rq ? AT(rct, i - rt) : AT(rcq, i - rq);
+        return i < NX ? AT(rci, i) : i < rt ? AT(rcd, i - NX) : i < rq ? AT(rct, i - rt) : i < rb ? AT(rcq, i - rq)
+                                                                                                 : AT(rcb, i - rb);
     };
     double th_o = 0, pinf = 0;
     for (int i = lane; i < ne; i += 64) {
@@ -3868,13 +4095,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             lin += AT(T, q);
         }
         for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
+            const double u = BVU(e);
             bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
         }
         if (dm.ns)
             for (int k = lane; k <= N; k += 64) {
-                bar += log(AT(S, k));
-                lin += AT(S, k);
+                bar += log(BVS(k));
+                lin += BVS(k);
             }
         return objective_w(p, dm, ws, b, lane, 0.0) - mu_o * wsum(bar) + kappa_d * mu_o * wsum(lin);
     };
@@ -3906,6 +4133,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
         for (int i = lane; i < NX; i += 64) AT(yi, i) = 0.0;
         for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0.0;
         for (int i = lane; i < 8; i += 64) AT(yt, i) = 0.0;
+        for (int q = lane; q < ngb; q += 64) AT(yb, q) = 0.0;
         wsync();
         // the restoration's theta_max / theta_min from its merit at the start (proximity term 0 at x_R)
         double th0 = 0;
@@ -3938,6 +4166,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
     for (int i = lane; i < N * NX; i += 64) AT(rcd, i) += -AT(rp, NX + i) + AT(rn, NX + i);
     for (int j = lane; j < nc; j += 64) AT(rct, j) += -AT(rp, rt + j) + AT(rn, rt + j);
     for (int q = lane; q < (N + 1) * M; q += 64) AT(rcq, q) += -AT(rp, rq + q) + AT(rn, rq + q);
+    for (int q = lane; q < ngb; q += 64) AT(rcb, q) += -AT(rp, rb + q) + AT(rn, rb + q);
     wsync();
     // ---- optimality measures of the restoration problem (oracle errors(), resto branch)
     double dual = 0, primal = 0, c0 = 0, cmu = 0, ysum = 0, zsum = 0, nzc = 0;
@@ -3984,14 +4213,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 const double ur = ori[oU + k * NU + i], dr = fmin(1.0, 1.0 / fabs(ur));
-                double t = zeta * dr * dr * (AT(U, k * NU + i) - ur) - AT(zl, k * NU + i) + AT(zu, k * NU + i);
+                double t = zeta * dr * dr * (AT(U, k * NU + i) - ur) +
+                           (dm.gcb ? AT(yb, k * NU + i) : -AT(zl, k * NU + i) + AT(zu, k * NU + i));
 #pragma unroll
                 for (int a = 0; a < NX; ++a) t -= Bu[a][i] * AT(yk, k * NX + a);
                 dual_(t);
             }
         if (dm.ns) {
             const double sr = ori[oS + k], dr = fmin(1.0, 1.0 / fabs(sr));
-            double t = zeta * dr * dr * (AT(S, k) - sr) - AT(zs, k);
+            double t = zeta * dr * dr * (AT(S, k) - sr) + (dm.gcb ? AT(yb, N * NU + k) : -AT(zs, k));
             if (dm.sd)
                 for (int j = 0; j < M; ++j) t += AT(yd, k * M + j);
             dual_(t);
@@ -4014,13 +4244,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
         ysum += fabs(y);
     }
     for (int e = lane; e < N * NU; e += 64) {
-        const double u = AT(U, e);
+        const double u = BVU(e);
         compl_(AT(zl, e), u - p.umin[e % NU]);
         compl_(AT(zu, e), p.umax[e % NU] - u);
     }
     if (dm.ns)
-        for (int k = lane; k <= N; k += 64) compl_(AT(zs, k), AT(S, k));
+        for (int k = lane; k <= N; k += 64) compl_(AT(zs, k), BVS(k));
     for (int q = lane; q < (N + 1) * M; q += 64) compl_(AT(vt, q), AT(T, q));
+    for (int q = lane; q < ngb; q += 64)  // bound-row slacks: -y - z_L + z_U
+        dual_(q < N * NU ? -AT(yb, q) - AT(zl, q) + AT(zu, q) : -AT(yb, q) - AT(zs, q - N * NU));
     dual = wmax(dual);
     primal = wmax(primal);
     c0 = wmax(c0);
@@ -4060,8 +4292,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             const double tau_o = SC(SC_RTAUO);
             double az = 1.0, zmax = 0;
             auto dz = [&](double z, double so, double sn) { return (mu_o - z * sn) / so; };
+            // the bounded quantities at x_R and now: U / S, or the bound rows' slacks (general bounds)
+            const int oBU = dm.gcb ? osb : oU, oBS = dm.gcb ? osb + N * NU : oS;
             for (int e = lane; e < N * NU; e += 64) {
-                const double lo = p.umin[e % NU], hi = p.umax[e % NU], uo = ori[oU + e], un = AT(U, e);
+                const double lo = p.umin[e % NU], hi = p.umax[e % NU], uo = ori[oBU + e], un = BVU(e);
                 AT(dzl, e) = dz(ori[ozl + e], uo - lo, un - lo);
                 AT(dzu, e) = dz(ori[ozu + e], hi - uo, hi - un);
                 az = frac_to_bound(ori[ozl + e], AT(dzl, e), tau_o, az);
@@ -4069,7 +4303,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             }
             if (dm.ns)
                 for (int k = lane; k <= N; k += 64) {
-                    AT(dzs, k) = dz(ori[ozs + k], ori[oS + k], AT(S, k));
+                    AT(dzs, k) = dz(ori[ozs + k], ori[oBS + k], BVS(k));
                     az = frac_to_bound(ori[ozs + k], AT(dzs, k), tau_o, az);
                 }
             for (int q = lane; q < (N + 1) * M; q += 64) {
@@ -4101,6 +4335,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             for (int i = lane; i < NX; i += 64) AT(yi, i) = 0.0;
             for (int i = lane; i < N * NX; i += 64) AT(yk, i) = 0.0;
             for (int i = lane; i < 8; i += 64) AT(yt, i) = 0.0;
+            for (int q = lane; q < ngb; q += 64) AT(yb, q) = 0.0;
             wsync();
             if (lane == 0) {  // k_iter_a (launched next) takes the instance's iteration from this evaluation
                 SC(SC_MU) = mu_o;
@@ -4142,12 +4377,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             cmx(AT(rzn, i), AT(rn, i));
         }
         for (int e = lane; e < N * NU; e += 64) {
-            const double u = AT(U, e);
+            const double u = BVU(e);
             cmx(AT(zl, e), u - p.umin[e % NU]);
             cmx(AT(zu, e), p.umax[e % NU] - u);
         }
         if (dm.ns)
-            for (int k = lane; k <= N; k += 64) cmx(AT(zs, k), AT(S, k));
+            for (int k = lane; k <= N; k += 64) cmx(AT(zs, k), BVS(k));
         for (int q = lane; q < (N + 1) * M; q += 64) cmx(AT(vt, q), AT(T, q));
         cmu = wmax(cm);
     }
@@ -4184,6 +4419,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     const Dims& dm = *dd_;
     const Ws& ws = *ws_;
     if (ws.prio) __builtin_amdgcn_s_setprio(2);  // NLOT_SETPRIO (see k_ric)
+    using SV = Solver<DYN>;
     using RS = Resto<DYN>;
     constexpr int NX = Dyn<DYN>::NX, NU = Dyn<DYN>::NU;
     const int lane = threadIdx.x, nlist = cnt[5];
@@ -4191,7 +4427,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     if (SC(SC_RESTO) == 0.0 || (int)SC(SC_RIC) != 2) return;
     (void)o;
     const int N = dm.N, M = dm.M, nc = dm.nc;
-    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const int rt = NX + N * NX, rq = rt + nc, rb = rq + (N + 1) * M, ne = RS::n_rows(dm);
     const double kappa_d = 1e-5, dw = SC(SC_DW), mu = SC(SC_MU), tau = SC(SC_TAU), rho = SC(SC_RHO),
                  zeta = SC(SC_ZETA);
     const double* ori = &AT(wdi, 0);
@@ -4237,11 +4473,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         }
         if (dm.ns) {
             const double s_ = AT(S, k), ds = AT(dS, k), sr = ori[oS + k], dr = fmin(1.0, 1.0 / fabs(sr));
-            const double dzs_ = mu / s_ - AT(zs, k) - (AT(zs, k) / s_) * ds;
-            AT(dzs, k) = dzs_;
-            amax = frac_to_bound(s_, ds, tau, amax);
-            az = frac_to_bound(AT(zs, k), dzs_, tau, az);
-            gd += (zeta * dr * dr * (s_ - sr) - mu / s_ + kappa_d * mu) * ds;
+            if (dm.gcb) {  // bound row S - sb with sb, p and n eliminated (oracle recover, resto branch)
+                const int qb = N * NU + k;
+                const double sv = AT(sb, qb), sig = AT(zs, k) / sv, bg = -mu / sv + kappa_d * mu;
+                double Db;
+                const double rhs = SV::bound_row_resto(dm, ws, b, qb, sig, bg, dw, mu, &Db);
+                const double yn = Db * ds + rhs, db = (yn - bg) / (sig + dw);
+                const double dzs_ = mu / sv - AT(zs, k) - sig * db;
+                AT(yb_n, qb) = yn;
+                AT(dsb, qb) = db;
+                AT(dzs, k) = dzs_;
+                pn_step(rb + qb, yn);
+                amax = frac_to_bound(sv, db, tau, amax);
+                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                gd += zeta * dr * dr * (s_ - sr) * ds + bg * db;
+            } else {
+                const double dzs_ = mu / s_ - AT(zs, k) - (AT(zs, k) / s_) * ds;
+                AT(dzs, k) = dzs_;
+                amax = frac_to_bound(s_, ds, tau, amax);
+                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                gd += (zeta * dr * dr * (s_ - sr) - mu / s_ + kappa_d * mu) * ds;
+            }
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
@@ -4253,6 +4505,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     for (int i = lane; i < N * NX; i += 64) pn_step(NX + i, AT(yk_n, i));
     for (int j = lane; j < nc; j += 64) pn_step(rt + j, AT(yt_n, j));
     for (int e = lane; e < N * NU; e += 64) {
+        if (dm.gcb) {  // bound row U - sb with sb, p and n eliminated (oracle recover, resto branch)
+            const double u = AT(U, e), du = AT(dU, e), ur = ori[oU + e], dr = fmin(1.0, 1.0 / fabs(ur));
+            const double sv = AT(sb, e), sl = sv - p.umin[e % NU], su = p.umax[e % NU] - sv;
+            const double sig = AT(zl, e) / sl + AT(zu, e) / su, bg = -mu / sl + mu / su;
+            double Db;
+            const double rhs = SV::bound_row_resto(dm, ws, b, e, sig, bg, dw, mu, &Db);
+            const double yn = Db * du + rhs, db = (yn - bg) / (sig + dw);
+            const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * db;
+            const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * db;
+            AT(yb_n, e) = yn;
+            AT(dsb, e) = db;
+            AT(dzl, e) = dzl_;
+            AT(dzu, e) = dzu_;
+            pn_step(rb + e, yn);
+            amax = frac_to_bound(sl, db, tau, amax);
+            amax = frac_to_bound(su, -db, tau, amax);
+            az = frac_to_bound(AT(zl, e), dzl_, tau, az);
+            az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+            gd += zeta * dr * dr * (u - ur) * du + bg * db;
+            continue;
+        }
         const double u = AT(U, e), sl = u - p.umin[e % NU], su = p.umax[e % NU] - u, du = AT(dU, e);
         const double ur = ori[oU + e], dr = fmin(1.0, 1.0 / fabs(ur));
         const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * du;
@@ -4280,14 +4553,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         lin += AT(T, q);
     }
     for (int e = lane; e < N * NU; e += 64) {
-        const double u = AT(U, e);
+        const double u = BVU(e);
         bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
     }
     if (dm.ns)
         for (int k = lane; k <= N; k += 64) {
-            bar += log(AT(S, k));
-            lin += AT(S, k);
+            bar += log(BVS(k));
+            lin += BVS(k);
         }
+    for (int q = lane; q < ne - rb; q += 64) th += fabs(AT(rcb, q));  // bound rows (c - p + n)
     double pn_lin, pn_bar;
     RS::pn_sums(dm, ws, b, lane, 0.0, &pn_lin, &pn_bar);
     const double theta = wsum(th);
@@ -4339,7 +4613,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
     if (SC(SC_RESTO) == 0.0 || (int)SC(SC_PHASE) != PH_LS) return;
     (void)o;
     const int N = dm.N, M = dm.M, nc = dm.nc;
-    const int rt = NX + N * NX, rq = rt + nc, ne = rq + (N + 1) * M;
+    const int rt = NX + N * NX, rq = rt + nc, rb = rq + (N + 1) * M, ne = RS::n_rows(dm);
     const double a0 = SC(SC_ALPHA), mu = SC(SC_MU), rho = SC(SC_RHO), kappa_d = 1e-5;
     const int rank0 = (int)SC(SC_RANK), ncand = (int)SC(SC_NCAND);
     const double* x0b = x0 + (size_t)b * NX;
@@ -4367,8 +4641,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
                 for (int i = 0; i < NX; ++i)
                     th += fabs(AT(X, (k + 1) * NX + i) + al * AT(dX, (k + 1) * NX + i) - (xk[i] + p.dt * f[i]) -
                                pr(NX + k * NX + i));
+                if (dm.gcb) {  // bound rows U - sb - p + n, the barrier of sb
 #pragma unroll
-                for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+                    for (int i = 0; i < NU; ++i) {
+                        const int qb = k * NU + i;
+                        const double sv = AT(sb, qb) + al * AT(dsb, qb);
+                        th += fabs(u[i] - sv - pr(rb + qb));
+                        bar += log(sv - p.umin[i]) + log(p.umax[i] - sv);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) bar += log(u[i] - p.umin[i]) + log(p.umax[i] - u[i]);
+                }
             }
             double d[MMAX];
             knot_eval(p, dm, ws, rank, k, xk, d, nullptr, nullptr, nullptr, tval);
@@ -4380,8 +4664,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
                 lin += t;
             }
             if (dm.ns) {
-                bar += log(sk);
-                lin += sk;
+                if (dm.gcb) {  // bound row S - sb - p + n
+                    const int qb = N * NU + k;
+                    const double sv = AT(sb, qb) + al * AT(dsb, qb);
+                    th += fabs(sk - sv - pr(rb + qb));
+                    bar += log(sv);
+                    lin += sv;
+                } else {
+                    bar += log(sk);
+                    lin += sk;
+                }
             }
         }
         double pn_lin, pn_bar;
@@ -4447,6 +4739,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
         return fmax(fmin(zn, ks * mu / sl), mu / (ks * sl));
     };
     for (int i = lane; i < (N + 1) * NX; i += 64) AT(X, i) += al * AT(dX, i);
+    if (dm.gcb) {  // U, S free; the bound rows' slacks and multipliers
+        for (int e = lane; e < N * NU; e += 64) AT(U, e) += al * AT(dU, e);
+        if (dm.ns)
+            for (int k = lane; k <= N; k += 64) AT(S, k) += al * AT(dS, k);
+        for (int q = lane; q < dm.ngb; q += 64) {
+            const double sv = AT(sb, q) + al * AT(dsb, q);
+            AT(sb, q) = sv;
+            AT(yb, q) += al * (AT(yb_n, q) - AT(yb, q));
+            if (q < N * NU) {
+                AT(zl, q) = zupd(AT(zl, q), AT(dzl, q), sv - p.umin[q % NU]);
+                AT(zu, q) = zupd(AT(zu, q), AT(dzu, q), p.umax[q % NU] - sv);
+            } else {
+                AT(zs, q - N * NU) = zupd(AT(zs, q - N * NU), AT(dzs, q - N * NU), sv);
+            }
+        }
+    } else {
     for (int e = lane; e < N * NU; e += 64) {
         const double u = AT(U, e) + al * AT(dU, e);
         AT(U, e) = u;
@@ -4459,6 +4767,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
             AT(S, k) = s_;
             AT(zs, k) = zupd(AT(zs, k), AT(dzs, k), s_);
         }
+    }
     for (int q = lane; q < (N + 1) * M; q += 64) {
         const double t = AT(T, q) + al * AT(dT, q);
         AT(T, q) = t;
@@ -4515,8 +4824,8 @@ static int validate(const NlotProblem* p, const NlotSolverOptions* o, const Nlot
         return NLOT_ERR_INVALID;
     }
     if (p->N < 2 || p->N > 4096 || p->dt <= 0) { set_error("N must be in [2, 4096], dt > 0"); return NLOT_ERR_INVALID; }
-    if (o->general_bounds) {
-        set_error("general_bounds = 1 (bounds as constraint rows) is implemented in the CPU restatement only");
+    if (o->general_bounds != 0 && o->general_bounds != 1) {
+        set_error("general_bounds: 0 variable bounds, 1 constraint rows (CasADi Opti's form)");
         return NLOT_ERR_INVALID;
     }
     if (p->integrator != NLOT_INTEG_EULER && p->integrator != NLOT_INTEG_RK4) {
@@ -4564,7 +4873,8 @@ template <int DYN>
 int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, const double* x0, const double* xg,
                const double* Xinit, double* X, double* U, double* S, double* cost, int32_t* status, int32_t* iters,
                int64_t B, void* workspace, hipStream_t st) {
-    const Dims dm = make_dims(p);
+    Dims dm = make_dims(p);
+    dm.gcb = o.general_bounds ? 1 : 0;
     const bool use_mlp = p.sdf_kind == NLOT_SDF_MLP;
     // slots: min(B, max_active) (continuous batching) or B; the workspace holds the slots' state only
     const int cap_slots = (int)(o.max_active > 0 && o.max_active < B ? o.max_active : B);

@@ -792,6 +792,7 @@ typedef struct {
     int resto, ne;
     int rej_filter, last_rej_filter, n_filt_rej, n_filt_resets; /* IPOPT filter reset heuristic (trigger 5, max 5) */
     int n_soc_tried, n_soc_acc;                                  /* second-order corrections started / accepted */
+    long n_trials; /* trial-point merit evaluations (one SDF value evaluation of the trial's corners each) */
     double rho, zeta;
     double *XR, *UR, *SR, *DRX, *DRU, *DRS; /* reference point and its proximity scaling */
     double *rp, *rn, *rzp, *rzn;            /* p, n and their bound multipliers */
@@ -2225,6 +2226,7 @@ static void trial_primal(const Sol* s, double a, Trial* t) {
 }
 static void trial_merit(const Sol* s, const Trial* t, double mu, double* th, double* ph, double* rci, double* rcd,
                         double* rct, double* rcq, double* rcb) {
+    ((Sol*)s)->n_trials++;
     if (s->resto) merit_resto(s, t->X, t->U, t->S, t->T, t->SB, t->P, t->N, mu, th, ph, rci, rcd, rct, rcq, rcb);
     else merit_r(s, t->X, t->U, t->S, t->T, t->SB, mu, th, ph, rci, rcd, rct, rcq, rcb);
 }
@@ -2480,6 +2482,18 @@ static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, 
     if (fc && atoi(fc) > 0 && atoi(fc) < s->fcap) s->fcap = atoi(fc);
 }
 
+/* Per-iteration trace (test infrastructure: oracle_solve_trace): the iterate (X, U) at the top of iteration it, i.e.
+ * the point a run with max_iter = it returns (inside a restoration phase: the restoration iterate, as the GPU solver
+ * reports it).  Thread-local, so parallel runs trace independently. */
+static __thread double* g_trace;
+static __thread int g_trace_cap;
+static void trace_rec(const Sol* s, int it, const double* X, const double* U) {
+    if (!g_trace || it < 0 || it >= g_trace_cap) return;
+    const size_t nX = (size_t)(s->N + 1) * s->nx, nU = (size_t)s->N * s->nu;
+    memcpy(g_trace + (size_t)it * (nX + nU), X, sizeof(double) * nX);
+    memcpy(g_trace + (size_t)it * (nX + nU) + nX, U, sizeof(double) * nU);
+}
+
 /* IPOPT MinC_1NrmRestorationPhase (Waechter & Biegler 2006 §3.3, IPOPT's documented defaults), run on the
  * restoration workspace r for the current point of s.  Returns 0 when it found a point acceptable to the
  * original filter (s then holds it: equality multipliers 0 as constr_mult_reset_threshold = 0, bound
@@ -2566,6 +2580,7 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
     for (;;) {
         eval_full(r);
         errors(r, &e);
+        trace_rec(s, *iter, r->X, r->U);
         double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
         if (!isfinite(E0)) {
             status = NLOT_NUMERIC;
@@ -2718,7 +2733,8 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
  * seen, [4] = final mu, [5] = E_0 (scaled overall error), [6] = restoration phases, [7] = watchdog /
  * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny),
  * [8] = theta (1-norm) at the last line-search failure, -1 if none, [9] / [10] = peak size of the line-search
- * (incl. restoration) / adaptive-mu filter, [11] / [12] = their forgotten entries (NLOT_ORACLE_FILT_CAP only).
+ * (incl. restoration) / adaptive-mu filter, [11] / [12] = their forgotten entries (NLOT_ORACLE_FILT_CAP only),
+ * [13] = trial-point merit evaluations (sequential line-search trials incl. corrections, soft and restoration steps).
  * info holds >= 16 doubles. */
 /* oracle_solve_one with an initial guess for the controls and slacks too (Uinit / Sinit, NULL = the reference's
  * U = S = 0), pushed into their bounds as IPOPT pushes a starting point; test infrastructure (warm starts from a
@@ -2730,6 +2746,18 @@ int oracle_solve_one(const NlotProblem* p, const NlotSolverOptions* o, const Nlo
                      const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
                      int* iters_out, double* info) {
     return oracle_solve_warm(p, o, m, x0, xg, Xinit, NULL, NULL, Xout, Uout, Sout, cost, iters_out, info);
+}
+/* oracle_solve_one that also records the iterate (X, U) at the top of every iteration it < trace_cap into
+ * trace[it * ((N+1) nx + N nu)] (test infrastructure: per-instance iterate fixtures) */
+int oracle_solve_trace(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
+                       const double* xg, const double* Xinit, double* Xout, double* Uout, double* Sout, double* cost,
+                       int* iters_out, double* info, double* trace, int trace_cap) {
+    g_trace = trace;
+    g_trace_cap = trace_cap;
+    const int st = oracle_solve_warm(p, o, m, x0, xg, Xinit, NULL, NULL, Xout, Uout, Sout, cost, iters_out, info);
+    g_trace = NULL;
+    g_trace_cap = 0;
+    return st;
 }
 int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const NlotMlpDesc* m, const double* x0,
                       const double* xg, const double* Xinit, const double* Uinit, const double* Sinit, double* Xout,
@@ -2834,6 +2862,7 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
     for (;;) {
         eval_full(s);
         errors(s, &e);
+        trace_rec(s, iter, s->X, s->U);
         double E0 = fmax(fmax(e.dual / e.sd, e.primal), e.compl0 / e.sc);
         if (dump) { /* [iter, mu, f, E0, dual, primal, free mode, resto phases], X and yd, one record per iteration */
             const double hd[8] = {(double)iter, s->mu, s->f, E0, e.dual, e.primal, (double)s->free_mode,
@@ -3167,6 +3196,7 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         info[10] = s->max_nafilt;
         info[11] = s->filt_ovf + (r_alloc ? r->filt_ovf : 0);
         info[12] = s->afilt_ovf;
+        info[13] = (double)(s->n_trials + (r_alloc ? r->n_trials : 0));
     }
     if (r_alloc) free(r->arena);
     free(s->arena);
@@ -3218,6 +3248,7 @@ void oracle_default_options(NlotSolverOptions* o) {
     o->resto_proximity_weight = 1.0;
     o->bound_mult_reset_threshold = 1000.0;
     o->resto_failure_feasibility_threshold = 0.0;
+    o->general_bounds = 1; /* the bounds as constraint rows, CasADi Opti's form (runner.py:67-69,101-103) */
 }
 
 int oracle_sizeof_problem(void) { return (int)sizeof(NlotProblem); }

@@ -43,6 +43,8 @@ def lib():
                                        C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, dp]
         L.oracle_solve_warm.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
                                          C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, dp, dp, ip, dp]
+        L.oracle_solve_trace.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
+                                         C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, dp, dp, C.c_int]
         L.oracle_solve_batch.argtypes = [C.POINTER(_abi.NlotProblem), C.POINTER(_abi.NlotSolverOptions),
                                          C.POINTER(_abi.NlotMlpDesc), dp, dp, dp, dp, dp, dp, dp, ip, ip,
                                          C.c_long, C.c_int]
@@ -159,7 +161,27 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init
                 constr_viol=info[2], lin_resid=info[3], mu=info[4], E0=info[5], resto_phases=int(info[6]),
                 watchdogs=ev // 1000000, soft_resto_steps=(ev // 10000) % 100, soc_tried=(ev // 100) % 100,
                 tiny_steps=ev % 100, theta_fail=float(info[8]), max_filter=int(info[9]),
-                max_mu_filter=int(info[10]), filter_forgotten=int(info[11]), mu_filter_forgotten=int(info[12]))
+                max_mu_filter=int(info[10]), filter_forgotten=int(info[11]), mu_filter_forgotten=int(info[12]),
+                trials=int(info[13]))
+
+
+def solve_trace(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, cap=201):
+    """solve_one plus the iterate (X, U) at the top of every iteration it < cap: trace[it] = the point a run with
+    max_iter = it returns; rows past the final iteration stay NaN."""
+    pc = problem.to_c()
+    opt = opt or _abi.default_options()
+    N, nx, nu = problem.N, problem.nx, problem.nu
+    X, U, S = np.zeros((N + 1, nx)), np.zeros((N, nu)), np.zeros(N + 1)
+    cost, info = np.zeros(1), np.zeros(16)
+    it = (C.c_int * 1)()
+    tr = np.full((cap, (N + 1) * nx + N * nu), np.nan)
+    x0 = np.ascontiguousarray(x0, np.float64)
+    xg = np.ascontiguousarray(xg, np.float64)
+    Xi = None if X_init is None else np.ascontiguousarray(X_init, np.float64)
+    st = lib().oracle_solve_trace(C.byref(pc), C.byref(opt), C.byref(hm.desc) if hm else None, _dp(x0), _dp(xg),
+                                  _dp(Xi), _dp(X), _dp(U), _dp(S), _dp(cost), it, _dp(info), _dp(tr), cap)
+    return dict(status=st, X=X, U=U, S=S, cost=float(cost[0]), iters=int(it[0]), trace=tr, trials=int(info[13]),
+                resto_phases=int(info[6]))
 
 
 def solve_batch(problem, x0, xg, hm: HostMlp = None, opt=None, threads=0):

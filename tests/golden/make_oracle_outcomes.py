@@ -1,18 +1,31 @@
 #!/usr/bin/env python3
 """Oracle outcome fixtures for the solve-level GPU parity tests whose oracle runs are too long for a GPU test.
 
-    python tests/golden/make_oracle_outcomes.py [--threads 8]   ->  tests/golden/oracle_outcomes.npz
+    python tests/golden/make_oracle_outcomes.py [--threads 8] [--form rows|varbounds] [--only metric|b6]
+        rows (default):  tests/golden/oracle_outcomes.npz            (the reference's constraint-row bounds)
+        varbounds:       tests/golden/oracle_outcomes_varbounds.npz  (the same bounds as variable bounds)
 
 For each case it stores the instances (x0, xg, and the initial guesses where the case has its own) and the CPU
-oracle's status / final cost / iterations under tests/outcomes.PERTURBATIONS (x0, x0 +- 1e-13 e_x, x0 +- 1e-13 e_y, and
-the net summed in reverse order), with IPOPT's settings
-(default_options: max_iter 1000, tol 1e-4, adaptive mu, restoration on):
+oracle's status / final cost / iterations / final-iterate deviation under tests/outcomes.PERTURBATIONS (x0,
+x0 +- 1e-13 e_x, x0 +- 1e-13 e_y, and the net summed in reverse order), with IPOPT's settings (default_options:
+max_iter 1000, tol 1e-4, adaptive mu, restoration on; general_bounds by --form):
 
   metric: 128 seeded instances of the headline workload (unicycle_2nd, b3 body, N = 50, artefact FourierMLP; the
           first 128 start/goal pairs of sample_start_goal(seed 0));
   b6:     24 benchmark-6 instances (BASELINE configs[3]: N = 100, the trained ring SDF) from the YAML's RRT initial
           guess, computed by the oracle's RRT restatement (oracle/rrt_oracle.py) and stored, so that the GPU test
           starts both solvers from the identical guess.
+
+Per-instance pinned iterates: every run records its iterate at the top of each iteration
+(oracle_solve_trace).  For instance i, k_i is the last iteration (at most PIN_CAP = 200, at most the shortest of its
+six runs) up to which all five perturbed runs stay within PIN_TOL (max |dX|, |dU|) of the unperturbed run: 1e-5 on
+these learned-SDF cases (the reverse-order run changes the fp32 net's outputs at the rounding level, which the
+iterates feel at ~1e-7..1e-6 from the first iterations; 1e-5 keeps a 10x margin under the GPU test's 1e-4, the
+fp32-MLP iterate tolerance of DESIGN.md §5);
+{case}_kpin[i] = k_i, {case}_Xpin / _Upin = the unperturbed iterate at k_i (what max_iter = k_i returns),
+{case}_pin_spread = the perturbed runs' largest deviation up to k_i.  A GPU test runs every instance to k_i — failed
+and chaotic instances included — and compares the iterate.  {case}_trials: the run's trial-point evaluations (IPOPT's
+sequential backtracking: one SDF value evaluation of the trial's corners each; DESIGN.md §8f cost model).
 
 The oracle is deterministic (one instance per thread, no reductions across threads), so the GPU box's oracle
 build reproduces these numbers bitwise; tests/test_oracle_outcomes_fixture.py re-runs a few instances on the CPU
@@ -21,6 +34,7 @@ import argparse
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -29,6 +43,11 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+PIN_CAP = 200
+PIN_TOL = 1e-5
+OUT = {"rows": os.path.join(HERE, "oracle_outcomes.npz"),
+       "varbounds": os.path.join(HERE, "oracle_outcomes_varbounds.npz")}
 
 
 def metric_instances(n=128):
@@ -57,57 +76,101 @@ def b6_instances(n=24):
     return X0, XG, Xi
 
 
+def pin(trace0, dev, iters):
+    """k_i, and the perturbed runs' largest deviation up to it: dev [m, n, cap] per-iteration deviations of the
+    perturbed runs (row 0 unused), iters [m, n] final iterations."""
+    m, n, cap = dev.shape
+    kpin = np.zeros(n, np.int32)
+    spread = np.zeros(n)
+    for i in range(n):
+        kmax = min(PIN_CAP, cap - 1, int(iters[:, i].min()))
+        d = np.nanmax(dev[1:, i, :kmax + 1], axis=0)
+        bad = np.nonzero(~(d <= PIN_TOL))[0]
+        k = kmax if len(bad) == 0 else int(bad[0]) - 1
+        kpin[i] = max(k, 0)
+        spread[i] = float(np.nanmax(d[:kpin[i] + 1]))
+    return kpin, spread
+
+
+def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
+    """Outcomes under every perturbation, with the per-instance pinned iterates."""
+    from outcomes import PERTURBATIONS, mlp_order
+
+    n, m = len(X0), len(PERTURBATIONS)
+
+    def one(args):  # one perturbation of one instance (ctypes releases the GIL)
+        i, (c, d, _) = args
+        x = X0[i].copy()
+        x[c] += d
+        return O.solve_trace(prob, x, XG[i], hm, opt=opt, X_init=None if Xi is None else Xi[i], cap=PIN_CAP + 1)
+
+    st = np.zeros((m, n), np.int32)
+    trials = np.zeros((m, n), np.int32)
+    cost = np.zeros((m, n))
+    its = np.zeros((m, n), np.int32)
+    xdev = np.zeros((m, n))
+    dev = np.full((m, n, PIN_CAP + 1), np.nan)
+    XU0, T0 = None, None
+    with ThreadPoolExecutor(threads) as ex:
+        for p, pd in enumerate(PERTURBATIONS):  # one batch per perturbation: the net's summation order is process-wide
+            if pd[2] and hm is None:  # no net: the reverse-order run is the unperturbed run
+                st[p], cost[p], its[p], xdev[p], dev[p], trials[p] = st[0], cost[0], its[0], xdev[0], 0.0, trials[0]
+                continue
+            with mlp_order(pd[2]):
+                rs = list(ex.map(one, [(i, pd) for i in range(n)]))
+            XU = np.stack([np.concatenate([np.ravel(r["X"]), np.ravel(r["U"])]) for r in rs])
+            T = np.stack([r["trace"] for r in rs])
+            if XU0 is None:
+                XU0, T0 = XU, T
+            st[p] = [r["status"] for r in rs]
+            cost[p] = [r["cost"] for r in rs]
+            its[p] = [r["iters"] for r in rs]
+            trials[p] = [r["trials"] for r in rs]
+            xdev[p] = np.abs(XU - XU0).max(1)
+            dev[p] = np.abs(T - T0).max(2)
+    kpin, spread = pin(T0, dev, its)
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    XUp = T0[np.arange(n), kpin]
+    return {"status": st, "cost": cost, "iters": its, "xdev": xdev, "trials": trials, "kpin": kpin, "pin_spread": spread,
+            "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx), "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
-    ap.add_argument("--out", default=os.path.join(HERE, "oracle_outcomes.npz"))
+    ap.add_argument("--form", default="rows", choices=list(OUT))
+    ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
     a = ap.parse_args()
+    out_path = a.out or OUT[a.form]
     import oracle as O
-    from outcomes import oracle_outcomes
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
 
-    opt = _abi.default_options()
-    data = dict(np.load(a.out)) if (a.only and os.path.exists(a.out)) else {}
+    opt = _abi.default_options(general_bounds=1 if a.form == "rows" else 0)
+    data = dict(np.load(out_path)) if (a.only and os.path.exists(out_path)) else {}
+    data["general_bounds"] = np.array(opt.general_bounds)
+
+    def report(case, out, t):
+        kp = out["kpin"]
+        print(f"{case}: {time.time() - t:.0f} s, statuses {np.bincount(out['status'][0], minlength=7).tolist()}, "
+              f"k_pin min / median / max {kp.min()} / {int(np.median(kp))} / {kp.max()}", flush=True)
+
     if a.only in (None, "metric"):
         t = time.time()
         x0, xg = metric_instances()
-        out = oracle_outcomes(O, METRIC_PROBLEM, x0, xg, O.HostMlp(MlpWeights.artefact()), opt, threads=a.threads)
+        out = run_case(O, METRIC_PROBLEM, x0, xg, O.HostMlp(MlpWeights.artefact()), opt, None, a.threads)
         data.update({"metric_x0": x0, "metric_xg": xg, **{f"metric_{k}": v for k, v in out.items()}})
-        print(f"metric: {time.time() - t:.0f} s, statuses {np.bincount(out['status'][0], minlength=7).tolist()}",
-              flush=True)
+        report("metric", out, t)
     if a.only in (None, "b6"):
         t = time.time()
         X0, XG, Xi = b6_instances()
         hm6 = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")))
-        from concurrent.futures import ThreadPoolExecutor
-
-        from outcomes import PERTURBATIONS, mlp_order
-
-        def one(args):  # one perturbation of one instance (ctypes releases the GIL)
-            i, (c, d, _) = args
-            x = X0[i].copy()
-            x[c] += d
-            r = O.solve_one(B6_PROBLEM, x, XG[i], hm6, opt=opt, X_init=Xi[i])
-            return r["status"], r["cost"], r["iters"], np.concatenate([np.ravel(r["X"]), np.ravel(r["U"])])
-
-        res = []
-        with ThreadPoolExecutor(a.threads) as ex:
-            for pd in PERTURBATIONS:  # one batch per perturbation: the net's summation order is process-wide
-                with mlp_order(pd[2]):
-                    res += list(ex.map(one, [(i, pd) for i in range(len(X0))]))
-        n, m = len(X0), len(PERTURBATIONS)
-        XU = np.stack([r[3] for r in res]).reshape(m, n, -1)
-        out = {"status": np.array([r[0] for r in res], np.int32).reshape(m, n),
-               "cost": np.array([r[1] for r in res], float).reshape(m, n),
-               "iters": np.array([r[2] for r in res], np.int32).reshape(m, n),
-               "xdev": np.abs(XU - XU[0]).max(2)}
+        out = run_case(O, B6_PROBLEM, X0, XG, hm6, opt, Xi, a.threads)
         data.update({"b6_x0": X0, "b6_xg": XG, "b6_xinit": Xi, **{f"b6_{k}": v for k, v in out.items()}})
-        print(f"b6: {time.time() - t:.0f} s, statuses {np.bincount(out['status'][0], minlength=7).tolist()}",
-              flush=True)
-    np.savez_compressed(a.out, **data)
+        report("b6", out, t)
+    np.savez_compressed(out_path, **data)
 
 
 if __name__ == "__main__":

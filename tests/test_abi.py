@@ -73,7 +73,7 @@ def test_workspace_holds_the_slots_only():
 
 def test_solve_batch_refuses_bad_arguments_before_the_device():
     """nlot_solve_batch validates on the host and fails loudly (NLOT_ERR_INVALID + nlot_last_error) before any device
-    call, so these run without a GPU: an empty or oversized batch, the CPU-only general_bounds option, an unknown
+    call, so these run without a GPU: an empty or oversized batch, a general_bounds value other than 0 / 1, an unknown
     mu_strategy, a learned-SDF problem without a net, null output pointers."""
     import ctypes as C
 
@@ -93,10 +93,11 @@ def test_solve_batch_refuses_bad_arguments_before_the_device():
     assert call(base, (1 << 26) + 1) == (-1, "B out of range")
     rc, msg = call(base, 4)
     assert rc == -1 and msg == "nlot_solve_batch: null pointer"
+    assert base.general_bounds == 1  # the reference's NLP form (runner.py:67-69,101-103) is the default
     o = _abi.gpu_options()
-    o.general_bounds = 1
+    o.general_bounds = 2
     rc, msg = call(o, 4)
-    assert rc == -1 and "CPU restatement only" in msg
+    assert rc == -1 and "general_bounds" in msg
     o = _abi.gpu_options()
     o.mu_strategy = 2
     assert call(o, 4)[0] == -1 and "mu_strategy" in call(o, 4)[1]

@@ -78,15 +78,20 @@ def _yaml_case(fn):
 CASES = list(_cases().keys())
 
 
+# the bounds as the reference's constraint rows (runner.py:67-69,101-103; the default) and as variable bounds
+FORMS = {"rows": 1, "varbounds": 0}
+
+
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("name", CASES)
-def test_iterates_match_oracle(name):
+def test_iterates_match_oracle(name, form):
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.solver import solve_batch
 
     prob, x0, xg = _cases()[name]
     for k in (1, 3, 8):
-        opt = _abi.gpu_options(max_iter=k)
+        opt = _abi.gpu_options(max_iter=k, general_bounds=FORMS[form])
         rg = solve_batch(prob, np.array([x0], float), np.array([xg], float), options=opt)
         rc = O.solve_one(prob, np.array(x0, float), np.array(xg, float), opt=opt)
         xp = np.array(x0, float)
@@ -96,7 +101,7 @@ def test_iterates_match_oracle(name):
         assert rg["status"][0].item() == rc["status"], (name, k)
         assert rg["iters"][0].item() == rc["iters"], (name, k)
         dx = {n: float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U", "S")}
-        print(name, "k", k, "status", rc["status"], dx, "oracle sensitivity", sens)
+        print(name, form, "k", k, "status", rc["status"], dx, "oracle sensitivity", sens)
         tol = max(1e-7 if k <= 3 else 1e-6, 20 * sens)
         for n, v in dx.items():
             assert v <= tol, (name, k, n, v)
@@ -134,4 +139,5 @@ def test_full_solves_match_oracle(name):
         assert np.abs(X[b, 1:] - F).max() < 1e-4
         lo = np.array([c[0] for c in prob.control_bounds])
         hi = np.array([c[1] for c in prob.control_bounds])
-        assert (U[b] >= lo - 1e-9).all() and (U[b] <= hi + 1e-9).all()
+        # the bound rows hold to constr_viol_tol (U itself is free in the reference's constraint-row form)
+        assert (U[b] >= lo - 1e-4).all() and (U[b] <= hi + 1e-4).all()

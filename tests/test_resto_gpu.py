@@ -36,8 +36,9 @@ def _case(name):
     return _cases()[name]
 
 
+@pytest.mark.parametrize("form", ["rows", "varbounds"])
 @pytest.mark.parametrize("name", list(ITERS))
-def test_restoration_iterates_match_oracle(name):
+def test_restoration_iterates_match_oracle(name, form):
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.solver import solve_batch
@@ -45,7 +46,7 @@ def test_restoration_iterates_match_oracle(name):
     prob, x0, xg = _case(name)
     resto_seen = 0
     for k in ITERS[name]:
-        opt = _abi.default_options(max_iter=k)
+        opt = _abi.default_options(max_iter=k, general_bounds=1 if form == "rows" else 0)
         rg = solve_batch(prob, np.array([x0], float), np.array([xg], float), options=opt)
         rc = O.solve_one(prob, np.array(x0, float), np.array(xg, float), opt=opt)
         xp = np.array(x0, float)
@@ -53,7 +54,7 @@ def test_restoration_iterates_match_oracle(name):
         rp = O.solve_one(prob, xp, np.array(xg, float), opt=opt)
         sens = max(float(np.abs(rp[n] - rc[n]).max()) for n in ("X", "U", "S"))
         dx = {n: float(np.abs(rg[n][0].cpu().numpy() - rc[n]).max()) for n in ("X", "U", "S")}
-        print(name, "k", k, "status", rc["status"], "iters", rc["iters"], "resto phases", rc["resto_phases"],
+        print(name, form, "k", k, "status", rc["status"], "iters", rc["iters"], "resto phases", rc["resto_phases"],
               "soft", rc["soft_resto_steps"], dx, "oracle sensitivity", sens, flush=True)
         resto_seen = max(resto_seen, rc["resto_phases"])
         if rp["status"] == rc["status"] and rp["iters"] == rc["iters"]:  # outcome reproducible by the oracle itself

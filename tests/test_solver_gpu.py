@@ -22,9 +22,12 @@ def _oracle():
 
 
 STRATEGIES = {"adaptive": {}, "monotone": dict(mu_strategy=0, barrier_tol_factor=10.0)}
+# iterate parity also for the variable-bound form (the default is the reference's constraint-row bounds)
+ITER_STRATEGIES = {**STRATEGIES, "adaptive_varbounds": dict(general_bounds=0),
+                   "monotone_varbounds": dict(mu_strategy=0, barrier_tol_factor=10.0, general_bounds=0)}
 
 
-@pytest.mark.parametrize("strategy", list(STRATEGIES))
+@pytest.mark.parametrize("strategy", list(ITER_STRATEGIES))
 def test_iterates_match_oracle_b2(strategy):
     O = _oracle()
     from nlotrajectories_amd import _abi
@@ -33,19 +36,24 @@ def test_iterates_match_oracle_b2(strategy):
 
     b = BENCHMARKS["b2"]
     for k in (1, 2, 5, 10, 20):
-        opt = _abi.gpu_options(max_iter=k, **STRATEGIES[strategy])
+        opt = _abi.gpu_options(max_iter=k, **ITER_STRATEGIES[strategy])
         rg = solve_batch(b["problem"], np.array([b["start"]]), np.array([b["goal"]]), options=opt)
         rc = O.solve_one(b["problem"], b["start"], b["goal"], opt=opt)
         assert rg["iters"][0].item() == rc["iters"] == k
         dx = {n: np.abs(rg[n][0].cpu().numpy() - rc[n]).max() for n in ("X", "U", "S")}
-        print(strategy, "k", k, "max |gpu - oracle|", dx)
-        # fp64 on both sides; summation orders differ, and the differences grow along the nonconvex path
-        tol = 1e-7 if k <= 10 else 1e-6
+        xp = np.array(b["start"], float)
+        xp[0] += 1e-13
+        rp = O.solve_one(b["problem"], xp, b["goal"], opt=opt)
+        sens = max(float(np.abs(rp[n] - rc[n]).max()) for n in ("X", "U", "S"))
+        print(strategy, "k", k, "max |gpu - oracle|", dx, "oracle sensitivity", sens)
+        # fp64 on both sides; summation orders differ, and the differences grow along the nonconvex path as the
+        # oracle's own response to a 1e-13 change of the start does (2.2e-7 at k = 20 with the constraint rows)
+        tol = max(1e-7 if k <= 10 else 1e-6, 20 * sens)
         for n in dx:
             assert dx[n] <= tol, (k, n, dx[n])
 
 
-@pytest.mark.parametrize("strategy", list(STRATEGIES))
+@pytest.mark.parametrize("strategy", list(ITER_STRATEGIES))
 def test_iterates_match_oracle_learned(artefact, strategy):
     O = _oracle()
     from nlotrajectories_amd import _abi
@@ -56,7 +64,7 @@ def test_iterates_match_oracle_learned(artefact, strategy):
     mlp, hm = DeviceMlp(artefact), O.HostMlp(artefact)
     x0, xg = [0, 0, 0.785, 0, 0], [1, 1, 0.785, 0, 0]
     for k in (1, 3):
-        opt = _abi.gpu_options(max_iter=k, **STRATEGIES[strategy])
+        opt = _abi.gpu_options(max_iter=k, **ITER_STRATEGIES[strategy])
         rg = solve_batch(METRIC_PROBLEM, np.array([x0]), np.array([xg]), mlp=mlp, options=opt)
         rc = O.solve_one(METRIC_PROBLEM, x0, xg, hm, opt=opt)
         np.testing.assert_allclose(rg["X"][0].cpu().numpy(), rc["X"], atol=1e-4)
@@ -152,23 +160,25 @@ def test_safeguards_iterate_parity(artefact):
     assert socs >= 2
 
 
-def test_tiny_step_rule_matches_oracle():
+@pytest.mark.parametrize("form", ["rows", "varbounds"])
+def test_tiny_step_rule_matches_oracle(form):
     """IPOPT's tiny-step rule, made to fire with a large tiny_step_tol: full steps without a line search, and
     STOP_AT_TINY_STEP after two in a row — same iterations and status on the GPU and in the oracle.  The
-    start/goal pair runs along the top edge of the square, clear of the obstacle: a well-conditioned path
-    (delta_w <= 1, dual infeasibility <= 1) whose outcome is reproducible (a 1e-13 start perturbation moves the
-    oracle's iterate by 4e-9); without the rule it solves in 20 iterations instead of stopping at 7.  (Pairs
-    grazing the obstacle reach delta_w = 1e6 and dual infeasibility 1e5 in their first iteration, where the
-    GPU's and the oracle's summation orders part.)"""
+    start/goal pair runs along the top edge of the square, clear of the obstacle: a well-conditioned path whose
+    outcome the oracle reproduces under +-1e-13 changes of the start's x and y in both bound forms (constraint rows:
+    STOP_AT_TINY_STEP at 7 iterations, 41 to solve without the rule; variable bounds: 33 and 291).  (The round-4 pair
+    (0, 0.924) -> (1, 0.98) is chaotic with the constraint rows: the oracle stops at 29 or solves at 82 / 99 under
+    1e-13 changes; pairs grazing the obstacle reach delta_w = 1e6 in their first iteration, where the GPU's and the
+    oracle's summation orders part.)"""
     O = _oracle()
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.solver import solve_batch
 
     b = BENCHMARKS["b2"]
-    th = float(np.arctan2(0.98 - 0.924, 1.0))
-    x0, xg = [0.0, 0.924, th, 0.0, 0.0], [1.0, 0.98, th, 0.0, 0.0]
-    opt = _abi.gpu_options(tiny_step_tol=0.05, tiny_step_y_tol=1e3)
+    th = float(np.arctan2(0.97 - 0.93, 0.9))
+    x0, xg = [0.1, 0.93, th, 0.0, 0.0], [1.0, 0.97, th, 0.0, 0.0]
+    opt = _abi.gpu_options(tiny_step_tol=0.05, tiny_step_y_tol=1e3, general_bounds=1 if form == "rows" else 0)
     rg = solve_batch(b["problem"], np.array([x0]), np.array([xg]), options=opt)
     rc = O.solve_one(b["problem"], x0, xg, opt=opt)
     print("tiny: oracle", rc["status"], rc["iters"], rc["tiny_steps"], "gpu", rg["status"][0].item(),
@@ -179,7 +189,8 @@ def test_tiny_step_rule_matches_oracle():
 
 
 def test_solution_satisfies_constraints():
-    """Every instance reported solved satisfies the NLP's equalities to 1e-4 (constr_viol_tol)."""
+    """Every instance reported solved satisfies the NLP's equalities and (constraint rows) bounds to 1e-4
+    (constr_viol_tol)."""
     O = _oracle()
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.sampling import sample_start_goal
@@ -197,7 +208,7 @@ def test_solution_satisfies_constraints():
         for k in range(p.N):
             F = X[b, k] + p.dt * O.dynamics(p, X[b, k], U[b, k])
             assert np.abs(X[b, k + 1] - F).max() < 1e-4
-        assert (U[b] >= -2 - 1e-9).all() and (U[b] <= 2 + 1e-9).all() and (S[b] >= 0).all()
+        assert (U[b] >= -2 - 1e-4).all() and (U[b] <= 2 + 1e-4).all() and (S[b] >= -1e-4).all()
 
 
 @pytest.mark.parametrize("case", ["metric", "b2", "b2_many_waves"])
