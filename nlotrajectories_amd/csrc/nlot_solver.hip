@@ -115,10 +115,10 @@ enum Scal {
     SC_COUNT
 };
 // Filters (line search, adaptive-mu progress, restoration): IPOPT's Filter is an unbounded list from which
-// dominated entries are removed.  At most one entry enters per iteration, and the peak size measured over the
-// metric workload is 59 (oracle, 256 instances), so 1024 entries per filter are unbounded in
-// effect.  An overflow would forget the oldest entry; it is counted (NlotSolveStats.filter_forgotten) and never
-// happens on any measured workload.
+// dominated entries are removed.  At most one entry enters per iteration (the line-search filter can grow to
+// 2 max_iter + O(1) in principle); the largest size measured over the round-4 metric bench was 613 (bench.py
+// config.filters), so 1024 entries per filter are unbounded in effect there.  An overflow forgets the oldest entry;
+// it is counted (NlotSolveStats.filter_forgotten, the restoration filter included) and reported by bench.py.
 constexpr int FILT_MAX = 1024;
 // ints per step-parity counter set (workspace counters: 2 sets): [0..8) the phase machine's counts (Ws::cnt), [8..11)
 // diagnostics of the factorising Newton solves (attempts summed, their maximum, solves needing more than one), [11]

@@ -793,6 +793,7 @@ typedef struct {
     int rej_filter, last_rej_filter, n_filt_rej, n_filt_resets; /* IPOPT filter reset heuristic (trigger 5, max 5) */
     int n_soc_tried, n_soc_acc;                                  /* second-order corrections started / accepted */
     long n_trials; /* trial-point merit evaluations (one SDF value evaluation of the trial's corners each) */
+    int term; /* diagnostics: how the run ended (TERM_*) */
     double rho, zeta;
     double *XR, *UR, *SR, *DRX, *DRU, *DRS; /* reference point and its proximity scaling */
     double *rp, *rn, *rzp, *rzn;            /* p, n and their bound multipliers */
@@ -2482,6 +2483,10 @@ static void sol_setup(Sol* s, const NlotProblem* p, const NlotSolverOptions* o, 
     if (fc && atoi(fc) > 0 && atoi(fc) < s->fcap) s->fcap = atoi(fc);
 }
 
+/* how a run ended (diagnostic, info[14]) */
+enum { TERM_SOLVED = 0, TERM_MAXITER = 1, TERM_MAXITER_RESTO = 2, TERM_RESTO_LS = 3, TERM_RESTO_FEAS_REJECTED = 4,
+       TERM_RESTO_INFEASIBLE = 5, TERM_ALMOST_FEASIBLE = 6, TERM_NUMERIC = 7, TERM_TINY = 8, TERM_LS = 9 };
+
 /* Per-iteration trace (test infrastructure: oracle_solve_trace): the iterate (X, U) at the top of iteration it, i.e.
  * the point a run with max_iter = it returns (inside a restoration phase: the restoration iterate, as the GPU solver
  * reports it).  Thread-local, so parallel runs trace independently. */
@@ -2605,12 +2610,14 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
                 for (int q = 0; q < (N + 1) * M; ++q) pinf = fmax(pinf, fabs(s->rcq[q]));
                 for (int q = 0; q < s->nb; ++q) pinf = fmax(pinf, fabs(s->rcb[q]));
                 status = pinf <= thr ? NLOT_RESTO_FAILED : NLOT_INFEASIBLE;
+                s->term = pinf <= thr ? TERM_RESTO_FEAS_REJECTED : TERM_RESTO_INFEASIBLE;
                 break;
             }
         }
         first = 0;
         if (*iter >= o->max_iter) {
             status = NLOT_MAXITER;
+            s->term = TERM_MAXITER_RESTO;
             break;
         }
         /* monotone barrier update inside the restoration phase */
@@ -2649,6 +2656,7 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
             fprintf(stderr, "  resto it %3d mu %.2e fR %.6f thR %.2e E0 %.2e a %.2e\n", *iter, r->mu, r->f, theta, E0, alpha);
         if (!ok) {
             status = NLOT_RESTO_FAILED;
+            s->term = TERM_RESTO_LS;
             break;
         }
         if (!fa) filter_add(r, theta, phi);
@@ -2734,7 +2742,9 @@ static int restoration(Sol* s, Sol* r, int* iter, double* lin_resid) {
  * soft-restoration / SOC / tiny-step events (packed: 1e6 * watchdog + 1e4 * soft + 1e2 * soc tried + tiny),
  * [8] = theta (1-norm) at the last line-search failure, -1 if none, [9] / [10] = peak size of the line-search
  * (incl. restoration) / adaptive-mu filter, [11] / [12] = their forgotten entries (NLOT_ORACLE_FILT_CAP only),
- * [13] = trial-point merit evaluations (sequential line-search trials incl. corrections, soft and restoration steps).
+ * [13] = trial-point merit evaluations (sequential line-search trials incl. corrections, soft and restoration steps),
+ * [14] = how the run ended (TERM_*: restoration line search failed / converged to a feasible point the original filter
+ * rejects / converged infeasible, almost feasible at the restoration's entry, max_iter inside restoration, ...).
  * info holds >= 16 doubles. */
 /* oracle_solve_one with an initial guess for the controls and slacks too (Uinit / Sinit, NULL = the reference's
  * U = S = 0), pushed into their bounds as IPOPT pushes a starting point; test infrastructure (warm starts from a
@@ -3141,6 +3151,7 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
              * (acceptable_tol 1e-6 < tol here, so none) IPOPT stops with Restoration_Failed. */
             if (ref.theta <= 1e-2 * o->tol) {
                 status = NLOT_RESTO_FAILED;
+                s->term = TERM_ALMOST_FEASIBLE;
                 break;
             }
             /* ---- feasibility restoration phase ---- */
@@ -3197,6 +3208,10 @@ int oracle_solve_warm(const NlotProblem* p, const NlotSolverOptions* o, const Nl
         info[11] = s->filt_ovf + (r_alloc ? r->filt_ovf : 0);
         info[12] = s->afilt_ovf;
         info[13] = (double)(s->n_trials + (r_alloc ? r->n_trials : 0));
+        /* [14] how the run ended (TERM_*): the status, told apart by where it came from */
+        info[14] = status == NLOT_SOLVED ? TERM_SOLVED : status == NLOT_NUMERIC ? TERM_NUMERIC
+                   : status == NLOT_TINY_STEP ? TERM_TINY : status == NLOT_LS_FAILED ? TERM_LS
+                   : status == NLOT_MAXITER && s->term != TERM_MAXITER_RESTO ? TERM_MAXITER : s->term;
     }
     if (r_alloc) free(r->arena);
     free(s->arena);

@@ -139,6 +139,12 @@ def knot_constraints(problem, xk, sk=0.0, hm: HostMlp = None):
     return d[:m], g[:m]
 
 
+# oracle/nlot_oracle.c TERM_*: how a run ended (info[14])
+TERM_NAMES = ("solved", "max_iter", "max_iter_in_restoration", "restoration_line_search_failed",
+              "restoration_converged_feasible_rejected_by_filter", "restoration_converged_infeasible",
+              "almost_feasible_at_restoration_entry", "numeric", "tiny_step", "line_search_failed")
+
+
 def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init=None, S_init=None):
     pc = problem.to_c()
     opt = opt or _abi.default_options()
@@ -162,7 +168,7 @@ def solve_one(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, U_init
                 watchdogs=ev // 1000000, soft_resto_steps=(ev // 10000) % 100, soc_tried=(ev // 100) % 100,
                 tiny_steps=ev % 100, theta_fail=float(info[8]), max_filter=int(info[9]),
                 max_mu_filter=int(info[10]), filter_forgotten=int(info[11]), mu_filter_forgotten=int(info[12]),
-                trials=int(info[13]))
+                trials=int(info[13]), term=TERM_NAMES[int(info[14])])
 
 
 def solve_trace(problem, x0, xg, hm: HostMlp = None, opt=None, X_init=None, cap=201):

@@ -37,6 +37,7 @@ def main():
     st = last_stats()
     st["B"], st["max_iter"] = B, it
     st["status_counts"] = torch.bincount(r["status"].long(), minlength=7).tolist()
+    st["instance_iterations"] = int(r["iters"].long().sum().item())
     print(json.dumps(st), flush=True)
 
 

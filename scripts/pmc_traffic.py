@@ -18,10 +18,17 @@ import sys
 def family(name):
     if re.search(r"k_ric<\d+, false, false>", name):
         return "k_ric"
+    if re.search(r"k_ric<\d+, false, true>", name):
+        return "k_ric_soc"
+    if re.search(r"k_ric<\d+, true, false>", name):
+        return "k_ric_resto"
     if "mlp_bf16<128, true" in name:
         return "mlp_full"
     if "mlp_bf16<128, false" in name:
         return "mlp_value"
+    for k in ("k_iter_a", "k_iter_b", "k_accept", "k_resto_a", "k_resto_b", "k_resto_ls"):
+        if k + "<" in name:
+            return k
     return None
 
 
@@ -29,11 +36,19 @@ def main():
     d, out = sys.argv[1], sys.argv[2]
     tot = collections.defaultdict(float)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = []
         for path in glob.glob(os.path.join(d, f"pmc_{c}", "**", "*counter_collection.csv"), recursive=True):
-            for r in csv.DictReader(open(path)):
-                f = family(r["Kernel_Name"])
-                if f and r["Counter_Name"] == c:
-                    tot[(f, c)] += float(r["Counter_Value"]) * 1024.0 * (2.0 if c == "FETCH_SIZE" else 1.0)
+            rows += [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == c and family(r["Kernel_Name"])]
+        # the first factorising k_ric dispatch is the INIT step's least-squares multiplier solve (every instance, not in
+        # NlotSolveStats.ric_solves): excluded, so that bytes per solve are the Newton solves' own (round 5; round 4's
+        # file included it: 65,536 LSQ solves over 626,165 counted ones)
+        ric = [int(r["Dispatch_Id"]) for r in rows if family(r["Kernel_Name"]) == "k_ric"]
+        lsq = min(ric) if ric else None
+        for r in rows:
+            f = family(r["Kernel_Name"])
+            if f == "k_ric" and int(r["Dispatch_Id"]) == lsq:
+                f = "k_ric_lsq"
+            tot[(f, c)] += float(r["Counter_Value"]) * 1024.0 * (2.0 if c == "FETCH_SIZE" else 1.0)
     st = json.loads(open(os.path.join(d, "pmc_FETCH_SIZE_stats.json")).read().strip().splitlines()[-1])
     pf, pv, reused = st["mlp_points_full"], st["mlp_points_value"], st["mlp_points_full_reused"]
     rf = reused / max(pf, 1)
@@ -59,6 +74,17 @@ def main():
                   "write_bytes_per_solve": tot[("k_ric", "WRITE_SIZE")] / st["ric_solves"],
                   "algorithmic_bytes_per_solve": 143616.0},
     }
+    # the phase kernels and the side-stream Newton solves per instance-iteration, next to SURVEY.md
+    # §8d's algorithmic 2 * 4 * (nvar + ncon) bytes per problem-iteration
+    ii = st.get("instance_iterations")
+    if ii:
+        res["per_instance_iteration"] = {
+            k: {"fetch_bytes": tot[(k, "FETCH_SIZE")] / ii, "write_bytes": tot[(k, "WRITE_SIZE")] / ii,
+                "hbm_bytes": (tot[(k, "FETCH_SIZE")] + tot[(k, "WRITE_SIZE")]) / ii}
+            for k in ("k_iter_a", "k_iter_b", "k_accept", "k_ric", "k_ric_soc", "k_ric_resto", "k_resto_a", "k_resto_b",
+                      "k_resto_ls", "mlp_full", "mlp_value")}
+        res["per_instance_iteration"]["instance_iterations"] = ii
+        res["per_instance_iteration"]["algorithmic_bytes_survey_8d"] = 5736.0
     for k, u in (("mlp_full", "point"), ("mlp_value", "point"), ("k_ric", "solve")):
         e = res[k]
         e[f"hbm_bytes_per_{u}"] = e[f"fetch_bytes_per_{u}"] + e[f"write_bytes_per_{u}"]
