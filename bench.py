@@ -316,11 +316,11 @@ def main():
     alg_bytes = 2 * 4 * (nvar + ncon)
     ric_alg = ric_solves_per_launch * alg_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     ric_traffic = None
-    # PMC at bench size (B = 65536): scripts/pmc_traffic.sh + scripts/pmc_traffic.py -> profiles/r04/ (round 3's file
-    # as the fallback)
-    tf = os.path.join(ROOT, "profiles", "r04", "pmc_traffic_r04_B65536.json")
-    if not os.path.exists(tf):
-        tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_r03m_B65536.json")
+    # PMC at bench size (B = 65536): scripts/pmc_traffic.sh + scripts/pmc_traffic.py -> profiles/r05/ (the newest
+    # round's file that exists)
+    tf = next((t for t in (os.path.join(ROOT, "profiles", r, f) for r, f in
+                           (("r05", "pmc_traffic_r05_B65536.json"), ("r04", "pmc_traffic_r04_B65536.json"),
+                            ("r03", "pmc_traffic_r03m_B65536.json"))) if os.path.exists(t)), "")
     pmc = None
     if os.path.exists(tf):
         with open(tf) as f:
