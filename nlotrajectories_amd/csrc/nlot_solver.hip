@@ -1323,19 +1323,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             { const long long t = wall_clock64(); ph[0] += t - tq; tq = t; }
 #endif
             ric_sync();
-            // ---- batch 2: the control columns of QE (Q_vv, Q_xv) ----
-            double Qv[NV][NZ];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const d2v* src = reinterpret_cast<const d2v*>(&sh.QT[v][0]);
-#pragma unroll
-                for (int i2 = 0; i2 < NZ / 2; ++i2) {
-                    const d2v x = src[i2];
-                    Qv[v][2 * i2] = x.x;
-                    Qv[v][2 * i2 + 1] = x.y;
-                }
-                if (NZ & 1) Qv[v][NZ - 1] = sh.QT[v][NZ - 1];
-            }
+            // ---- batch 2: the control columns of QE (Q_vv, Q_xv), read from LDS where they are used (holding all
+            //      NV x NZ of them in registers across the factorisation spilled the factorising sweep) ----
+            auto Qv = [&](int v, int i) { return sh.QT[v][i]; };
 #ifdef NLOT_PHASE_PROF
             { const long long t = wall_clock64(); ph[1] += t - tq; tq = t; }
 #endif
@@ -1346,8 +1336,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             if (nv == 3 && NV == 3) {
                 // pivoted LDL^T of the symmetric 3x3 (pivot order of ldl_factor: largest diagonal first,
                 // then the larger remaining diagonal), reciprocal pivots
-                auto qv = [&](int a, int c) {  // Q_vv[a][c] = QE[NX + a][NX + c] = Qv[c][NX + a] (static a, c)
-                    return Qv[c][NX + a];
+                auto qv = [&](int a, int c) {  // Q_vv[a][c] = QE[NX + a][NX + c] = Qv(c, NX + a) (static a, c)
+                    return Qv(c, NX + a);
                 };
                 double scale = 1e-300;
 #pragma unroll
@@ -1416,7 +1406,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 #pragma unroll
                 for (int a = 0; a < NV; ++a)
 #pragma unroll
-                    for (int c = 0; c < NV; ++c) L[a][c] = (a < nv && c < nv) ? Qv[c][NX + a] : 0.0;
+                    for (int c = 0; c < NV; ++c) L[a][c] = (a < nv && c < nv) ? Qv(c, NX + a) : 0.0;
                 if (ldl_factor<NV>(L, nv, perm, &nneg)) return 1;
                 negsum += nneg;
                 if (negsum > neg_lim) return 1;
@@ -1450,7 +1440,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 for (int i = 0; i < NX; ++i) {
                     double t = q[i];
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) t += Qv[v][i] * gcol[v];
+                    for (int v = 0; v < NV; ++v) t += Qv(v, i) * gcol[v];
                     vr[i] = t;
                 }
                 d2v* vd = reinterpret_cast<d2v*>(&sh.VU[gc][0]);
@@ -3953,6 +3943,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
         }  // PH_LS
     }
     wsync();
+    if (SC(SC_RESTO) == 2.0) {  // back from a restoration phase in this step's k_resto_a (k_resto_a, "returning")
+        wsync();
+        if (lane == 0) {
+            SC(SC_RESTO) = 0;
+            SC(SC_ACCSLOT) = -1;
+        }
+        wsync();
+        emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+    }
+    wsync();
     ph = (int)SC(SC_PHASE);
     if (ph == PH_DONE) {
         retire(p, dm, ws, b, lane);
@@ -4337,11 +4337,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
             for (int i = lane; i < 8; i += 64) AT(yt, i) = 0.0;
             for (int q = lane; q < ngb; q += 64) AT(yb, q) = 0.0;
             wsync();
-            if (lane == 0) {  // k_iter_a (launched next) takes the instance's iteration from this evaluation
+            // SC_RESTO = 2, "returning": k_resto_a runs on the restoration stream concurrently with this step's
+            // k_iter_a, which passes the instance by; k_accept (after the join) ends the phase and lists the point's
+            // corners for the next step's full launch, whose k_iter_a takes the iteration from there (the same
+            // evaluation one global step later: the instance's arithmetic is unchanged)
+            if (lane == 0) {
                 SC(SC_MU) = mu_o;
                 SC(SC_TAU) = tau_o;
                 SC(SC_DWLAST) = SC(SC_RDWO);
-                SC(SC_RESTO) = 0;
+                SC(SC_RESTO) = 2;
                 SC(SC_INSOFT) = 0;
                 SC(SC_SOFTCNT) = 0;
                 SC(SC_WD) = 0;
@@ -5147,31 +5151,33 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         }
         if (soc_fork == 2) NLOT_HIP_CHECK((hipError_t)(soc_chain(true) == NLOT_OK ? hipSuccess : hipErrorUnknown));
         if (ev[4]) (void)hipEventRecord(ev[4], st);
-        if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
-            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
-                               (int)PASS_INIT, C, Cn);
-            launch_ric(act, C + 2, (int)MODE_LSQ, nullptr, 1 << 30);
-        }
-        // restoration phases (list actr, count C[5]): before k_iter_a, which continues the iteration of an instance
-        // that k_resto_a returns to the original problem
+        // restoration phases (list actr, count C[5]) on a stream of their own, forked once the step's evaluations are
+        // in (they need nothing else of the step; disjoint instances): k_resto_a, their Newton solves, k_resto_b.  An
+        // instance k_resto_a returns to the original problem is passed by this step's k_iter_a and continues next
+        // step (k_accept); round 5: k_resto_a (one long wavefront per restoring instance, ~0.5 ms) left the main
+        // stream's critical path
         const int n_resto = std::min(n_active, resto_bound);
-        if (n_resto > 0)
-            hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, st, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C);
-        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
-                           (int)(soc_fork == 0 ? PASS_ALL : PASS_EVAL), C, Cn);
-        if (soc_fork == 0) NLOT_HIP_CHECK((hipError_t)(soc_chain(false) == NLOT_OK ? hipSuccess : hipErrorUnknown));
-        // the Newton solves and the corrections run over the compacted lists k_iter_a wrote (ws.ricl / ws.socl,
-        // counts C[4] / C[6]; the grids are host bounds, blocks past the count exit): one group per instance that
-        // has work, so a launch holds as many wavefronts as it has solves / 4
-        NLOT_HIP_CHECK(hipEventRecord(res.e_a, st));
-        if (n_resto > 0) {  // the restoration chain on a stream of its own (disjoint instances)
+        if (n_resto > 0) {
+            NLOT_HIP_CHECK(hipEventRecord(res.e_a, st));
             NLOT_HIP_CHECK(hipStreamWaitEvent(s3, res.e_a, 0));
+            hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, s3, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C);
             hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s3,
                                dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON, C + 15, 1 << 30);
             hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, s3, dP, dD, o, dW, actr, C,
                                use_mlp ? ws.tpts[q] : nullptr);
             NLOT_HIP_CHECK(hipEventRecord(res.e_r, s3));
         }
+        if (init_step) {  // INIT: slack push + least-squares multipliers (one Riccati solve)
+            hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
+                               (int)PASS_INIT, C, Cn);
+            launch_ric(act, C + 2, (int)MODE_LSQ, nullptr, 1 << 30);
+        }
+        hipLaunchKernelGGL(k_iter_a<DYN>, dim3(n_active), dim3(64), 0, st, dP, dD, o, dW, act, ws.x0s, ws.xgs,
+                           (int)(soc_fork == 0 ? PASS_ALL : PASS_EVAL), C, Cn);
+        if (soc_fork == 0) NLOT_HIP_CHECK((hipError_t)(soc_chain(false) == NLOT_OK ? hipSuccess : hipErrorUnknown));
+        // the Newton solves and the corrections run over the compacted lists k_iter_a wrote (ws.ricl / ws.socl,
+        // counts C[4] / C[6]; the grids are host bounds, blocks past the count exit): one group per instance that
+        // has work, so a launch holds as many wavefronts as it has solves / 4
         if (ev[6]) (void)hipEventRecord(ev[6], st);
         launch_ric(ws.ricl, C + 4, (int)MODE_NEWTON, C + 8, n_active > ric_tries_min ? ric_tries : 1 << 30);
         if (ev[6]) (void)hipEventRecord(ev[7], st);

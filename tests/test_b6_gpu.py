@@ -49,7 +49,10 @@ def test_b6_batch_matches_oracle():
     reproduces it, tests/test_rrt.py) and the oracle's outcomes at x0 and x0 +- 1e-13 are the fixture
     tests/golden/oracle_outcomes.npz (its 1000-iteration N = 100 solves take minutes of CPU).  Split parity
     (tests/outcomes.py): identical status and final cost within 1e-4 on every oracle-reproducible instance, the
-    oracle's own spread on the chaotic ones; and every instance the GPU reports solved satisfies its constraints
+    oracle's own spread on the chaotic ones; a solve floor (the GPU solves at least as many instances as the perturbed
+    oracle run that solves fewest, less one, and at least one; jointly solved instances end within 10 % of the
+    oracle's cost — the chaotic group's status agreement alone would pass a GPU that solves nothing here, where the
+    oracle's statuses are mostly failures); and every instance the GPU reports solved satisfies its constraints
     (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack)."""
     import os
 
@@ -65,6 +68,13 @@ def test_b6_batch_matches_oracle():
     st, cost = r["status"].cpu().numpy(), r["cost"].cpu().numpy()
     print("b6 batch statuses gpu", st.tolist(), "oracle", out["status"].tolist(), flush=True)
     check_outcome_parity("b6 (24, RRT init)", st, cost, out, min_reproducible=1)
+    floor = max(1, int(min((out["status"][k] == 0).sum() for k in range(out["status"].shape[0]))) - 1)
+    both = (st == 0) & (out["status"][0] == 0)
+    rel = np.abs(cost - out["cost"][0]) / np.abs(out["cost"][0])
+    print(f"b6 solved: gpu {int((st == 0).sum())}, floor {floor}, jointly {int(both.sum())}, "
+          f"max relative cost difference {rel[both].max() if both.any() else 0.0:.3g}", flush=True)
+    assert (st == 0).sum() >= floor
+    assert (rel[both] <= 0.1).all(), rel[both]
     X, U = r["X"].cpu().numpy(), r["U"].cpu().numpy()
     for i in np.where(st == 0)[0]:
         assert np.abs(X[i, 0] - X0[i]).max() < 1e-4

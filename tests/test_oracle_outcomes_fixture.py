@@ -1,24 +1,35 @@
-"""tests/golden/oracle_outcomes.npz still describes this oracle (CPU): the GPU parity tests compare against its stored
-oracle outcomes (tests/outcomes.py), so a change of the oracle's arithmetic must regenerate it
-(tests/golden/make_oracle_outcomes.py).  Re-runs the fixture's quickest instances (fewest iterations) at x0,
-two perturbed starts and the reverse-order net and asks for bitwise the same status, iterations and final cost."""
+"""tests/golden/oracle_outcomes.npz (the reference's constraint-row bounds) and oracle_outcomes_varbounds.npz still
+describe this oracle (CPU): the GPU parity tests compare against their stored oracle outcomes (tests/outcomes.py) and
+pinned iterates (tests/test_pinned_iterates_gpu.py), so a change of the oracle's arithmetic must regenerate them
+(tests/golden/make_oracle_outcomes.py).  Re-runs the fixture's quickest instances (fewest iterations) at x0, two
+perturbed starts and the reverse-order net and asks for bitwise the same status, iterations and final cost, and a
+few pinned iterates (max_iter = k_i) bitwise."""
 import os
 
 import numpy as np
+import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+FILES = {"rows": "oracle_outcomes.npz", "varbounds": "oracle_outcomes_varbounds.npz"}
 
 
-def _fixture():
-    return dict(np.load(os.path.join(HERE, "golden", "oracle_outcomes.npz")))
+def _fixture(form="rows"):
+    return dict(np.load(os.path.join(HERE, "golden", FILES[form])))
 
 
-def test_fixture_layout():
-    f = _fixture()
-    for case, n in (("metric", 128), ("b6", 24)):
+@pytest.mark.parametrize("form", list(FILES))
+def test_fixture_layout(form):
+    f = _fixture(form)
+    assert int(f["general_bounds"]) == (1 if form == "rows" else 0)
+    for case, n, N, nx in (("metric", 128, 50, 5), ("b6", 24, 100, 7)):
         assert f[f"{case}_x0"].shape[0] == n and f[f"{case}_status"].shape == (6, n)
         assert f[f"{case}_cost"].shape == (6, n) and f[f"{case}_iters"].shape == (6, n)
         assert f[f"{case}_xdev"].shape == (6, n) and (f[f"{case}_xdev"][0] == 0).all()
+        assert f[f"{case}_trials"].shape == (6, n) and (f[f"{case}_trials"] >= 0).all()
+        kp = f[f"{case}_kpin"]
+        assert kp.shape == (n,) and (kp >= 0).all() and (kp <= 200).all() and (kp <= f[f"{case}_iters"].min(0)).all()
+        assert f[f"{case}_Xpin"].shape == (n, N + 1, nx) and f[f"{case}_Upin"].shape == (n, N, 2)
+        assert (f[f"{case}_pin_spread"] <= 1e-5).all()
     assert f["b6_xinit"].shape == (24, 101, 7)
     # the split has both groups on the headline workload (tests/outcomes.py)
     import sys
@@ -31,14 +42,15 @@ def test_fixture_layout():
     assert 0 < R.sum() < len(R)
 
 
-def test_fixture_matches_oracle():
+@pytest.mark.parametrize("form", list(FILES))
+def test_fixture_matches_oracle(form):
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
 
-    f = _fixture()
-    opt = _abi.default_options()
+    f = _fixture(form)
+    opt = _abi.default_options(general_bounds=int(f["general_bounds"]))
     hm = O.HostMlp(MlpWeights.artefact())
     its = f["metric_iters"][0]
     import sys
@@ -61,3 +73,9 @@ def test_fixture_matches_oracle():
     res = O.solve_one(B6_PROBLEM, f["b6_x0"][i], f["b6_xg"][i], hm6, opt=opt, X_init=f["b6_xinit"][i])
     assert res["status"] == f["b6_status"][0, i] and res["iters"] == f["b6_iters"][0, i]
     assert res["cost"] == f["b6_cost"][0, i]
+    # pinned iterates: the unperturbed run stopped at max_iter = k_i returns the stored iterate bitwise
+    kp = f["metric_kpin"]
+    for i in list(np.argsort(kp, kind="stable")[:2]) + [int(np.argmax(kp))]:
+        o = _abi.default_options(general_bounds=int(f["general_bounds"]), max_iter=int(kp[i]))
+        res = O.solve_one(METRIC_PROBLEM, f["metric_x0"][i], f["metric_xg"][i], hm, opt=o)
+        assert (res["X"] == f["metric_Xpin"][i]).all() and (res["U"] == f["metric_Upin"][i]).all(), (i, kp[i])

@@ -71,10 +71,15 @@ def test_iterates_match_oracle_learned(artefact, strategy):
         np.testing.assert_allclose(rg["U"][0].cpu().numpy(), rc["U"], atol=1e-4)
 
 
-def _fixture():
+def _fixture(form="rows"):
+    """tests/golden/make_oracle_outcomes.py's outcomes: the reference's constraint-row bounds (the default) or the
+    variable-bound form"""
     import os
 
-    return dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_outcomes.npz")))
+    name = "oracle_outcomes.npz" if form == "rows" else "oracle_outcomes_varbounds.npz"
+    f = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)))
+    assert int(f["general_bounds"]) == (1 if form == "rows" else 0)
+    return f
 
 
 @pytest.mark.parametrize("strategy", list(STRATEGIES))
@@ -104,9 +109,11 @@ def test_batch_b2_analytic_matches_oracle(strategy):
     assert ((sg == 0) & (out["status"][0] == 0)).sum() >= 0.5 * len(x0), info
 
 
-def test_batch_learned_sdf_matches_oracle(artefact):
+@pytest.mark.parametrize("form", ["rows", "varbounds"])
+def test_batch_learned_sdf_matches_oracle(artefact, form):
     """The metric workload (learned SDF, the reference's settings: tol 1e-4, max_iter 1000, adaptive mu,
-    restoration) on the 128 seeded instances of tests/golden/oracle_outcomes.npz, whose oracle outcomes under the six
+    restoration; the bounds as constraint rows, and as variable bounds) on the 128 seeded instances of
+    tests/golden/oracle_outcomes*.npz, whose oracle outcomes under the six
     perturbations of tests/outcomes.PERTURBATIONS the fixture holds (tests/golden/make_oracle_outcomes.py; the
     oracle's 1000-iteration runs take minutes of CPU).  Split parity (tests/outcomes.py): identical status and final cost within 1e-4 on every
     oracle-reproducible instance; the oracle's own spread on the chaotic ones."""
@@ -116,14 +123,14 @@ def test_batch_learned_sdf_matches_oracle(artefact):
     from nlotrajectories_amd.problem import METRIC_PROBLEM
     from nlotrajectories_amd.solver import solve_batch
 
-    f = _fixture()
+    f = _fixture(form)
     out = {k: f[f"metric_{k}"] for k in ("status", "cost", "iters", "xdev")}
     rg = solve_batch(METRIC_PROBLEM, f["metric_x0"], f["metric_xg"], mlp=DeviceMlp(artefact),
-                     options=_abi.gpu_options())
+                     options=_abi.gpu_options(general_bounds=int(f["general_bounds"])))
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
     print("metric GPU status counts", np.bincount(sg, minlength=7).tolist(), "oracle",
           np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
-    check_outcome_parity("metric (128, max_iter 1000)", sg, cg, out, min_reproducible=24)
+    check_outcome_parity(f"metric {form} (128, max_iter 1000)", sg, cg, out, min_reproducible=24)
 
 
 def test_safeguards_iterate_parity(artefact):
