@@ -442,6 +442,17 @@ def main():
             mlp_value["overlap_note"] = note.replace("%%", "%")
             mlp_full["overlap_note"] = ("the full launch shares the CUs with the early value launch of the previous "
                                         "step's candidates (fourth stream); its event-timed duration includes that")
+        # per-dispatch fractions from the profiler (the event brackets above include the streams' overlap): committed
+        # from a rocprofv3 --kernel-trace --stats run of this command (scripts/rocprof_fracs.py)
+        df = os.path.join(ROOT, "profiles", "r05", "mlp_dispatch_fracs_r05c.json")
+        if os.path.exists(df) and not (stress or b6):
+            with open(df) as fh:
+                dd = json.load(fh)
+            src = os.path.relpath(df, ROOT)
+            mlp_full["rocprof_dispatch_frac"] = {"frac": dd["full"]["frac"], "avg_dispatch_ms": dd["full"]["avg_dispatch_ms"],
+                                                 "source": src}
+            mlp_value["rocprof_dispatch_frac"] = {"frac": dd["value"]["frac"], "avg_step_ms": dd["value"]["avg_step_ms"],
+                                                  "source": src}
         # the dominant kernel by device time: k_ric on the metric workload, the SDF-MLP on the stress workload
         if stress:
             rooflines = {"roofline": mlp_full, "roofline_mlp_value": mlp_value, "roofline_ric": ric}
