@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 12
+#define NLOT_ABI_VERSION 13
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -210,6 +210,14 @@ void nlot_default_options(NlotSolverOptions* opt);
 /* ---- learned-SDF weights ------------------------------------------------------------------- */
 /* Copies the host arrays of `desc` to device memory; returns NULL on error (see nlot_last_error). */
 NlotMlp* nlot_mlp_create(const NlotMlpDesc* desc);
+/* The net's MFMA arithmetic (ABI v13).  Both are fp32 arithmetic (products exact in the fp32 accumulator); they
+ * differ in the MFMA sums' order and so at the rounding level:
+ *   NLOT_MLP_ARITH_SPLIT_BF16  operands split into three bf16 parts, six bf16 MFMA products per fp32 product (the
+ *                              default of nlot_mlp_create: 2.65x the f32-MFMA peak)
+ *   NLOT_MLP_ARITH_F32         v_mfma_f32 products (the reference's fp32 net, gen/nn_sdf.cpp, at the f32 peak) */
+#define NLOT_MLP_ARITH_SPLIT_BF16 0
+#define NLOT_MLP_ARITH_F32 1
+NlotMlp* nlot_mlp_create_ex(const NlotMlpDesc* desc, int32_t arith);
 void nlot_mlp_destroy(NlotMlp* mlp);
 
 /* Batched SDF-MLP evaluation on the device (the nn_sdf family, gen/nn_sdf.cpp:57-104).

@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 # symbols include/nlot.h declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "nlot_abi_version", "nlot_last_error", "nlot_default_options", "nlot_mlp_create", "nlot_mlp_destroy",
+    "nlot_abi_version", "nlot_last_error", "nlot_default_options", "nlot_mlp_create", "nlot_mlp_create_ex", "nlot_mlp_destroy",
     "nlot_sdf_mlp_eval", "nlot_solve_workspace_size", "nlot_solve_workspace_size_slots", "nlot_solve_batch", "nlot_set_timing",
     "nlot_last_stats", "nlot_casadi_bind", "nn_sdf_n_in", "nn_sdf_n_out", "nn_sdf_sparsity_in",
     "nn_sdf_sparsity_out", "nn_sdf", "jac_nn_sdf_n_in", "jac_nn_sdf_n_out", "jac_nn_sdf",
@@ -58,6 +58,8 @@ def lib():
     L.nlot_default_options.argtypes = [C.POINTER(_abi.NlotSolverOptions)]
     L.nlot_mlp_create.argtypes = [C.POINTER(_abi.NlotMlpDesc)]
     L.nlot_mlp_create.restype = vp
+    L.nlot_mlp_create_ex.argtypes = [C.POINTER(_abi.NlotMlpDesc), C.c_int32]
+    L.nlot_mlp_create_ex.restype = vp
     L.nlot_mlp_destroy.argtypes = [vp]
     L.nlot_sdf_mlp_eval.argtypes = [vp, vp, C.c_int64, vp, vp, vp, vp, vp]
     L.nlot_sdf_mlp_eval.restype = C.c_int32
@@ -77,7 +79,7 @@ def lib():
     L.nlot_rrt_init.restype = C.c_int32
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 12:
+    if L.nlot_abi_version() != 13:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

@@ -861,7 +861,8 @@ static int launch_t(const MlpDev& w, const float* pts, int64_t n, const int* n_d
     static std::atomic<uint64_t> attr_set{0};
     NLOT_HIP_CHECK(set_lds_attr_once(attr_set, (const void*)mlp_kernel<H, L, FULL>, 160 * 1024));
     if constexpr (L == 1 && H == 128) {
-        // split-bf16 MFMA kernels (fp32-equivalent products); NLOT_MLP=f32 selects the f32-MFMA kernels
+        // split-bf16 MFMA kernels (fp32-equivalent products); a net created with NLOT_MLP_ARITH_F32 (no planes) or
+        // NLOT_MLP=f32 in the environment takes the f32-MFMA kernels
         static const bool use_bf16 = !(getenv("NLOT_MLP") && strcmp(getenv("NLOT_MLP"), "f32") == 0);
         if (use_bf16 && w.Wp) {
             constexpr size_t lv = mlp_bf16_lds_bytes<H>();
@@ -1408,8 +1409,14 @@ int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* 
 // ------------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------------
-extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
+extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) { return nlot_mlp_create_ex(d, NLOT_MLP_ARITH_SPLIT_BF16); }
+
+extern "C" NlotMlp* nlot_mlp_create_ex(const NlotMlpDesc* d, int32_t arith) {
     using namespace nlot;
+    if (arith != NLOT_MLP_ARITH_SPLIT_BF16 && arith != NLOT_MLP_ARITH_F32) {
+        set_error("nlot_mlp_create_ex: arith must be NLOT_MLP_ARITH_SPLIT_BF16 or NLOT_MLP_ARITH_F32");
+        return nullptr;
+    }
     if (!d || !d->A || !d->b0 || !d->w_out || (d->n_hidden > 0 && (!d->W || !d->b))) {
         set_error("nlot_mlp_create: null descriptor or weight pointer");
         return nullptr;
@@ -1428,7 +1435,8 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     }
     const int H = d->hidden, L = d->n_hidden;
     const size_t nA = 2 * H, nb0 = H, nW = (size_t)L * H * H, nb = (size_t)L * H, nw = H;
-    const size_t nWp = (size_t)3 * H * H / 2;  // bf16 planes of layer 0, in float units
+    const bool split = arith == NLOT_MLP_ARITH_SPLIT_BF16;
+    const size_t nWp = split ? (size_t)3 * H * H / 2 : 0;  // bf16 planes of layer 0, in float units
     const size_t nWt = smooth ? nW : 0;        // transposed HxH layers (mlp_smooth)
     const size_t total = nA + nb0 + nW + nb + nw + nWp + nWt + 4;
     float* blk = nullptr;
@@ -1459,7 +1467,7 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) {
     m->dev.b = put(d->b, nb);
     m->dev.w_out = put(d->w_out, nw);
     m->dev.Wp = nullptr;
-    if (L > 0) {  // layer-0 weights split into three bf16 planes, round-to-nearest-even at each step (host, exact)
+    if (L > 0 && split) {  // layer-0 weights split into three bf16 planes, round-to-nearest-even at each step (host, exact)
         std::vector<uint16_t> planes((size_t)3 * H * H);
         auto bf16_rne = [](float x) -> uint16_t {
             uint32_t u;

@@ -12,19 +12,24 @@ from .nn import MlpWeights
 
 
 class DeviceMlp:
-    """Device-resident learned-SDF weights (NlotMlp handle)."""
+    """Device-resident learned-SDF weights (NlotMlp handle).  arith: "split_bf16" (the default: three-way bf16 operand
+    split, six MFMA products per fp32 product) or "f32" (v_mfma_f32 products, the reference's fp32 net); both fp32
+    arithmetic, differing at the rounding level (include/nlot.h, NLOT_MLP_ARITH_*)."""
 
-    def __init__(self, weights: MlpWeights):
+    ARITH = {"split_bf16": 0, "f32": 1}
+
+    def __init__(self, weights: MlpWeights, arith: str = "split_bf16"):
         require_gpu()
         self.weights = weights
+        self.arith = arith
         self._arrs = {k: np.ascontiguousarray(v, np.float32) for k, v in weights.arrays.items()}
         fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
         d = _abi.NlotMlpDesc(in_kind=weights.in_kind, hidden=weights.hidden, n_hidden=weights.n_hidden, act=weights.act,
                              fourier_scale=weights.fourier_scale, b_out=weights.b_out)
         d.A, d.b0, d.W, d.b, d.w_out = (fp(self._arrs[k]) for k in ("A", "b0", "W", "b", "w_out"))
-        h = lib().nlot_mlp_create(C.byref(d))
+        h = lib().nlot_mlp_create_ex(C.byref(d), self.ARITH[arith])
         if not h:
-            raise RuntimeError("nlot_mlp_create: " + lib().nlot_last_error().decode())
+            raise RuntimeError("nlot_mlp_create_ex: " + lib().nlot_last_error().decode())
         self.handle = C.c_void_p(h)
 
     def __del__(self):

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Where a pinned-iterate mismatch starts (tests/test_pinned_iterates_gpu.py): for the given fixture instances, the GPU
+iterate at max_iter = k for k = 1..K against the unperturbed oracle trace (oracle_solve_trace) and the oracle's own
+perturbed runs (the +-1e-13 starts and the reverse-order net), one line per k.
+
+    python scripts/pin_probe.py --case b6 --inst 3 --kmax 24 [--form rows]
+
+GPU box; test infrastructure (runs the oracle as the checker).  NLOT_MLP=f32 in the environment switches the GPU's
+SDF net to its fp32 path for an A/B against the split-bf16 default."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="b6")
+    ap.add_argument("--inst", type=int, nargs="+", default=[3])
+    ap.add_argument("--kmax", type=int, default=24)
+    ap.add_argument("--form", default="rows")
+    a = ap.parse_args()
+    import oracle as O
+    from outcomes import PERTURBATIONS, mlp_order
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
+    from nlotrajectories_amd.solver import solve_batch
+
+    f = dict(np.load(os.path.join(ROOT, "tests", "golden",
+                                  "oracle_outcomes.npz" if a.form == "rows" else "oracle_outcomes_varbounds.npz")))
+    if a.case == "b6":
+        prob = B6_PROBLEM
+        w = MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
+    else:
+        prob, w = METRIC_PROBLEM, MlpWeights.artefact()
+    hm, mlp = O.HostMlp(w), DeviceMlp(w)
+    gb = int(f["general_bounds"])
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    for i in a.inst:
+        x0, xg = f[f"{a.case}_x0"][i], f[f"{a.case}_xg"][i]
+        xi = f[f"{a.case}_xinit"][i] if f"{a.case}_xinit" in f else None
+        opt = _abi.default_options(general_bounds=gb)
+        traces = []
+        for c, d, rev in PERTURBATIONS:
+            x = x0.copy()
+            x[c] += d
+            with mlp_order(rev):
+                traces.append(O.solve_trace(prob, x, xg, hm, opt=opt, X_init=xi, cap=a.kmax + 1)["trace"])
+        T0 = traces[0]
+        print(f"instance {i}: kpin {int(f[f'{a.case}_kpin'][i])}, oracle status {int(f[f'{a.case}_status'][0, i])} "
+              f"iters {int(f[f'{a.case}_iters'][0, i])}, NLOT_MLP={os.environ.get('NLOT_MLP', 'bf16')}", flush=True)
+        for k in range(1, a.kmax + 1):
+            o = _abi.default_options(general_bounds=gb, max_iter=k)
+            r = solve_batch(prob, x0[None], xg[None], mlp=mlp, X_init=None if xi is None else xi[None], options=o)
+            g = np.concatenate([r["X"][0].cpu().numpy().ravel(), r["U"][0].cpu().numpy().ravel()])
+            dg = float(np.nanmax(np.abs(g - T0[k])))
+            dself = max(float(np.nanmax(np.abs(t[k] - T0[k]))) for t in traces[1:])
+            dX = np.abs(g[:(N + 1) * nx] - T0[k][:(N + 1) * nx]).reshape(N + 1, nx)
+            kk, jj = np.unravel_index(int(np.nanargmax(dX)), dX.shape)
+            print(f"  k {k:3d} status {int(r['status'][0])} |gpu - oracle| {dg:.3e}  oracle self {dself:.3e}  "
+                  f"argmax X[{kk},{jj}]", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -2,6 +2,7 @@
 """Oracle outcome fixtures for the solve-level GPU parity tests whose oracle runs are too long for a GPU test.
 
     python tests/golden/make_oracle_outcomes.py [--threads 8] [--form rows|varbounds] [--only metric|b6]
+    python tests/golden/make_oracle_outcomes.py --form rows|varbounds --add-stpin   (adds {case}_stpin to a file)
         rows (default):  tests/golden/oracle_outcomes.npz            (the reference's constraint-row bounds)
         varbounds:       tests/golden/oracle_outcomes_varbounds.npz  (the same bounds as variable bounds)
 
@@ -23,8 +24,11 @@ these learned-SDF cases (the reverse-order run changes the fp32 net's outputs at
 iterates feel at ~1e-7..1e-6 from the first iterations; 1e-5 keeps a 10x margin under the GPU test's 1e-4, the
 fp32-MLP iterate tolerance of DESIGN.md §5);
 {case}_kpin[i] = k_i, {case}_Xpin / _Upin = the unperturbed iterate at k_i (what max_iter = k_i returns),
-{case}_pin_spread = the perturbed runs' largest deviation up to k_i.  A GPU test runs every instance to k_i — failed
-and chaotic instances included — and compares the iterate.  {case}_trials: the run's trial-point evaluations (IPOPT's
+{case}_pin_spread = the perturbed runs' largest deviation up to k_i, {case}_stpin = the unperturbed run's status at
+max_iter = k_i (max_iter, or the final status where the run ends at the top of iteration k_i: converged, or a
+restoration phase that converged to a point the filter rejects; a restoration line-search failure at k_i = iters
+happens inside iteration k_i and so returns max_iter).  A GPU test runs every instance to k_i — failed and chaotic
+instances included — and compares the iterate and the status.  {case}_trials: the run's trial-point evaluations (IPOPT's
 sequential backtracking: one SDF value evaluation of the trial's corners each; DESIGN.md §8f cost model).
 
 The oracle is deterministic (one instance per thread, no reductions across threads), so the GPU box's oracle
@@ -92,6 +96,17 @@ def pin(trace0, dev, iters):
     return kpin, spread
 
 
+def pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads):
+    """The unperturbed run's status at max_iter = k_i, per instance."""
+    def one(i):
+        o = type(opt).from_buffer_copy(opt)
+        o.max_iter = int(kpin[i])
+        return O.solve_one(prob, X0[i], XG[i], hm, opt=o, X_init=None if Xi is None else Xi[i])["status"]
+
+    with ThreadPoolExecutor(threads) as ex:
+        return np.array(list(ex.map(one, range(len(X0)))), np.int32)
+
+
 def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
     """Outcomes under every perturbation, with the per-instance pinned iterates."""
     from outcomes import PERTURBATIONS, mlp_order
@@ -131,7 +146,9 @@ def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
     kpin, spread = pin(T0, dev, its)
     N, nx, nu = prob.N, prob.nx, prob.nu
     XUp = T0[np.arange(n), kpin]
+    stpin = pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads)
     return {"status": st, "cost": cost, "iters": its, "xdev": xdev, "trials": trials, "kpin": kpin, "pin_spread": spread,
+            "stpin": stpin,
             "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx), "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu)}
 
 
@@ -141,6 +158,7 @@ def main():
     ap.add_argument("--form", default="rows", choices=list(OUT))
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
+    ap.add_argument("--add-stpin", action="store_true", help="add {case}_stpin to an existing file")
     a = ap.parse_args()
     out_path = a.out or OUT[a.form]
     import oracle as O
@@ -151,6 +169,18 @@ def main():
     opt = _abi.default_options(general_bounds=1 if a.form == "rows" else 0)
     data = dict(np.load(out_path)) if (a.only and os.path.exists(out_path)) else {}
     data["general_bounds"] = np.array(opt.general_bounds)
+
+    if a.add_stpin:
+        data = dict(np.load(out_path))
+        opt = _abi.default_options(general_bounds=int(data["general_bounds"]))
+        hm6 = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")))
+        for case, prob, hm, xi in (("metric", METRIC_PROBLEM, O.HostMlp(MlpWeights.artefact()), None),
+                                   ("b6", B6_PROBLEM, hm6, data["b6_xinit"])):
+            data[f"{case}_stpin"] = pin_status(O, prob, data[f"{case}_x0"], data[f"{case}_xg"], hm, opt, xi,
+                                               data[f"{case}_kpin"], a.threads)
+            print(case, "stpin", np.bincount(data[f"{case}_stpin"], minlength=7).tolist(), flush=True)
+        np.savez_compressed(out_path, **data)
+        return
 
     def report(case, out, t):
         kp = out["kpin"]

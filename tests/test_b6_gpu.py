@@ -53,21 +53,39 @@ def test_b6_batch_matches_oracle():
     oracle run that solves fewest, less one, and at least one; jointly solved instances end within 10 % of the
     oracle's cost — the chaotic group's status agreement alone would pass a GPU that solves nothing here, where the
     oracle's statuses are mostly failures); and every instance the GPU reports solved satisfies its constraints
-    (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack)."""
+    (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack).  Run with the f32 net (every
+    reproducible instance) and with the product's split-bf16 net (every one but one that the f32 net hits and the
+    split-bf16 net's rounding moves: outcomes.rounding_excused).  A reproducible instance the GPU misses is run from
+    twelve more oracle starts (outcomes.WIDE, x0 +- 1e-11 .. 1e-7): fixture instance 18, whose oracle paths part at
+    iteration 37 and meet again at the restoration failure of iteration 404 under the fixture's six runs, ends in
+    max_iter from x0 + 1e-7 e_y, as it does on the GPU's split-bf16 net."""
     import os
 
-    O, prob, b, mlp, hm = _setup()
-    from outcomes import check_outcome_parity
+    O, prob, b, _, hm = _setup()
+    from outcomes import WIDE, check_outcome_parity, oracle_outcomes, rounding_excused
     from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp
     from nlotrajectories_amd.solver import solve_batch
 
     f = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_outcomes.npz")))
     X0, XG, Xi = f["b6_x0"], f["b6_xg"], f["b6_xinit"]
     out = {k: f[f"b6_{k}"] for k in ("status", "cost", "iters", "xdev")}
-    r = solve_batch(prob, X0, XG, mlp=mlp, X_init=Xi, options=_abi.default_options())
-    st, cost = r["status"].cpu().numpy(), r["cost"].cpu().numpy()
-    print("b6 batch statuses gpu", st.tolist(), "oracle", out["status"].tolist(), flush=True)
-    check_outcome_parity("b6 (24, RRT init)", st, cost, out, min_reproducible=1)
+    opt = _abi.default_options()
+    widen = lambda i: oracle_outcomes(O, prob, X0[i], XG[i], hm, opt=opt, X_init=Xi[i], perturbations=WIDE)
+    w = MlpWeights.load(os.path.join(DATA, "b6_mlp128_seed0.npz"))
+    res = {}
+    for arith in ("f32", "split_bf16"):
+        r = solve_batch(prob, X0, XG, mlp=DeviceMlp(w, arith), X_init=Xi, options=opt)
+        res[arith] = (r["status"].cpu().numpy(), r["cost"].cpu().numpy())
+        print("b6 batch statuses", arith, "gpu", res[arith][0].tolist(), flush=True)
+    print("b6 batch statuses oracle", out["status"].tolist(), flush=True)
+    check_outcome_parity("b6 (24, RRT init) f32 net", *res["f32"], out, min_reproducible=1, widen=widen)
+    ex = rounding_excused(out, *res["f32"], *res["split_bf16"])
+    print("b6 split-bf16 net: excused", np.nonzero(ex)[0].tolist(), flush=True)
+    assert ex.sum() <= 1
+    check_outcome_parity("b6 (24, RRT init) split-bf16 net", *res["split_bf16"], out, widen=widen, excused=ex)
+    st, cost = res["split_bf16"]
     floor = max(1, int(min((out["status"][k] == 0).sum() for k in range(out["status"].shape[0]))) - 1)
     both = (st == 0) & (out["status"][0] == 0)
     rel = np.abs(cost - out["cost"][0]) / np.abs(out["cost"][0])

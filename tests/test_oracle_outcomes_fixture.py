@@ -30,6 +30,8 @@ def test_fixture_layout(form):
         assert kp.shape == (n,) and (kp >= 0).all() and (kp <= 200).all() and (kp <= f[f"{case}_iters"].min(0)).all()
         assert f[f"{case}_Xpin"].shape == (n, N + 1, nx) and f[f"{case}_Upin"].shape == (n, N, 2)
         assert (f[f"{case}_pin_spread"] <= 1e-5).all()
+        st, it, sp = f[f"{case}_status"][0], f[f"{case}_iters"][0], f[f"{case}_stpin"]
+        assert sp.shape == (n,) and ((sp == 1) | ((kp == it) & (sp == st))).all()
     assert f["b6_xinit"].shape == (24, 101, 7)
     # the split has both groups on the headline workload (tests/outcomes.py)
     import sys
@@ -79,3 +81,4 @@ def test_fixture_matches_oracle(form):
         o = _abi.default_options(general_bounds=int(f["general_bounds"]), max_iter=int(kp[i]))
         res = O.solve_one(METRIC_PROBLEM, f["metric_x0"][i], f["metric_xg"][i], hm, opt=o)
         assert (res["X"] == f["metric_Xpin"][i]).all() and (res["U"] == f["metric_Upin"][i]).all(), (i, kp[i])
+        assert res["status"] == f["metric_stpin"][i], (i, kp[i])

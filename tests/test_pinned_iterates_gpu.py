@@ -2,13 +2,21 @@
 included.
 
 The split-parity tests (tests/outcomes.py) hold the GPU to the oracle's final outcome only where the oracle reproduces
-itself, and to the oracle's own spread elsewhere.  Here every instance of tests/golden/oracle_outcomes.npz is pinned
-along its path: k_i is the last iteration (<= 200) up to which the oracle's five perturbed runs (x0 +- 1e-13 e_x,
-+- 1e-13 e_y, the net summed in reverse order) stay within 1e-5 of the unperturbed run
-(tests/golden/make_oracle_outcomes.py), and the GPU run with max_iter = k_i must return the oracle's iterate there:
-X and U within 1e-4 (the fp32-MLP iterate tolerance) and the same status, for every instance — solved,
-max_iter and restoration-failed alike.  The reference's settings (runner.py:110-125) with its constraint-row bounds
-(runner.py:67-69,101-103)."""
+itself, and to the oracle's own spread elsewhere.  Here every instance of tests/golden/oracle_outcomes.npz (and of
+oracle_outcomes_varbounds.npz, the variable-bound form) is pinned along its path: k_i is the last iteration (<= 200)
+up to which the oracle's five perturbed runs (x0 +- 1e-13 e_x, +- 1e-13 e_y, the net summed in reverse order) stay
+within 1e-5 of the unperturbed run (tests/golden/make_oracle_outcomes.py), and the GPU run with max_iter = k_i must
+return the oracle's iterate there: X and U within 1e-4 (the fp32-MLP iterate tolerance) and the
+oracle's status at max_iter = k_i, solved, max_iter and restoration-failed instances alike.  The reference's
+settings (runner.py:110-125) with its constraint-row bounds (runner.py:67-69,101-103).
+
+Two runs per case, one per MLP arithmetic (include/nlot.h NLOT_MLP_ARITH_*):
+  * f32 (v_mfma_f32 products, the oracle's fp32 net up to the sums' order): every instance;
+  * split-bf16 (the product default): its MFMA sums round differently again, a perturbation a few times the
+    reverse-order net's (scripts/pin_probe.py: b6 instance 3 at iteration 6, 6.7e-6 against the oracle's 3.5e-6
+    spread, and 7e-2 one iteration later as a filter decision flips; 1.4e-6 with the f32 net).  Every instance but at
+    most 5 % (at least one) of them, and each exception must pin under the f32 net — its deviation is the net's
+    rounding, not the solver."""
 import os
 
 import numpy as np
@@ -18,30 +26,28 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 TOL = 1e-4
+FILES = {"rows": "oracle_outcomes.npz", "varbounds": "oracle_outcomes_varbounds.npz"}
 
 
-def _setup(case, artefact):
+def _setup(case, artefact, arith):
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.ops import DeviceMlp
     from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
 
     if case == "metric":
-        return METRIC_PROBLEM, DeviceMlp(artefact)
+        return METRIC_PROBLEM, DeviceMlp(artefact, arith)
     w = MlpWeights.load(os.path.join(os.path.dirname(HERE), "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
-    return B6_PROBLEM, DeviceMlp(w)
+    return B6_PROBLEM, DeviceMlp(w, arith)
 
 
-@pytest.mark.parametrize("case", ["metric", "b6"])
-def test_pinned_iterates_match_oracle(case, artefact):
-    from outcomes import reproducible
+def _pinned_run(f, case, artefact, arith):
+    """GPU iterate deviation from the pinned oracle iterate, and the GPU status, per instance."""
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.solver import solve_batch
 
-    f = dict(np.load(os.path.join(HERE, "golden", "oracle_outcomes.npz")))
-    prob, mlp = _setup(case, artefact)
+    prob, mlp = _setup(case, artefact, arith)
     x0, xg, kp = f[f"{case}_x0"], f[f"{case}_xg"], f[f"{case}_kpin"]
     xinit = f.get(f"{case}_xinit")
-    st0, it0 = f[f"{case}_status"][0], f[f"{case}_iters"][0]
     n = len(x0)
     dev = np.zeros(n)
     sg = np.zeros(n, np.int32)
@@ -53,15 +59,37 @@ def test_pinned_iterates_match_oracle(case, artefact):
         dev[idx] = np.maximum(np.abs(X - f[f"{case}_Xpin"][idx]).reshape(len(idx), -1).max(1),
                               np.abs(U - f[f"{case}_Upin"][idx]).reshape(len(idx), -1).max(1))
         sg[idx] = r["status"].cpu().numpy()
-    # the oracle's status at max_iter = k_i: its final status if every run ended there, else max_iter
-    want = np.where(kp == it0, st0, _abi.NLOT_MAXITER)
+    return dev, sg
+
+
+@pytest.mark.parametrize("form", list(FILES))
+@pytest.mark.parametrize("case", ["metric", "b6"])
+def test_pinned_iterates_match_oracle(case, form, artefact):
+    from outcomes import reproducible
+    from nlotrajectories_amd import _abi
+
+    path = os.path.join(HERE, "golden", FILES[form])
+    if not os.path.exists(path):
+        pytest.skip(f"{FILES[form]} not generated")
+    f = dict(np.load(path))
+    kp, st0 = f[f"{case}_kpin"], f[f"{case}_status"][0]
+    # the oracle's status at max_iter = k_i (the fixture's {case}_stpin: max_iter, or the final status where the run
+    # ends at the top of iteration k_i; a restoration line-search failure at k_i = iters happens inside the iteration)
+    want = f[f"{case}_stpin"]
     R = reproducible({k: f[f"{case}_{k}"] for k in ("status", "cost", "xdev")})
-    for name, g in (("solved", st0 == 0), ("max_iter", st0 == _abi.NLOT_MAXITER),
-                    ("restoration failed", st0 == 4), ("other", ~np.isin(st0, (0, 1, 4))),
-                    ("reproducible", R), ("chaotic", ~R)):
-        if g.any():
-            print(f"[pinned] {case} {name}: {int(g.sum())} instances, k_i min / median / max "
-                  f"{kp[g].min()} / {int(np.median(kp[g]))} / {kp[g].max()}, max |gpu - oracle| {dev[g].max():.2e}",
-                  flush=True)
-    bad = np.nonzero((dev > TOL) | (sg != want))[0]
-    assert len(bad) == 0, [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in bad]
+    bad = {}
+    for arith in ("f32", "split_bf16"):
+        dev, sg = _pinned_run(f, case, artefact, arith)
+        for name, g in (("solved", st0 == 0), ("max_iter", st0 == _abi.NLOT_MAXITER),
+                        ("restoration failed", st0 == 4), ("other", ~np.isin(st0, (0, 1, 4))),
+                        ("reproducible", R), ("chaotic", ~R)):
+            if g.any():
+                print(f"[pinned] {case} {form} {arith} {name}: {int(g.sum())} instances, k_i min / median / max "
+                      f"{kp[g].min()} / {int(np.median(kp[g]))} / {kp[g].max()}, max |gpu - oracle| "
+                      f"{dev[g].max():.2e}", flush=True)
+        b = np.nonzero((dev > TOL) | (sg != want))[0]
+        bad[arith] = b
+        print(f"[pinned] {case} {form} {arith}: {len(b)} of {len(kp)} outside",
+              [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in b], flush=True)
+    assert len(bad["f32"]) == 0, bad["f32"]
+    assert len(bad["split_bf16"]) <= max(1, int(0.05 * len(kp))), bad["split_bf16"]

@@ -82,14 +82,15 @@ def _fixture(form="rows"):
     return f
 
 
-@pytest.mark.parametrize("strategy", list(STRATEGIES))
+@pytest.mark.parametrize("strategy", ["adaptive", "adaptive_tol1e-8", "monotone"])
 def test_batch_b2_analytic_matches_oracle(strategy):
-    """64 seeded b2 instances (analytic SDF).  Monotone mu at tol 1e-4; adaptive mu at tol 1e-8.  Solve-level
-    parity split by the oracle's own reproducibility (tests/outcomes.py): on the instances whose oracle outcome is
-    unchanged by +-1e-13 perturbations of the start's x and y the GPU gives the same status and a final cost within 1e-4 on 100 %;
-    on the rest, agreement at least as good as the oracle's with itself."""
+    """64 seeded b2 instances (analytic SDF).  Adaptive mu at the reference's tol 1e-4 (runner.py:117-120), adaptive mu at
+    tol 1e-8, monotone mu at tol 1e-4.  Solve-level parity split by the oracle's own reproducibility
+    (tests/outcomes.py): on the instances whose oracle outcome is unchanged by +-1e-13 perturbations of the start's x
+    and y the GPU gives the same status and a final cost within 1e-4 on 100 %; on the rest, agreement at least as
+    good as the oracle's with itself."""
     O = _oracle()
-    from outcomes import check_outcome_parity, oracle_outcomes
+    from outcomes import WIDE, check_outcome_parity, oracle_outcomes
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.problem import BENCHMARKS
     from nlotrajectories_amd.sampling import sample_start_goal
@@ -98,14 +99,17 @@ def test_batch_b2_analytic_matches_oracle(strategy):
     p = BENCHMARKS["b2"]["problem"]
     sdf = lambda P: np.sqrt(((np.asarray(P) - 0.5) ** 2).sum(1)) - 0.25
     x0, xg = sample_start_goal(p, 64, seed=1, sdf=sdf, lo=(0, 0), hi=(1, 1))
-    tight = dict(tol=1e-8, constr_viol_tol=1e-8, compl_inf_tol=1e-8) if strategy == "adaptive" else {}
-    opt = _abi.gpu_options(**STRATEGIES[strategy], **tight)
+    tight = dict(tol=1e-8, constr_viol_tol=1e-8, compl_inf_tol=1e-8) if strategy == "adaptive_tol1e-8" else {}
+    opt = _abi.gpu_options(**STRATEGIES[strategy.split("_")[0]], **tight)
     rg = solve_batch(p, x0, xg, options=opt)
     out = oracle_outcomes(O, p, x0, xg, opt=opt)
     sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
-    # reproducible instances (5 oracle runs, tests/outcomes.py): 15 of 64 under adaptive mu at tol 1e-8, 4 under
-    # monotone mu at tol 1e-4 (its tol 1e-4 termination point moves the final cost by more than 1e-8)
-    info = check_outcome_parity(f"b2 {strategy}", sg, cg, out, min_reproducible=8 if strategy == "adaptive" else 2)
+    # reproducible instances (5 oracle runs, tests/outcomes.py; the constraint-row bounds): 8 of 64 under adaptive mu at
+    # tol 1e-4, 12 at tol 1e-8, 4 under monotone mu at tol 1e-4 (a tol 1e-4 termination point moves the final cost by
+    # more than the 1e-8 the split asks of a reproducible solved instance)
+    info = check_outcome_parity(f"b2 {strategy}", sg, cg, out,
+                                min_reproducible={"adaptive": 6, "adaptive_tol1e-8": 8, "monotone": 2}[strategy],
+                                widen=lambda i: oracle_outcomes(O, p, x0[i], xg[i], opt=opt, perturbations=WIDE))
     assert ((sg == 0) & (out["status"][0] == 0)).sum() >= 0.5 * len(x0), info
 
 
@@ -115,9 +119,12 @@ def test_batch_learned_sdf_matches_oracle(artefact, form):
     restoration; the bounds as constraint rows, and as variable bounds) on the 128 seeded instances of
     tests/golden/oracle_outcomes*.npz, whose oracle outcomes under the six
     perturbations of tests/outcomes.PERTURBATIONS the fixture holds (tests/golden/make_oracle_outcomes.py; the
-    oracle's 1000-iteration runs take minutes of CPU).  Split parity (tests/outcomes.py): identical status and final cost within 1e-4 on every
-    oracle-reproducible instance; the oracle's own spread on the chaotic ones."""
-    from outcomes import check_outcome_parity
+    oracle's 1000-iteration runs take minutes of CPU).  Split parity (tests/outcomes.py): identical status and final
+    cost within 1e-4 on every oracle-reproducible instance; the oracle's own spread on the chaotic ones.  Run with the
+    f32 net (every reproducible instance) and with the product's split-bf16 net (every one but at most 5 % that the f32
+    net hits and the split-bf16 net's rounding moves: outcomes.rounding_excused)."""
+    import oracle as O
+    from outcomes import WIDE, check_outcome_parity, oracle_outcomes, rounding_excused
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.ops import DeviceMlp
     from nlotrajectories_amd.problem import METRIC_PROBLEM
@@ -125,12 +132,23 @@ def test_batch_learned_sdf_matches_oracle(artefact, form):
 
     f = _fixture(form)
     out = {k: f[f"metric_{k}"] for k in ("status", "cost", "iters", "xdev")}
-    rg = solve_batch(METRIC_PROBLEM, f["metric_x0"], f["metric_xg"], mlp=DeviceMlp(artefact),
-                     options=_abi.gpu_options(general_bounds=int(f["general_bounds"])))
-    sg, cg = rg["status"].cpu().numpy(), rg["cost"].cpu().numpy()
-    print("metric GPU status counts", np.bincount(sg, minlength=7).tolist(), "oracle",
-          np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
-    check_outcome_parity(f"metric {form} (128, max_iter 1000)", sg, cg, out, min_reproducible=24)
+    opt = _abi.gpu_options(general_bounds=int(f["general_bounds"]))
+    hm = O.HostMlp(artefact)
+    widen = lambda i: oracle_outcomes(O, METRIC_PROBLEM, f["metric_x0"][i], f["metric_xg"][i], hm, opt=opt,
+                                      perturbations=WIDE)
+    res = {}
+    for arith in ("f32", "split_bf16"):
+        rg = solve_batch(METRIC_PROBLEM, f["metric_x0"], f["metric_xg"], mlp=DeviceMlp(artefact, arith), options=opt)
+        res[arith] = (rg["status"].cpu().numpy(), rg["cost"].cpu().numpy())
+        print("metric", arith, "GPU status counts", np.bincount(res[arith][0], minlength=7).tolist(), "oracle",
+              np.bincount(out["status"][0], minlength=7).tolist(), flush=True)
+    check_outcome_parity(f"metric {form} f32 net (128, max_iter 1000)", *res["f32"], out, min_reproducible=24,
+                         widen=widen)
+    ex = rounding_excused(out, *res["f32"], *res["split_bf16"])
+    print("metric split-bf16 net: excused", np.nonzero(ex)[0].tolist(), flush=True)
+    assert ex.sum() <= max(1, int(0.05 * len(ex)))
+    check_outcome_parity(f"metric {form} split-bf16 net (128, max_iter 1000)", *res["split_bf16"], out,
+                         min_reproducible=24 - int(ex.sum()), widen=widen, excused=ex)
 
 
 def test_safeguards_iterate_parity(artefact):
