@@ -1109,6 +1109,11 @@ struct RicWpe {
 // maps x_{k+1} = (I + D P)^-1 (y - D (p + G nu)); every stage block must be positive definite.
 // SOC = true: the second-order corrections (SC_RICFIX >= 0) by substitution with the stored factors; the SOC = false
 // launch skips them (separate instantiations: the substitution's registers stay out of the factorising sweep's).
+#ifdef NLOT_RIC_PROF
+// tuning builds only: k_ric's phase times summed over its groups (wall clock, 10 ns), per instantiation kind
+// (0 Newton, 1 correction, 2 restoration) x [backward, F1, F2, F3 + multipliers, solves]; printed by run()
+__device__ unsigned long long g_ric_prof[3][5];
+#endif
 template <int DYN, bool RESTO, bool SOC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, RESTO, SOC>::value))) void k_ric(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                             const Ws* __restrict__ ws_, const int* __restrict__ active, int n_active,
@@ -1608,9 +1613,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     // Writes k_0 into the gains and p_0 into vf (the forward sweep's inputs), nu_[0] and dx0.
     auto backward_rhs = [&]() {
         const int li = l < NZ ? l : 0, lx = l < NX ? l : 0, lm = l < 2 ? l : 0, la = l < NC ? l : 0;
-        // one stage's inputs of this lane (row lx / column li / terminal column la), loaded a stage ahead
+        // one stage's inputs of this lane (row lx / column li / terminal column la; the stored Q_vv factor one element
+        // per lane, shuffled where the solve needs it), SD - 1 stages ahead: a stage is a few shuffles and ~40 fused
+        // multiply-adds, an HBM round trip several microseconds under the bulk's load
+        constexpr int SD = 3;
+        static_assert(QFL <= G, "one factor element per lane");
         struct In {
-            double cl, g, m0, m1, P[NX], ab[NX], gam[NX], qf[QFL], kt[NV], bu[NU];
+            double cl, g, m0, m1, P[NX], ab[NX], gam[NX], qfl, kt[NV], bu[NU];
         };
         auto load = [&](int k, In& d) {
             const double* slot = SL + (size_t)k * SLOT;
@@ -1625,19 +1634,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 d.ab[r] = slot[sAB + r * NAB + li];
                 d.gam[r] = vn[r * NCOL + NX + 2 + la];
             }
-            const double* f = &AT(qfac, k * QFL);
-#pragma unroll
-            for (int e = 0; e < QFL; ++e) d.qf[e] = f[e];
+            d.qfl = AT(qfac, k * QFL + (l < QFL ? l : 0));
 #pragma unroll
             for (int v = 0; v < NV; ++v) d.kt[v] = slot[sGN + lx * NV + v];
 #pragma unroll
             for (int v = 0; v < NU; ++v) d.bu[v] = slot[sAB + lx * NAB + NX + v];
         };
         double pn = 0.0, psi = 0.0;
-        In cur, nxt;
-        load(N, cur);
-        for (int k = N; k >= 0; --k) {
-            if (k > 0) load(k - 1, nxt);
+        // three buffers with static names (a rotated array of structs costs register copies), each refilled with the
+        // stage SD below the one it held as soon as that stage is done
+        In b0, b1, b2;
+        static_assert(SD == 3, "three stage buffers");
+        load(N, b0);
+        if (N >= 1) load(N - 1, b1);
+        if (N >= 2) load(N - 2, b2);
+        auto stage_k = [&](const int k, const In& cur) {
             const int nv = (k < N ? NU : 0) + ns;
             const bool kn = k < N;
             const double cl = kn && l < NX ? cur.cl : 0.0;
@@ -1668,8 +1679,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
 #pragma unroll
                 for (int a = 0; a < NV; ++a) {
 #pragma unroll
-                    for (int cc = 0; cc < NV; ++cc) L[a][cc] = cur.qf[a * NV + cc];
-                    perm[a] = (int)cur.qf[NV * NV + a];
+                    for (int cc = 0; cc < NV; ++cc) L[a][cc] = __shfl(cur.qfl, gb + a * NV + cc);
+                    perm[a] = (int)__shfl(cur.qfl, gb + NV * NV + a);
                 }
                 ldl_solve1<NV>(L, nv, perm, kv);
             }
@@ -1696,7 +1707,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 for (int r = 0; r < NX; ++r) psi += cur.gam[r] * e[r];
             }
             pn = pl;
-            cur = nxt;
+        };
+        for (int k = N; k >= 0;) {
+            stage_k(k, b0);
+            if (k - SD >= 0) load(k - SD, b0);
+            if (--k < 0) break;
+            stage_k(k, b1);
+            if (k - SD >= 0) load(k - SD, b1);
+            if (--k < 0) break;
+            stage_k(k, b2);
+            if (k - SD >= 0) load(k - SD, b2);
+            --k;
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) dx0[i] = -AT(rci, i);
@@ -1861,6 +1882,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     int n_att = 0;
     PROF_T(tr0);
 #endif
+#ifdef NLOT_RIC_PROF
+    const long long rp0 = wall_clock64();
+#endif
     if constexpr (SOC) backward_rhs();
     int n_tries = 0;
     bool deferred = false;
@@ -1925,6 +1949,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         return;
     }
 
+#ifdef NLOT_RIC_PROF
+    constexpr int rpk = SOC ? 1 : RESTO ? 2 : 0;
+    long long rpt = wall_clock64();
+    if (l == 0 && mode == MODE_NEWTON) {
+        atomicAdd(&g_ric_prof[rpk][0], (unsigned long long)(rpt - rp0));
+        atomicAdd(&g_ric_prof[rpk][4], 1ull);
+    }
+    auto rp_mark = [&](int i) {
+        const long long t = wall_clock64();
+        if (l == 0 && mode == MODE_NEWTON) atomicAdd(&g_ric_prof[rpk][i], (unsigned long long)(t - rpt));
+        rpt = t;
+    };
+#else
+    auto rp_mark = [](int) {};
+#endif
     // forward sweep.  (F1) closed-loop maps per knot, in parallel over knots: row i of stage k's phi block is
     // [Phi_i | off_0,i off_1,i] with Phi = A + B K, off_r = c + B (k_r + Kn nu_r); the slot's [A B 0 | c] stays, so a
     // second-order correction (same A, B, K: the same Phi) recomputes the offsets only, and k_iter_a rebuilds only c
@@ -1948,14 +1987,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         for (int v = 0; v < NU; ++v)
 #pragma unroll
             for (int c = 0; c < NX; ++c) Kt[v][c] = GN[c * NV + v];
-#pragma unroll 1
+        // every row of [A B | c] in registers before the first store (the stores into phi might alias the slot for
+        // the compiler: row by row, each row was a dependent HBM round trip; ~4-10 us each under the bulk's load)
+        double ab[NX][NX + NU + 1];
+#pragma unroll
         for (int i = 0; i < NX; ++i) {
             const double* r_ = slot + sAB + i * NAB;
-            double* pr = ph + i * PR;
-            double Bi[NU];
 #pragma unroll
-            for (int v = 0; v < NU; ++v) Bi[v] = r_[NX + v];
-            double o0 = r_[NZ], o1 = r_[NZ];
+            for (int c = 0; c < NX + NU; ++c) ab[i][c] = (SOC && c < NX) ? 0.0 : r_[c];
+            ab[i][NX + NU] = r_[NZ];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double* pr = ph + i * PR;
+            const double* Bi = &ab[i][NX];
+            double o0 = ab[i][NX + NU], o1 = ab[i][NX + NU];
 #pragma unroll
             for (int v = 0; v < NU; ++v) {
                 o0 += Bi[v] * dv[0][v];
@@ -1964,7 +2010,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
             if constexpr (!SOC) {
 #pragma unroll
                 for (int c = 0; c < NX; ++c) {
-                    double t = r_[c];
+                    double t = ab[i][c];
 #pragma unroll
                     for (int v = 0; v < NU; ++v) t += Bi[v] * Kt[v][c];
                     pr[c] = t;
@@ -2005,6 +2051,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         }
     }
     __syncthreads();
+    rp_mark(1);
     // (F2) the chain dx_{k+1} = Phi_k dx_k + off_k: lane i < NX of the group carries dx[i] of both
     //      right-hand sides; the other components arrive by group shuffles; rows prefetched a stage ahead
     double* dXo[2] = {&AT(dX, 0), &AT(dX2, 0)};
@@ -2075,20 +2122,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         }
     }
     __syncthreads();  // dX visible to every lane
+    rp_mark(2);
     // (F3) controls and slacks in parallel over knots: dv_k = k_r + K dx_k + Kn nu_r
+    // (both right-hand sides per knot: the gains and both dx_k loaded once, before the first store)
+    for (int k = l; k <= N; k += G) {
+        const double* GN = SL + (size_t)k * SLOT + sGN;
+        double gn[NCOL * NV], dxk[2][NX];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-        if (rr >= nr) break;
-        for (int k = l; k <= N; k += G) {
-            const double* GN = SL + (size_t)k * SLOT + sGN;
+        for (int e = 0; e < NCOL * NV; ++e) gn[e] = GN[e];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) dxk[rr][c] = rr < nr ? dXo[rr][k * NX + c] : 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            if (rr >= nr) break;
             double dv[NV];
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                double t = GN[(NX + rr) * NV + v];
+                double t = gn[(NX + rr) * NV + v];
 #pragma unroll
-                for (int c = 0; c < NX; ++c) t += GN[c * NV + v] * dXo[rr][k * NX + c];
+                for (int c = 0; c < NX; ++c) t += gn[c * NV + v] * dxk[rr][c];
 #pragma unroll
-                for (int cc = 0; cc < NC; ++cc) t += GN[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
+                for (int cc = 0; cc < NC; ++cc) t += gn[(NX + 2 + cc) * NV + v] * nu_[rr][cc];
                 dv[v] = t;
             }
             if (k < N)
@@ -2102,28 +2158,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     double* yio[2] = {&AT(yi_n, 0), &AT(yi2, 0)};
     double* yko[2] = {&AT(yk_n, 0), &AT(yk2, 0)};
     double* yto[2] = {&AT(yt_n, 0), &AT(yt2, 0)};
+    // (both right-hand sides per knot: the value function block, M and both dx loaded once, before the first store)
+    for (int k = l - 1; k < N; k += G) {
+        const double* v1 = &AT(vf, (k + 1) * VF);
+        double vb[NX * NCOL], xn[2][NX], d01[2][2], s0[4];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-        if (rr >= nr) break;
-        for (int k = l - 1; k < N; k += G) {
-            const double* v1 = &AT(vf, (k + 1) * VF);
-            double xn[NX];
+        for (int e = 0; e < NX * NCOL; ++e) vb[e] = v1[e];
 #pragma unroll
-            for (int c = 0; c < NX; ++c) xn[c] = dXo[rr][(k + 1) * NX + c];
+        for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+            for (int c = 0; c < NX; ++c) xn[rr][c] = rr < nr ? dXo[rr][(k + 1) * NX + c] : 0.0;
+            d01[rr][0] = (rr < nr && k >= 0) ? dXo[rr][k * NX] : 0.0;
+            d01[rr][1] = (rr < nr && k >= 0) ? dXo[rr][k * NX + 1] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s0[e] = k >= 0 ? SL[(size_t)k * SLOT + sM + e] : 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            if (rr >= nr) break;
             double mx0 = 0, mx1 = 0;
             if (k >= 0) {
-                const double* s0 = SL + (size_t)k * SLOT + sM;
-                const double d0 = dXo[rr][k * NX], d1 = dXo[rr][k * NX + 1];
+                const double d0 = d01[rr][0], d1 = d01[rr][1];
                 mx0 = s0[0] * d0 + s0[2] * d1;
                 mx1 = s0[1] * d0 + s0[3] * d1;
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double t = v1[i * NCOL + NX + rr];
+                double t = vb[i * NCOL + NX + rr];
 #pragma unroll
-                for (int c = 0; c < NX; ++c) t += v1[i * NCOL + c] * xn[c];
+                for (int c = 0; c < NX; ++c) t += vb[i * NCOL + c] * xn[rr][c];
 #pragma unroll
-                for (int cc = 0; cc < NC; ++cc) t += v1[i * NCOL + NX + 2 + cc] * nu_[rr][cc];
+                for (int cc = 0; cc < NC; ++cc) t += vb[i * NCOL + NX + 2 + cc] * nu_[rr][cc];
                 if (k < 0) {
                     yio[rr][i] = -t;
                 } else {
@@ -2132,6 +2197,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
                 }
             }
         }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        if (rr >= nr) break;
         if (l < nc) {
             double v = 0;
 #pragma unroll
@@ -2141,6 +2210,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         }
     }
     __syncthreads();
+    rp_mark(3);
 #ifdef NLOT_PHASE_PROF
     if (b == 0 && l == 0 && SC(SC_ITERS) < 8)
         printf("RICG it %d attempts %d build %lld backward %lld forward %lld total %lld (x10ns)\n", (int)SC(SC_ITERS),
@@ -5252,6 +5322,21 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         fold(step - 1);
     }
+#ifdef NLOT_RIC_PROF
+    {
+        unsigned long long hp[3][5];
+        NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        NLOT_HIP_CHECK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_ric_prof), sizeof(hp)));
+        const char* kinds[3] = {"newton", "correction", "restoration"};
+        for (int k = 0; k < 3; ++k)
+            if (hp[k][4])
+                fprintf(stderr, "[ric_prof] %s solves %llu: us per solve backward %.2f F1 %.2f F2 %.2f F3+mult %.2f\n",
+                        kinds[k], hp[k][4], hp[k][0] * 1e-2 / hp[k][4], hp[k][1] * 1e-2 / hp[k][4],
+                        hp[k][2] * 1e-2 / hp[k][4], hp[k][3] * 1e-2 / hp[k][4]);
+        const unsigned long long z[3][5] = {};
+        NLOT_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_ric_prof), z, sizeof(z)));
+    }
+#endif
     if (n_active > 0 || next_admit < Bi) {
         set_error("nlot_solve_batch: the global step cap was reached with instances unfinished (phase-machine bug)");
         return NLOT_ERR_INVALID;
