@@ -390,6 +390,27 @@ __device__ __forceinline__ void chunked_update(int n, int lane, Ld&& ld, St&& st
     }
 }
 
+// A lane-strided pass whose first chunk is loaded ahead (load), then consumed exactly as chunked_update would
+// (run: the same elements in the same order, later chunks loaded as they come): several reductions' loads issued
+// together cost one memory round trip instead of one each, with the arithmetic unchanged
+template <int CH, int NV>
+struct Pre {
+    double v[CH][NV];
+    template <class Ld>
+    __device__ __forceinline__ void load(int n, int lane, Ld&& ld) {
+#pragma unroll
+        for (int r = 0; r < CH; ++r)
+            if (lane + 64 * r < n) ld(lane + 64 * r, v[r]);
+    }
+    template <class Ld, class St>
+    __device__ __forceinline__ void run(int n, int lane, Ld&& ld, St&& st) {
+#pragma unroll
+        for (int r = 0; r < CH; ++r)
+            if (lane + 64 * r < n) st(lane + 64 * r, v[r]);
+        if (n > 64 * CH) chunked_update<4, NV>(n, lane + 64 * CH, ld, st);
+    }
+};
+
 // ---- wave-level helpers (64 lanes; results broadcast from lane 0 so every lane branches alike) ----
 __device__ inline double wsum(double v) {
 #pragma unroll
@@ -2571,6 +2592,24 @@ __device__ int ls_failed(const NlotSolverOptions& o, const NlotProblem& p, const
 // INIT (their first step); SOC = the second-order corrections' stages only (side stream, at the start of the step: they
 // need no MLP evaluation); EVAL = everything but the corrections; ALL = both.  (INIT instances first take their
 // least-squares multipliers from k_ric's solve).
+#ifdef NLOT_KPROF
+// tuning builds only: phase times of the per-instance kernels summed over their waves (wall clock, 10 ns), [kernel]
+// [phase]; slot 15 counts the waves that reached the last mark; printed by run()
+__device__ unsigned long long g_kprof[4][16];
+#define KPROF_INIT long long kp_t = wall_clock64()
+#define KPROF(kid, ph)                                                                              \
+    do {                                                                                             \
+        const long long kp_n = wall_clock64();                                                       \
+        if (threadIdx.x == 0) atomicAdd(&g_kprof[kid][ph], (unsigned long long)(kp_n - kp_t));     \
+        kp_t = kp_n;                                                                                 \
+    } while (0)
+#define KPROF_COUNT(kid) \
+    if (threadIdx.x == 0) atomicAdd(&g_kprof[kid][15], 1ull)
+#else
+#define KPROF_INIT
+#define KPROF(kid, ph)
+#define KPROF_COUNT(kid)
+#endif
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))) void k_iter_a(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, const double* __restrict__ x0,
@@ -2609,6 +2648,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
         return;
     }
+    KPROF_INIT;
     const int N = dm.N, M = dm.M, nc = dm.nc;
     const int rank = (int)SC(SC_RANK);
     const double k1 = o.bound_push;
@@ -2692,7 +2732,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         wsync();
         if (lane == 0) SC(SC_RIC) = 0;
     }
+    KPROF(0, 0);  // entry, INIT work
     eval_knots(true);
+    KPROF(0, 1);  // SDF chain rule at the corners
     // residuals c(x) (IPOPT sign)
     for (int i = lane; i < NX; i += 64) AT(rci, i) = AT(X, i) - x0b[i];
     for (int i = lane; i < nc; i += 64) AT(rct, i) = AT(X, N * NX + dm.tidx[i]) - xgb[dm.tidx[i]];
@@ -2712,7 +2754,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         AT(rcb, q) = (q < N * NU ? AT(U, q) : AT(S, q - N * NU)) - AT(sb, q);
     wsync();
 
-    // the lane-strided sums below run through chunked_update (loads of 4 rows first, then the same per-lane order)
+    // the lane-strided sums below: every pass's first chunk loaded ahead (Pre), consumed in the same per-lane order
     auto theta_phi = [&](double mu, double* th, double* phv, double* fout = nullptr) {
         double t = 0, bar = 0, lin = 0;
         auto tsum = [&](int, const double* v) { t += fabs(v[0]); };
@@ -2752,10 +2794,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         }
     }
 
+    KPROF(0, 2);  // residuals (and theta / phi at INIT)
     // ---- optimality measures (IPOPT scaled E_0 / E_mu) ----
     double dual = 0, primal = 0, c0 = 0, cmu = 0, cviol = 0, ysum = 0, zsum = 0, nzc = 0;
     double dsq = 0, psq = 0, csum = 0;  // quality-function oracle: ||grad L||^2, ||c, d - t||^2, sum z s
     double d1 = 0, p1 = 0;              // soft restoration: 1-norms of the dual and primal residuals
+    // The passes below only read: their first chunks are all loaded here, ahead of the dual residuals' knot loop, and
+    // consumed in the original order (Pre) — one memory round trip instead of one per pass (13 passes)
+    const int nnu = N * NU;
+    auto ld_bs = [&](int q, double* v) {  // bound-row slacks: y, z_L (z_S), z_U
+        v[0] = AT(yb, q);
+        v[1] = q < nnu ? AT(zl, q) : AT(zs, q - nnu);
+        v[2] = q < nnu ? AT(zu, q) : 0.0;
+    };
+    auto ld_rci = [&](int i, double* v) { v[0] = AT(rci, i); };
+    auto ld_rct = [&](int i, double* v) { v[0] = AT(rct, i); };
+    auto ld_rcd = [&](int i, double* v) { v[0] = AT(rcd, i); };
+    auto ld_rcq = [&](int q, double* v) { v[0] = AT(rcq, q); v[1] = AT(dv, q); };
+    auto ld_rcb = [&](int q, double* v) { v[0] = AT(rcb, q); v[1] = q < nnu ? AT(U, q) : AT(S, q - nnu); };
+    auto ld_cu = [&](int e, double* v) { v[0] = BVU(e); v[1] = AT(zl, e); v[2] = AT(zu, e); };
+    auto ld_zs = [&](int k, double* v) { v[0] = AT(zs, k); v[1] = BVS(k); };
+    auto ld_vt = [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); };
+    auto ld_yi = [&](int i, double* v) { v[0] = AT(yi, i); };
+    auto ld_yk = [&](int i, double* v) { v[0] = AT(yk, i); };
+    auto ld_yt = [&](int i, double* v) { v[0] = AT(yt, i); };
+    auto ld_yd = [&](int q, double* v) { v[0] = AT(yd, q); };
+    auto ld_yb = [&](int q, double* v) { v[0] = AT(yb, q); };
+    Pre<3, 3> p_bs;
+    Pre<1, 1> p_rci, p_rct, p_yi, p_yt, p_yd;
+    Pre<4, 1> p_rcd, p_yk;
+    Pre<1, 2> p_rcq, p_zs, p_vt;
+    Pre<3, 2> p_rcb;
+    Pre<2, 3> p_cu;
+    Pre<3, 1> p_yb;
+    p_bs.load(ngb, lane, ld_bs);
+    p_rci.load(NX, lane, ld_rci);
+    p_rct.load(nc, lane, ld_rct);
+    p_rcd.load(N * NX, lane, ld_rcd);
+    p_rcq.load((N + 1) * M, lane, ld_rcq);
+    p_rcb.load(ngb, lane, ld_rcb);
+    p_cu.load(N * NU, lane, ld_cu);
+    if (dm.ns) p_zs.load(N + 1, lane, ld_zs);
+    p_vt.load((N + 1) * M, lane, ld_vt);
+    p_yi.load(NX, lane, ld_yi);
+    p_yk.load(N * NX, lane, ld_yk);
+    p_yt.load(nc, lane, ld_yt);
+    p_yd.load((N + 1) * M, lane, ld_yd);
+    p_yb.load(ngb, lane, ld_yb);
     for (int k = lane; k <= N; k += 64) {
         double r[NX];
 #pragma unroll
@@ -2830,36 +2915,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
             d1 += fabs(t);
         }
     }
-    for (int q = lane; q < ngb; q += 64) {  // bound-row slacks: -y - z_L + z_U
-        const double t = q < N * NU ? -AT(yb, q) - AT(zl, q) + AT(zu, q) : -AT(yb, q) - AT(zs, q - N * NU);
+    p_bs.run(ngb, lane, ld_bs, [&](int q, const double* v) {  // bound-row slacks: -y - z_L + z_U
+        const double t = q < nnu ? -v[0] - v[1] + v[2] : -v[0] - v[1];
         dual = fmax(dual, fabs(t));
         dsq += t * t;
         d1 += fabs(t);
-    }
+    });
     auto pri_ = [&](double v) {
         primal = fmax(primal, fabs(v));
         psq += v * v;
         p1 += fabs(v);
     };
     auto pri1 = [&](int, const double* v) { pri_(v[0]); };
-    chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(rci, i); }, pri1);
-    chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(rct, i); }, pri1);
-    chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(rcd, i); }, pri1);
+    p_rci.run(NX, lane, ld_rci, pri1);
+    p_rct.run(nc, lane, ld_rct, pri1);
+    p_rcd.run(N * NX, lane, ld_rcd, pri1);
     cviol = wmax(primal);
-    chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(rcq, q); v[1] = AT(dv, q); },
-                         [&](int, const double* v) {
-                             pri_(v[0]);
-                             cviol = fmax(cviol, fmax(0.0, -v[1]));
-                         });
-    for (int q = lane; q < ngb; q += 64) {  // bound rows: d(x) = U or S against its bounds
-        pri_(AT(rcb, q));
-        if (q < N * NU) {
-            const double u = AT(U, q);
+    p_rcq.run((N + 1) * M, lane, ld_rcq, [&](int, const double* v) {
+        pri_(v[0]);
+        cviol = fmax(cviol, fmax(0.0, -v[1]));
+    });
+    p_rcb.run(ngb, lane, ld_rcb, [&](int q, const double* v) {  // bound rows: d(x) = U or S against its bounds
+        pri_(v[0]);
+        if (q < nnu) {
+            const double u = v[1];
             cviol = fmax(cviol, fmax(0.0, fmax(p.umin[q % NU] - u, u - p.umax[q % NU])));
         } else {
-            cviol = fmax(cviol, fmax(0.0, -AT(S, q - N * NU)));
+            cviol = fmax(cviol, fmax(0.0, -v[1]));
         }
-    }
+    });
     auto compl_ = [&](double z, double s) {
         c0 = fmax(c0, fabs(z * s));
         cmu = fmax(cmu, fabs(z * s - mu0));
@@ -2867,20 +2951,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         zsum += fabs(z);
         nzc += 1;
     };
-    chunked_update<4, 3>(N * NU, lane, [&](int e, double* v) { v[0] = BVU(e); v[1] = AT(zl, e); v[2] = AT(zu, e); },
-                         [&](int e, const double* v) {
-                             compl_(v[1], v[0] - p.umin[e % NU]);
-                             compl_(v[2], p.umax[e % NU] - v[0]);
-                         });
+    p_cu.run(N * NU, lane, ld_cu, [&](int e, const double* v) {
+        compl_(v[1], v[0] - p.umin[e % NU]);
+        compl_(v[2], p.umax[e % NU] - v[0]);
+    });
     auto compl2 = [&](int, const double* v) { compl_(v[0], v[1]); };
-    if (dm.ns) chunked_update<4, 2>(N + 1, lane, [&](int k, double* v) { v[0] = AT(zs, k); v[1] = BVS(k); }, compl2);
-    chunked_update<4, 2>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(vt, q); v[1] = AT(T, q); }, compl2);
+    if (dm.ns) p_zs.run(N + 1, lane, ld_zs, compl2);
+    p_vt.run((N + 1) * M, lane, ld_vt, compl2);
     auto ysum1 = [&](int, const double* v) { ysum += fabs(v[0]); };
-    chunked_update<4, 1>(NX, lane, [&](int i, double* v) { v[0] = AT(yi, i); }, ysum1);
-    chunked_update<4, 1>(N * NX, lane, [&](int i, double* v) { v[0] = AT(yk, i); }, ysum1);
-    chunked_update<4, 1>(nc, lane, [&](int i, double* v) { v[0] = AT(yt, i); }, ysum1);
-    chunked_update<4, 1>((N + 1) * M, lane, [&](int q, double* v) { v[0] = AT(yd, q); }, ysum1);
-    chunked_update<4, 1>(ngb, lane, [&](int q, double* v) { v[0] = AT(yb, q); }, ysum1);
+    p_yi.run(NX, lane, ld_yi, ysum1);
+    p_yk.run(N * NX, lane, ld_yk, ysum1);
+    p_yt.run(nc, lane, ld_yt, ysum1);
+    p_yd.run((N + 1) * M, lane, ld_yd, ysum1);
+    p_yb.run(ngb, lane, ld_yb, ysum1);
     dual = wmax(dual);
     primal = wmax(primal);
     cviol = wmax(cviol);
@@ -2897,6 +2980,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
     const double E0 = fmax(fmax(dual / sd, primal), c0 / scc);
     // IPOPT's primal-dual system error at barrier parameter m (soft restoration): sum of the 1-norms of the dual,
     // primal and complementarity residuals over the element count
+    KPROF(0, 3);  // optimality measures
     const double n_pd = (double)((N + 1) * NX + N * NU + dm.ns * (N + 1) + (N + 1) * M + ngb) +
                         (double)(NX + nc + N * NX + (N + 1) * M + ngb) + nzc;
     auto pd_error = [&](double m) {
@@ -3053,9 +3137,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
         SC(SC_MUPD) = mu_pd;
     }
     wsync();
+    KPROF(0, 4);  // convergence test, mu update (theta / phi, progress filter), primal-dual error
     // ---- Newton system (free mode: affine mu = 0 and centering mu = avg right-hand sides): stage
     //      matrices here, factorisation + inertia correction in k_ric, the rest in k_iter_b ----
     SV::template build_stages<false>(p, dm, ws, b, lane, MODE_NEWTON, 0.0, use_qf ? 0.0 : mu, avg, use_qf ? 2 : 1, SL);
+    KPROF(0, 5);  // stage matrices
+    KPROF_COUNT(0);
     if (lane == 0) {
         SC(SC_E0) = E0;
         SC(SC_RMU0) = use_qf ? 0.0 : mu;
@@ -3115,6 +3202,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         return;
     }
     if (ric != 2) return;
+    KPROF_INIT;
     const bool soc = (int)SC(SC_PHASE) == PH_SOC;
     const int N = dm.N, M = dm.M;
     const double dw = SC(SC_DW), avg = SC(SC_AVG), dsq_w = SC(SC_DSQ), psq_w = SC(SC_PSQ), nzc = SC(SC_NZC);
@@ -3417,6 +3505,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         wsync();
         }
     }
+    KPROF(1, 0);  // quality-function mu oracle (free mode) / sigma choice
     // ---- recover dt, yd+, dz; fraction to the boundary; line-search reference values ----
     const double kappa_d = 1e-5;
     double amax = 1.0, az = 1.0, gd = 0;
@@ -3503,6 +3592,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     az = wmin(az);
     gd = wsum(gd);
     wsync();
+    KPROF(1, 1);  // step recovery, fraction to the boundary, gradient term
     if (soc) {  // second-order corrected direction: its fraction-to-boundary step is the one trial point
         if (lane == 0) {
             SC(SC_RIC) = 0;
@@ -3606,8 +3696,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         }
         return;
     }
+    KPROF(1, 2);  // theta / phi, tiny step, watchdog, soft restoration
     // the first line-search round: alpha_max alone (none for a tiny step)
     emit_points(p, dm, ws, b, lane, cnt, true, tp, tiny ? 0 : 1, amax);
+    KPROF(1, 3);  // trial corners
+    KPROF_COUNT(1);
 }
 
 // An instance leaves the active list (k_accept): its outputs (X, U, S, cost = the objective at X, status, iterations;
@@ -3859,6 +3952,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             wsync();
             emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
         } else {
+        KPROF_INIT;
         const double theta = SC(SC_THETA), phi = SC(SC_PHI), gd = SC(SC_GD);
         double rth = theta, rph = phi, rgd = gd, at_fix = -1.0;
         if (in_wd) {  // watchdog: the watchdog point's reference values and its alpha_max as the test step
@@ -3883,6 +3977,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             }
         }
         if (lane == 0) SC(SC_LASTREJF) = lastrej;
+        KPROF(2, 0);  // trial points: theta / phi, acceptance tests
         int next_round = 0;  // 1: emit the next backtracking round from SC_ALPHA; 2: PH_SOC
         bool tentative = false;
         wsync();
@@ -3966,6 +4061,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             }
         }
         wsync();
+        KPROF(2, 1);  // rejection: second-order correction's residuals, watchdog, next round
         if (ok) {
             // filter augmentation with the current point's values unless an f-type step met Armijo (or the
             // step is tiny: IPOPT takes it without the filter)
@@ -3998,7 +4094,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             }
             // corners of the new iterate, for the next step's full launch
             wsync();  // X complete
+            KPROF(2, 2);  // accepted: filter, the new iterate
             if (!stop_tiny) emit_points(p, dm, ws, b, lane, cnt_next, false, nullptr, 1, 0.0);
+            KPROF(2, 3);  // corners of the new iterate
         } else if (next_round == 2) {
             ph = PH_SOC;
             if (lane == 0) SC(SC_PHASE) = PH_SOC;
@@ -4009,7 +4107,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
             } else {
                 emit_points(p, dm, ws, b, lane, cnt_next, true, tp_next, n_later(na, SC(SC_AMIN), nspec_next), na);
             }
+            KPROF(2, 4);  // rejected: next round's corners
         }
+        KPROF_COUNT(2);
         }  // PH_LS
     }
     wsync();
@@ -5322,6 +5422,23 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         fold(step - 1);
     }
+#ifdef NLOT_KPROF
+    {
+        unsigned long long kp[4][16];
+        NLOT_HIP_CHECK(hipStreamSynchronize(st));
+        NLOT_HIP_CHECK(hipMemcpyFromSymbol(kp, HIP_SYMBOL(g_kprof), sizeof(kp)));
+        const char* kn[4] = {"k_iter_a", "k_iter_b", "k_accept", "k_resto"};
+        for (int k = 0; k < 4; ++k)
+            if (kp[k][15]) {
+                fprintf(stderr, "[kprof] %s waves %llu: us per wave", kn[k], kp[k][15]);
+                for (int i = 0; i < 15; ++i)
+                    if (kp[k][i]) fprintf(stderr, " [%d] %.2f", i, kp[k][i] * 1e-2 / kp[k][15]);
+                fprintf(stderr, "\n");
+            }
+        const unsigned long long z[4][16] = {};
+        NLOT_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_kprof), z, sizeof(z)));
+    }
+#endif
 #ifdef NLOT_RIC_PROF
     {
         unsigned long long hp[3][5];

@@ -14,9 +14,8 @@ import collections
 import csv
 import json
 
-CLASSES = (  # (class, substring of the kernel name); first match wins
-    ("ric_soc", "k_ric<3, false, true>"), ("ric_resto", "k_ric<3, true, false>"), ("ric", "k_ric<3, false, false>"),
-    ("ric_soc", ", false, true>"), ("ric_resto", ", true, false>"), ("ric", "k_ric<"),
+CLASSES = (  # (class, substrings of the kernel name: all must occur); first match wins
+    ("ric_soc", "k_ric<", ", false, true>"), ("ric_resto", "k_ric<", ", true, false>"), ("ric", "k_ric<"),
     ("iter_a", "k_iter_a"), ("iter_b", "k_iter_b"), ("accept", "k_accept"), ("resto_a", "k_resto_a"),
     ("resto_b", "k_resto_b"), ("resto_ls", "k_resto_ls"), ("points", "k_points"),
     ("mlp_full", "mlp_bf16<128, true"), ("mlp_value", "mlp_bf16<128, false"), ("mlp_full", "mlp_kernel<128, 1, true>"),
@@ -24,8 +23,8 @@ CLASSES = (  # (class, substring of the kernel name); first match wins
 
 
 def cls(name):
-    for c, s in CLASSES:
-        if s in name:
+    for c, *subs in CLASSES:
+        if all(s in name for s in subs):
             return c
     return None
 
@@ -52,6 +51,7 @@ def main():
             steps[i][r[2]].append(r)
     bulk = [i for i in range(1, len(acc)) if acc[i][3] >= a.min_active]
     dur = collections.defaultdict(list)
+    offs = collections.defaultdict(list)  # (start, end) of each launch relative to the step's start
     waits = collections.defaultdict(list)
     walls = []
     for i in bulk:
@@ -59,6 +59,8 @@ def main():
         walls.append(ends[i] - ends[i - 1])
         for c, lst in s.items():
             dur[c].append(sum(e - b for b, e, *_ in lst))
+            for j, (b, e, *_) in enumerate(sorted(lst)):
+                offs[f"{c}#{j}"].append((b - ends[i - 1], e - ends[i - 1]))
         if s.get("iter_b") and s.get("ric"):
             ib = s["iter_b"][0][0]
             ric_end = max(e for b, e, *_ in s["ric"])
@@ -79,6 +81,9 @@ def main():
     res = {"trace": a.trace, "bulk_steps": len(bulk), "min_active": a.min_active,
            "wall_us_per_step": mean(walls),
            "kernel_us_per_step": {c: mean(v) for c, v in sorted(dur.items())},
+           "launch_start_end_us_from_step_start": {
+               c: [mean([a for a, _ in v]), mean([b for _, b in v]), len(v)]
+               for c, v in sorted(offs.items(), key=lambda kv: sum(a for a, _ in kv[1]) / len(kv[1]))},
            "waits_us": {k: mean(v) for k, v in waits.items()}}
     print(json.dumps(res, indent=1))
     if a.out:

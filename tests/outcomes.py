@@ -103,18 +103,37 @@ def reproducible(out):
     return same & np.where(st[0] == 0, rel <= COST_REPRO, stopped)
 
 
-def rounding_excused(out, sg_f32, cg_f32, sg, cg):
-    """Oracle-reproducible instances on which the product's split-bf16 net misses the oracle's outcome while the f32
-    net (NLOT_MLP_ARITH_F32: the oracle's fp32 products, the sums in another order) hits it: the miss is the net's
-    rounding, a perturbation a few times the reverse-order net's (tests/test_pinned_iterates_gpu.py), not the solver.
-    Callers cap their number (at most 5 %, at least one)."""
+def rounding_excused(out, sg_other, cg_other, sg, cg):
+    """Oracle-reproducible instances on which one GPU net misses the oracle's outcome while the other hits it.  The
+    two nets (include/nlot.h NLOT_MLP_ARITH_*: split-bf16 and f32 MFMA) are both fp32 arithmetic whose sums round in
+    other orders than the oracle's fp32 net: a perturbation of the size of the reverse-order net's
+    (tests/test_pinned_iterates_gpu.py), which the fixture's five perturbed runs sample only five times.  A miss the
+    other net does not share is the net's rounding, not the solver.  Callers cap their number (5 %, at least one)."""
     so, co = out["status"][0], out["cost"][0]
 
     def miss(s, c):
         rel = np.abs(np.asarray(c, float) - co) / np.maximum(np.abs(co), 1e-300)
         return (np.asarray(s) != so) | ((so == 0) & (rel > 1e-4))
 
-    return reproducible(out) & miss(sg, cg) & ~miss(sg_f32, cg_f32)
+    return reproducible(out) & miss(sg, cg) & ~miss(sg_other, cg_other)
+
+
+def dual_net_parity(label, out, res, min_reproducible=0, widen=None):
+    """check_outcome_parity for the GPU run with each net (res = {"f32": (status, cost), "split_bf16": (...)}): a
+    reproducible instance one net misses and the other hits is excused for the net that misses it (at most 5 % of the
+    instances, at least one, per net); one that both miss fails (unless the oracle reaches the GPU's outcome from a
+    WIDE start)."""
+    n = len(out["status"][0])
+    cap = max(1, int(0.05 * n))
+    info = {}
+    for net, other in (("f32", "split_bf16"), ("split_bf16", "f32")):
+        ex = rounding_excused(out, *res[other], *res[net])
+        print(f"[parity] {label} {net} net: excused (the other net hits them) {np.nonzero(ex)[0].tolist()}", flush=True)
+        assert ex.sum() <= cap, (label, net, np.nonzero(ex)[0].tolist())
+        info[net] = check_outcome_parity(f"{label} {net} net", *res[net], out,
+                                         min_reproducible=max(0, min_reproducible - int(ex.sum())), widen=widen,
+                                         excused=ex)
+    return info
 
 
 def check_outcome_parity(label, sg, cg, out, min_reproducible=0, widen=None, excused=None):

@@ -53,16 +53,16 @@ def test_b6_batch_matches_oracle():
     oracle run that solves fewest, less one, and at least one; jointly solved instances end within 10 % of the
     oracle's cost — the chaotic group's status agreement alone would pass a GPU that solves nothing here, where the
     oracle's statuses are mostly failures); and every instance the GPU reports solved satisfies its constraints
-    (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack).  Run with the f32 net (every
-    reproducible instance) and with the product's split-bf16 net (every one but one that the f32 net hits and the
-    split-bf16 net's rounding moves: outcomes.rounding_excused).  A reproducible instance the GPU misses is run from
+    (dynamics, start / terminal states, per-corner learned SDF >= 0 without slack).  Run with the f32 net and
+    with the product's split-bf16 net (outcomes.dual_net_parity: a reproducible instance one net misses and the other
+    hits is excused for the first, at most one; none may be missed by both).  A reproducible instance the GPU misses is run from
     twelve more oracle starts (outcomes.WIDE, x0 +- 1e-11 .. 1e-7): fixture instance 18, whose oracle paths part at
     iteration 37 and meet again at the restoration failure of iteration 404 under the fixture's six runs, ends in
     max_iter from x0 + 1e-7 e_y, as it does on the GPU's split-bf16 net."""
     import os
 
     O, prob, b, _, hm = _setup()
-    from outcomes import WIDE, check_outcome_parity, oracle_outcomes, rounding_excused
+    from outcomes import WIDE, dual_net_parity, oracle_outcomes
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.ops import DeviceMlp
@@ -80,11 +80,7 @@ def test_b6_batch_matches_oracle():
         res[arith] = (r["status"].cpu().numpy(), r["cost"].cpu().numpy())
         print("b6 batch statuses", arith, "gpu", res[arith][0].tolist(), flush=True)
     print("b6 batch statuses oracle", out["status"].tolist(), flush=True)
-    check_outcome_parity("b6 (24, RRT init) f32 net", *res["f32"], out, min_reproducible=1, widen=widen)
-    ex = rounding_excused(out, *res["f32"], *res["split_bf16"])
-    print("b6 split-bf16 net: excused", np.nonzero(ex)[0].tolist(), flush=True)
-    assert ex.sum() <= 1
-    check_outcome_parity("b6 (24, RRT init) split-bf16 net", *res["split_bf16"], out, widen=widen, excused=ex)
+    dual_net_parity("b6 (24, RRT init)", out, res, min_reproducible=1, widen=widen)
     st, cost = res["split_bf16"]
     floor = max(1, int(min((out["status"][k] == 0).sum() for k in range(out["status"].shape[0]))) - 1)
     both = (st == 0) & (out["status"][0] == 0)
