@@ -319,7 +319,8 @@ def main():
     # PMC at bench size (B = 65536): scripts/pmc_traffic.sh + scripts/pmc_traffic.py -> profiles/r05/ (the newest
     # round's file that exists)
     tf = next((t for t in (os.path.join(ROOT, "profiles", r, f) for r, f in
-                           (("r05", "pmc_traffic_r05_B65536.json"), ("r04", "pmc_traffic_r04_B65536.json"),
+                           (("r05", "pmc_traffic_r05u_B65536.json"), ("r05", "pmc_traffic_r05_B65536.json"),
+                            ("r04", "pmc_traffic_r04_B65536.json"),
                             ("r03", "pmc_traffic_r03m_B65536.json"))) if os.path.exists(t)), "")
     pmc = None
     if os.path.exists(tf):
@@ -444,7 +445,8 @@ def main():
                                         "step's candidates (fourth stream); its event-timed duration includes that")
         # per-dispatch fractions from the profiler (the event brackets above include the streams' overlap): committed
         # from a rocprofv3 --kernel-trace --stats run of this command (scripts/rocprof_fracs.py)
-        df = os.path.join(ROOT, "profiles", "r05", "mlp_dispatch_fracs_r05c.json")
+        df = next((d for d in (os.path.join(ROOT, "profiles", "r05", f"mlp_dispatch_fracs_{t}.json")
+                               for t in ("r05u", "r05c")) if os.path.exists(d)), "")
         if os.path.exists(df) and not (stress or b6):
             with open(df) as fh:
                 dd = json.load(fh)

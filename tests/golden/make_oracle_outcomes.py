@@ -3,6 +3,7 @@
 
     python tests/golden/make_oracle_outcomes.py [--threads 8] [--form rows|varbounds] [--only metric|b6]
     python tests/golden/make_oracle_outcomes.py --form rows|varbounds --add-stpin   (adds {case}_stpin to a file)
+    python tests/golden/make_oracle_outcomes.py --form rows|varbounds --add-wide    (adds b6_wide_* to a file)
         rows (default):  tests/golden/oracle_outcomes.npz            (the reference's constraint-row bounds)
         varbounds:       tests/golden/oracle_outcomes_varbounds.npz  (the same bounds as variable bounds)
 
@@ -30,6 +31,11 @@ restoration phase that converged to a point the filter rejects; a restoration li
 happens inside iteration k_i and so returns max_iter).  A GPU test runs every instance to k_i — failed and chaotic
 instances included — and compares the iterate and the status.  {case}_trials: the run's trial-point evaluations (IPOPT's
 sequential backtracking: one SDF value evaluation of the trial's corners each; DESIGN.md §8f cost model).
+
+b6_wide_status / b6_wide_cost / b6_wide_iters [12, 24]: the b6 instances under tests/outcomes.WIDE (x0 +- 1e-11,
+1e-9, 1e-7 e_x, e_y): the oracle's own outcome spread at the size of the GPU's rounding differences (its fp32 net
+sums in other orders, its fp64 reductions and Riccati sweeps in other orders in every iteration), against which the
+GPU's chaotic b6 outcomes are measured (tests/outcomes.py).
 
 The oracle is deterministic (one instance per thread, no reductions across threads), so the GPU box's oracle
 build reproduces these numbers bitwise; tests/test_oracle_outcomes_fixture.py re-runs a few instances on the CPU
@@ -159,6 +165,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
     ap.add_argument("--add-stpin", action="store_true", help="add {case}_stpin to an existing file")
+    ap.add_argument("--add-wide", action="store_true", help="add b6_wide_* (outcomes under WIDE) to an existing file")
     a = ap.parse_args()
     out_path = a.out or OUT[a.form]
     import oracle as O
@@ -170,6 +177,32 @@ def main():
     data = dict(np.load(out_path)) if (a.only and os.path.exists(out_path)) else {}
     data["general_bounds"] = np.array(opt.general_bounds)
 
+    if a.add_wide:
+        from outcomes import WIDE
+
+        data = dict(np.load(out_path))
+        opt = _abi.default_options(general_bounds=int(data["general_bounds"]))
+        hm6 = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")))
+        X0, XG, Xi = data["b6_x0"], data["b6_xg"], data["b6_xinit"]
+        n, m = len(X0), len(WIDE)
+        t = time.time()
+
+        def one(args):
+            i, (c, d, _) = args
+            x = X0[i].copy()
+            x[c] += d
+            r = O.solve_one(B6_PROBLEM, x, XG[i], hm6, opt=opt, X_init=Xi[i])
+            return r["status"], r["cost"], r["iters"]
+
+        with ThreadPoolExecutor(a.threads) as ex:
+            rs = list(ex.map(one, [(i, pd) for pd in WIDE for i in range(n)]))
+        data["b6_wide_status"] = np.array([r[0] for r in rs], np.int32).reshape(m, n)
+        data["b6_wide_cost"] = np.array([r[1] for r in rs]).reshape(m, n)
+        data["b6_wide_iters"] = np.array([r[2] for r in rs], np.int32).reshape(m, n)
+        print(f"b6 wide: {time.time() - t:.0f} s, statuses "
+              f"{np.bincount(data['b6_wide_status'].ravel(), minlength=7).tolist()}", flush=True)
+        np.savez_compressed(out_path, **data)
+        return
     if a.add_stpin:
         data = dict(np.load(out_path))
         opt = _abi.default_options(general_bounds=int(data["general_bounds"]))

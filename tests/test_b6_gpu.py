@@ -71,6 +71,8 @@ def test_b6_batch_matches_oracle():
     f = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_outcomes.npz")))
     X0, XG, Xi = f["b6_x0"], f["b6_xg"], f["b6_xinit"]
     out = {k: f[f"b6_{k}"] for k in ("status", "cost", "iters", "xdev")}
+    if "b6_wide_status" in f:  # the oracle's outcomes under the WIDE starts (tests/golden/make_oracle_outcomes.py)
+        out.update(wide_status=f["b6_wide_status"], wide_cost=f["b6_wide_cost"])
     opt = _abi.default_options()
     widen = lambda i: oracle_outcomes(O, prob, X0[i], XG[i], hm, opt=opt, X_init=Xi[i], perturbations=WIDE)
     w = MlpWeights.load(os.path.join(DATA, "b6_mlp128_seed0.npz"))

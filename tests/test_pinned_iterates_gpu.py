@@ -16,8 +16,12 @@ of the reverse-order net's size that the fixture's five runs sample only five ti
 agree, often one iteration before a decision (filter, mu, restoration entry) flips, so a sixth perturbation can flip
 it at k_i already (scripts/pin_probe.py: b6 instance 3 at iteration 6 under the split-bf16 net, 6.7e-6 against the
 oracle's 3.5e-6 spread and 7e-2 one iteration later, while the f32 net tracks the oracle to 1.6e-6 through k_i = 20;
-metric instance 63 the other way round).  Per net every instance but 5 % (at least one), and no instance may miss
-under both nets: a miss one net does not share is that net's rounding, not the solver."""
+metric instance 63 the other way round).  The GPU also rounds its fp64 sums (Riccati sweeps, reductions) in other
+orders in every iteration, where the fixture's runs differ only at the start.  So an instance outside 1e-4 is run on
+the oracle from the twelve WIDE starts (x0 +- 1e-11 .. 1e-7, tests/outcomes.py) up to k_i: if one of them leaves the
+pinned iterate by more than 1e-4 there too, k_i was optimistic for the GPU's perturbation size and the instance is
+excused.  Per net every remaining instance but 5 % (at least one), and none may miss under both nets: a miss one net
+does not share is that net's rounding, not the solver."""
 import os
 
 import numpy as np
@@ -63,6 +67,45 @@ def _pinned_run(f, case, artefact, arith):
     return dev, sg
 
 
+def _wide_excused(f, case, form, idx, artefact):
+    """Instances among idx whose oracle run from one of the WIDE starts is more than TOL from the pinned iterate at
+    k_i (the oracle itself is not pinned there at the GPU's perturbation size)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import oracle as O
+    from outcomes import WIDE
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
+
+    if case == "metric":
+        prob, hm = METRIC_PROBLEM, O.HostMlp(artefact)
+    else:
+        prob = B6_PROBLEM
+        hm = O.HostMlp(MlpWeights.load(os.path.join(os.path.dirname(HERE), "nlotrajectories_amd", "data",
+                                                    "b6_mlp128_seed0.npz")))
+    N, nx = prob.N, prob.nx
+    xi = f.get(f"{case}_xinit")
+
+    def one(args):
+        i, (c, d, _) = args
+        x = f[f"{case}_x0"][i].copy()
+        x[c] += d
+        k = int(f[f"{case}_kpin"][i])
+        o = _abi.default_options(general_bounds=int(f["general_bounds"]), max_iter=k)
+        r = O.solve_one(prob, x, f[f"{case}_xg"][i], hm, opt=o, X_init=None if xi is None else xi[i])
+        return max(float(np.abs(r["X"] - f[f"{case}_Xpin"][i]).max()),
+                   float(np.abs(r["U"] - f[f"{case}_Upin"][i]).max()))
+
+    jobs = [(int(i), pd) for i in idx for pd in WIDE]
+    with ThreadPoolExecutor(16) as ex:
+        devs = np.array(list(ex.map(one, jobs))).reshape(len(idx), len(WIDE))
+    for i, d in zip(idx, devs):
+        print(f"[pinned] {case} {form} instance {int(i)} (k_i {int(f[f'{case}_kpin'][i])}): oracle from the WIDE starts "
+              f"max |dev| {d.max():.2e}", flush=True)
+    return {int(i) for i, d in zip(idx, devs) if d.max() > TOL}
+
+
 @pytest.mark.parametrize("form", list(FILES))
 @pytest.mark.parametrize("case", ["metric", "b6"])
 def test_pinned_iterates_match_oracle(case, form, artefact):
@@ -92,6 +135,10 @@ def test_pinned_iterates_match_oracle(case, form, artefact):
         bad[arith] = b
         print(f"[pinned] {case} {form} {arith}: {len(b)} of {len(kp)} outside",
               [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in b], flush=True)
+    union = np.union1d(bad["f32"], bad["split_bf16"])
+    exc = _wide_excused(f, case, form, union, artefact) if len(union) else set()
+    left = {a: np.array([i for i in bad[a] if int(i) not in exc], int) for a in bad}
+    print(f"[pinned] {case} {form}: excused by the oracle's WIDE starts {sorted(exc)}; left {left}", flush=True)
     cap = max(1, int(0.05 * len(kp)))
-    assert len(bad["f32"]) <= cap and len(bad["split_bf16"]) <= cap, bad
-    assert len(np.intersect1d(bad["f32"], bad["split_bf16"])) == 0, bad
+    assert len(left["f32"]) <= cap and len(left["split_bf16"]) <= cap, left
+    assert len(np.intersect1d(left["f32"], left["split_bf16"])) == 0, left
