@@ -3214,26 +3214,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     const int nc = dm.nc;
     constexpr double kMuMin = 1e-11;
     (void)o;
+    // the lane-strided sums: every pass's first chunk loaded ahead (Pre), consumed in the same per-lane order as the
+    // plain loops they replace (one memory round trip instead of one per pass and per 64 elements)
     auto theta_phi = [&](double mu, double* th, double* phv, double* fout = nullptr) {
         double t = 0, bar = 0, lin = 0;
-        for (int i = lane; i < NX; i += 64) t += fabs(AT(rci, i));
-        for (int i = lane; i < nc; i += 64) t += fabs(AT(rct, i));
-        for (int i = lane; i < N * NX; i += 64) t += fabs(AT(rcd, i));
-        for (int q = lane; q < (N + 1) * M; q += 64) {
-            t += fabs(AT(rcq, q));
-            bar += log(AT(T, q));
-            lin += AT(T, q);
-        }
-        for (int e = lane; e < N * NU; e += 64) {
-            const double u = BVU(e);
+        auto tsum = [&](int, const double* v) { t += fabs(v[0]); };
+        auto l_rci = [&](int i, double* v) { v[0] = AT(rci, i); };
+        auto l_rct = [&](int i, double* v) { v[0] = AT(rct, i); };
+        auto l_rcd = [&](int i, double* v) { v[0] = AT(rcd, i); };
+        auto l_rcq = [&](int q, double* v) { v[0] = AT(rcq, q); v[1] = AT(T, q); };
+        auto l_bu = [&](int e, double* v) { v[0] = BVU(e); };
+        auto l_bs = [&](int k, double* v) { v[0] = BVS(k); };
+        auto l_rcb = [&](int q, double* v) { v[0] = AT(rcb, q); };
+        Pre<1, 1> q_rci, q_rct, q_bs;
+        Pre<4, 1> q_rcd;
+        Pre<1, 2> q_rcq;
+        Pre<2, 1> q_bu;
+        Pre<3, 1> q_rcb;
+        q_rci.load(NX, lane, l_rci);
+        q_rct.load(nc, lane, l_rct);
+        q_rcd.load(N * NX, lane, l_rcd);
+        q_rcq.load((N + 1) * M, lane, l_rcq);
+        q_bu.load(N * NU, lane, l_bu);
+        if (dm.ns) q_bs.load(N + 1, lane, l_bs);
+        q_rcb.load(ngb, lane, l_rcb);
+        q_rci.run(NX, lane, l_rci, tsum);
+        q_rct.run(nc, lane, l_rct, tsum);
+        q_rcd.run(N * NX, lane, l_rcd, tsum);
+        q_rcq.run((N + 1) * M, lane, l_rcq, [&](int, const double* v) {
+            t += fabs(v[0]);
+            bar += log(v[1]);
+            lin += v[1];
+        });
+        q_bu.run(N * NU, lane, l_bu, [&](int e, const double* v) {
+            const double u = v[0];
             bar += log(u - p.umin[e % NU]) + log(p.umax[e % NU] - u);
-        }
+        });
         if (dm.ns)
-            for (int k = lane; k <= N; k += 64) {
-                bar += log(BVS(k));
-                lin += BVS(k);
-            }
-        for (int q = lane; q < ngb; q += 64) t += fabs(AT(rcb, q));
+            q_bs.run(N + 1, lane, l_bs, [&](int, const double* v) {
+                bar += log(v[0]);
+                lin += v[0];
+            });
+        q_rcb.run(ngb, lane, l_rcb, tsum);
         *th = wsum(t);
         const double fo = objective_w(p, dm, ws, b, lane, 0.0);
         *phv = fo - mu * wsum(bar) + 1e-5 * mu * wsum(lin);
@@ -3510,13 +3532,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
     const double kappa_d = 1e-5;
     double amax = 1.0, az = 1.0, gd = 0;
     for (int k = lane; k <= N; k += 64) {
-        for (int j = 0; j < M; ++j) {
+        // every input of the knot loaded before its first store (the stores might alias them for the compiler: each
+        // group of loads after a store was another dependent round trip); the arithmetic below is unchanged
+        double jd[MMAX][3], tq[MMAX], vq[MMAX], rq[MMAX], dxk[3], xs[3][2];
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) {
+            if (j >= M) break;
+            const int q = k * M + j;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) jd[j][a] = a < NX ? AT(Jd, q * 3 + a) : 0.0;
+            tq[j] = AT(T, q);
+            vq[j] = AT(vt, q);
+            rq[j] = AT(rcq, q);
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) dxk[a] = a < NX ? AT(dX, k * NX + a) : 0.0;
+        const double dSk = (dm.sd || dm.ns) ? AT(dS, k) : 0.0;
+        const int qb = N * NU + k;
+        const double Sk = dm.ns ? AT(S, k) : 0.0, zsk = dm.ns ? AT(zs, k) : 0.0;
+        const double sbk = (dm.ns && dm.gcb) ? AT(sb, qb) : 0.0, rcbk = (dm.ns && dm.gcb) ? AT(rcb, qb) : 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {  // knots k - 1, k, k + 1 (x, y) of the path-length term
+            const int kk = k - 1 + r;
+            xs[r][0] = (kk >= 0 && kk <= N) ? AT(X, kk * NX) : 0.0;
+            xs[r][1] = (kk >= 0 && kk <= N) ? AT(X, kk * NX + 1) : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) {
+            if (j >= M) break;
             const int q = k * M + j;
             double Jdz = 0;
-            for (int a = 0; a < 3 && a < NX; ++a) Jdz += AT(Jd, q * 3 + a) * AT(dX, k * NX + a);
-            if (dm.sd) Jdz += AT(dS, k);
-            const double t = AT(T, q), v = AT(vt, q);
-            const double dt_ = Jdz + AT(rcq, q);
+            for (int a = 0; a < 3 && a < NX; ++a) Jdz += jd[j][a] * dxk[a];
+            if (dm.sd) Jdz += dSk;
+            const double t = tq[j], v = vq[j];
+            const double dt_ = Jdz + rq[j];
             const double dvt_ = mu / t - v - (v / t) * dt_;
             AT(dT, q) = dt_;
             AT(yd_n, q) = (v / t + dw) * dt_ + (-mu / t + kappa_d * mu);
@@ -3527,67 +3576,79 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))
         }
         if (dm.ns) {
             if (dm.gcb) {  // the bound row S - sb: sb's step, the row multiplier (oracle recover)
-                const int qb = N * NU + k;
-                const double s = AT(S, k), ds = AT(dS, k), sv = AT(sb, qb), db = ds + AT(rcb, qb);
-                const double sig = AT(zs, k) / sv, bg = -mu / sv + kappa_d * mu;
-                const double dzs_ = mu / sv - AT(zs, k) - sig * db;
+                const double s = Sk, ds = dSk, sv = sbk, db = ds + rcbk;
+                const double sig = zsk / sv, bg = -mu / sv + kappa_d * mu;
+                const double dzs_ = mu / sv - zsk - sig * db;
                 AT(dsb, qb) = db;
                 AT(yb_n, qb) = (sig + dw) * db + bg;
                 AT(dzs, k) = dzs_;
                 amax = frac_to_bound(sv, db, tau, amax);
-                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                az = frac_to_bound(zsk, dzs_, tau, az);
                 gd += 2.0 * p.slack_penalty * s * ds + bg * db;
             } else {
-                const double s = AT(S, k), ds = AT(dS, k);
-                const double dzs_ = mu / s - AT(zs, k) - (AT(zs, k) / s) * ds;
+                const double s = Sk, ds = dSk;
+                const double dzs_ = mu / s - zsk - (zsk / s) * ds;
                 AT(dzs, k) = dzs_;
                 amax = frac_to_bound(s, ds, tau, amax);
-                az = frac_to_bound(AT(zs, k), dzs_, tau, az);
+                az = frac_to_bound(zsk, dzs_, tau, az);
                 gd += (2.0 * p.slack_penalty * s - mu / s + kappa_d * mu) * ds;
             }
         }
-        for (int seg = k - 1; seg <= k; ++seg) {  // path-length gradient . dx_k
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {  // path-length gradient . dx_k: segments k - 1 and k
+            const int seg = k - 1 + r;
             if (seg < 0 || seg >= N) continue;
-            const double dx = AT(X, (seg + 1) * NX) - AT(X, seg * NX);
-            const double dy = AT(X, (seg + 1) * NX + 1) - AT(X, seg * NX + 1);
+            const double dx = xs[r + 1][0] - xs[r][0];
+            const double dy = xs[r + 1][1] - xs[r][1];
             const double rr = sqrt(dx * dx + dy * dy + p.path_eps);
             const double sgn = seg == k ? -1.0 : 1.0;
-            gd += sgn * (dx / rr) * AT(dX, k * NX) + sgn * (dy / rr) * AT(dX, k * NX + 1);
+            gd += sgn * (dx / rr) * dxk[0] + sgn * (dy / rr) * dxk[1];
         }
     }
-    for (int e = lane; e < N * NU; e += 64) {
+    // the controls' bound rows in chunks of 2 x 64 (loads before stores; same element order as the plain loop)
+    chunked_update<2, 6>(N * NU, lane,
+                         [&](int e, double* v) {
+                             v[0] = AT(U, e);
+                             v[1] = AT(dU, e);
+                             v[2] = dm.gcb ? AT(sb, e) : 0.0;
+                             v[3] = dm.gcb ? AT(rcb, e) : 0.0;
+                             v[4] = AT(zl, e);
+                             v[5] = AT(zu, e);
+                         },
+                         [&](int e, const double* v) {
         const int i = e % NU, k = e / NU;
+        const double zle = v[4], zue = v[5];
         if (dm.gcb) {  // the bound row U - sb: sb's step d_sb = dU + rcb, the row multiplier (oracle recover)
-            const double u = AT(U, e), du = AT(dU, e), bv = AT(sb, e), sl = bv - p.umin[i], su = p.umax[i] - bv;
-            const double db = du + AT(rcb, e);
-            const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * db;
-            const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * db;
-            const double sig = AT(zl, e) / sl + AT(zu, e) / su, bg = -mu / sl + mu / su;
+            const double u = v[0], du = v[1], bv = v[2], sl = bv - p.umin[i], su = p.umax[i] - bv;
+            const double db = du + v[3];
+            const double dzl_ = mu / sl - zle - (zle / sl) * db;
+            const double dzu_ = mu / su - zue + (zue / su) * db;
+            const double sig = zle / sl + zue / su, bg = -mu / sl + mu / su;
             AT(dsb, e) = db;
             AT(yb_n, e) = (sig + dw) * db + bg;
             AT(dzl, e) = dzl_;
             AT(dzu, e) = dzu_;
             amax = frac_to_bound(sl, db, tau, amax);
             amax = frac_to_bound(su, -db, tau, amax);
-            az = frac_to_bound(AT(zl, e), dzl_, tau, az);
-            az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+            az = frac_to_bound(zle, dzl_, tau, az);
+            az = frac_to_bound(zue, dzu_, tau, az);
             if (p.use_smooth && k < N - 1) gd += 2.0 * p.smooth_weight * u * du;
             gd += bg * db;
-            continue;
+            return;
         }
-        const double u = AT(U, e), sl = u - p.umin[i], su = p.umax[i] - u, du = AT(dU, e);
-        const double dzl_ = mu / sl - AT(zl, e) - (AT(zl, e) / sl) * du;
-        const double dzu_ = mu / su - AT(zu, e) + (AT(zu, e) / su) * du;
+        const double u = v[0], sl = u - p.umin[i], su = p.umax[i] - u, du = v[1];
+        const double dzl_ = mu / sl - zle - (zle / sl) * du;
+        const double dzu_ = mu / su - zue + (zue / su) * du;
         AT(dzl, e) = dzl_;
         AT(dzu, e) = dzu_;
         amax = frac_to_bound(sl, du, tau, amax);
         amax = frac_to_bound(su, -du, tau, amax);
-        az = frac_to_bound(AT(zl, e), dzl_, tau, az);
-        az = frac_to_bound(AT(zu, e), dzu_, tau, az);
+        az = frac_to_bound(zle, dzl_, tau, az);
+        az = frac_to_bound(zue, dzu_, tau, az);
         double gu = -mu / sl + mu / su;
         if (p.use_smooth && k < N - 1) gu += 2.0 * p.smooth_weight * u;
         gd += gu * du;
-    }
+                         });
     amax = wmin(amax);
     az = wmin(az);
     gd = wsum(gd);
