@@ -222,17 +222,24 @@ static void oracle_mlp_point_smooth(const NlotMlpDesc* m, float px, float py, fl
  * layers, output layer, reverse sweep, input-layer contraction) accumulates in the reverse index order.  The result
  * differs from the default only by fp32 rounding: the same kind of difference the GPU's split-bf16 MFMA sums make, so
  * a solve whose outcome changes under it is not reproducible at the GPU's arithmetic.  Read per call (toggled
- * between whole batches by the Python side). */
+ * between whole batches by the Python side).  NLOT_ORACLE_MLP_REV=v >= 2: the index order i -> (i * m_v) mod H with
+ * an odd multiplier m_v (a permutation for H a power of two): more samples of the same kind of difference
+ * (tests/test_pinned_iterates_gpu.py). */
 static int mlp_rev(void) {
     const char* e = getenv("NLOT_ORACLE_MLP_REV");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
+}
+static int mlp_perm_mult(int v) {
+    static const int m[8] = {1, 1, 3, 5, 7, 11, 13, 17};
+    return m[v & 7];
 }
 
 void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
     enum { HM = 256, LM = 8 };
     const int H = m->hidden;
     const int rv = mlp_rev();
-#define RIX(i) (rv ? H - 1 - (i) : (i))
+    const int rvm = mlp_perm_mult(rv);
+#define RIX(i) (rv == 0 ? (i) : rv == 1 ? H - 1 - (i) : ((i) * rvm) % H)
     if (m->act != NLOT_ACT_RELU) {
         oracle_mlp_point_smooth(m, px, py, lam, want, out);
         return;
@@ -866,24 +873,37 @@ static int sol_alloc(Sol* s) {
 /* ============================================================================================ */
 /* NLP evaluation (runner.py:44-108)                                                            */
 /* ============================================================================================ */
+/* NLOT_ORACLE_SUM_REV=1 (test infrastructure, tests/test_pinned_iterates_gpu.py): the merit function's fp64 sums
+ * (theta, the barrier terms, the objective and the restoration objective: the values the filter and Armijo tests
+ * compare) accumulate in the reverse index order.  The result differs from the default only by fp64 rounding: the
+ * kind of difference the GPU's wave reductions make in every iteration (another summation order), where the
+ * fixture's perturbed runs differ only at the start.  Read per call (toggled between whole batches). */
+static int sum_rev(void) {
+    const char* e = getenv("NLOT_ORACLE_SUM_REV");
+    return e && e[0] == '1';
+}
+#define SRV(i, n) (srv ? (n) - 1 - (i) : (i))
+
 /* objective value at (X, U, S)  — runner.py:80-96 */
 static double objective(const Sol* s, const double* X, const double* U, const double* S) {
     const NlotProblem* p = s->p;
     int nx = s->nx, nu = s->nu, N = s->N;
+    const int srv = sum_rev();
     double f = 0;
-    for (int k = 0; k < N; ++k) {
+    for (int k_ = 0; k_ < N; ++k_) {
+        const int k = SRV(k_, N);
         double dx = X[(k + 1) * nx] - X[k * nx], dy = X[(k + 1) * nx + 1] - X[k * nx + 1];
         f += sqrt(dx * dx + dy * dy + p->path_eps);
     }
     if (p->use_slack) {
         double q = 0;
-        for (int k = 0; k <= N; ++k) q += S[k] * S[k];
+        for (int k = 0; k <= N; ++k) q += S[SRV(k, N + 1)] * S[SRV(k, N + 1)];
         f += p->slack_penalty * q;
     }
     if (p->use_smooth) {
         double q = 0;
         for (int k = 0; k < N - 1; ++k) /* sum_{k < N-1} ||u_k||^2, runner.py:92-95 (bug F7c kept) */
-            for (int i = 0; i < nu; ++i) q += U[k * nu + i] * U[k * nu + i];
+            for (int i = 0; i < nu; ++i) q += U[SRV(k, N - 1) * nu + i] * U[SRV(k, N - 1) * nu + i];
         f += p->smooth_weight * q;
     }
     return f;
@@ -893,12 +913,25 @@ static double objective(const Sol* s, const double* X, const double* U, const do
 static double objective_resto(const Sol* s, const double* X, const double* U, const double* S, const double* p,
                               const double* n) {
     int nx = s->nx, nu = s->nu, N = s->N;
+    const int srv = sum_rev();
     double a = 0, q = 0;
-    for (int i = 0; i < s->ne; ++i) a += p[i] + n[i];
-    for (int i = 0; i < (N + 1) * nx; ++i) q += pow(s->DRX[i] * (X[i] - s->XR[i]), 2);
-    for (int i = 0; i < N * nu; ++i) q += pow(s->DRU[i] * (U[i] - s->UR[i]), 2);
+    for (int i_ = 0; i_ < s->ne; ++i_) {
+        const int i = SRV(i_, s->ne);
+        a += p[i] + n[i];
+    }
+    for (int i_ = 0; i_ < (N + 1) * nx; ++i_) {
+        const int i = SRV(i_, (N + 1) * nx);
+        q += pow(s->DRX[i] * (X[i] - s->XR[i]), 2);
+    }
+    for (int i_ = 0; i_ < N * nu; ++i_) {
+        const int i = SRV(i_, N * nu);
+        q += pow(s->DRU[i] * (U[i] - s->UR[i]), 2);
+    }
     if (s->ns)
-        for (int k = 0; k <= N; ++k) q += pow(s->DRS[k] * (S[k] - s->SR[k]), 2);
+        for (int k_ = 0; k_ <= N; ++k_) {
+            const int k = SRV(k_, N + 1);
+            q += pow(s->DRS[k] * (S[k] - s->SR[k]), 2);
+        }
     return s->rho * a + 0.5 * s->zeta * q;
 }
 
@@ -930,22 +963,28 @@ static void barrier_terms(const Sol* s, const double* U, const double* S, const 
                           double* bar_out, double* lin_out) {
     const NlotProblem* p = s->p;
     int nu = s->nu, N = s->N, M = s->M;
+    const int srv = sum_rev();
     double bar = 0, lin = 0;
-    for (int q = 0; q < (N + 1) * M; ++q) {
+    for (int q_ = 0; q_ < (N + 1) * M; ++q_) {
+        const int q = SRV(q_, (N + 1) * M);
         bar += log(T[q]);
         lin += T[q];
     }
     if (s->gcb) {
-        for (int q = 0; q < s->nb; ++q) {
+        for (int q_ = 0; q_ < s->nb; ++q_) {
+            const int q = SRV(q_, s->nb);
             bar += log(SB[q] - blo(s, q));
             if (bhi_on(s, q)) bar += log(bhi(s, q) - SB[q]);
             else lin += SB[q];
         }
     } else {
-        for (int k = 0; k < N; ++k)
+        for (int k_ = 0; k_ < N; ++k_) {
+            const int k = SRV(k_, N);
             for (int i = 0; i < nu; ++i) bar += log(U[k * nu + i] - p->umin[i]) + log(p->umax[i] - U[k * nu + i]);
+        }
         if (s->ns)
-            for (int k = 0; k <= N; ++k) {
+            for (int k_ = 0; k_ <= N; ++k_) {
+                const int k = SRV(k_, N + 1);
                 bar += log(S[k] + s->brel);
                 lin += S[k] + s->brel;
             }
@@ -971,11 +1010,12 @@ static void merit_r(const Sol* s, const double* X, const double* U, const double
     if (!rcb) rcb = bb;
     residuals(s, X, U, S, T, SB, rci, rcd, rct, rcq, rcb);
     double th = 0, bar, lin;
-    for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
-    for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
-    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
-    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[q]);
-    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[q]);
+    const int srv = sum_rev();
+    for (int i = 0; i < nx; ++i) th += fabs(rci[SRV(i, nx)]);
+    for (int j = 0; j < s->nc; ++j) th += fabs(rct[SRV(j, s->nc)]);
+    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[SRV(i, N * nx)]);
+    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[SRV(q, (N + 1) * M)]);
+    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[SRV(q, s->nb)]);
     free(bd);
     barrier_terms(s, U, S, T, SB, &bar, &lin);
     const double kappa_d = 1e-5;
@@ -1005,14 +1045,16 @@ static void merit_resto(const Sol* s, const double* X, const double* U, const do
     for (int q = 0; q < (N + 1) * M; ++q) rcq[q] += -pp[row_q(s, q)] + nn[row_q(s, q)];
     for (int q = 0; q < s->nb; ++q) rcb[q] += -pp[row_b(s, q)] + nn[row_b(s, q)];
     double th = 0, bar, lin;
-    for (int i = 0; i < nx; ++i) th += fabs(rci[i]);
-    for (int j = 0; j < s->nc; ++j) th += fabs(rct[j]);
-    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[i]);
-    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[q]);
-    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[q]);
+    const int srv = sum_rev();
+    for (int i = 0; i < nx; ++i) th += fabs(rci[SRV(i, nx)]);
+    for (int j = 0; j < s->nc; ++j) th += fabs(rct[SRV(j, s->nc)]);
+    for (int i = 0; i < N * nx; ++i) th += fabs(rcd[SRV(i, N * nx)]);
+    for (int q = 0; q < (N + 1) * M; ++q) th += fabs(rcq[SRV(q, (N + 1) * M)]);
+    for (int q = 0; q < s->nb; ++q) th += fabs(rcb[SRV(q, s->nb)]);
     free(bd);
     barrier_terms(s, U, S, T, SB, &bar, &lin);
-    for (int i = 0; i < s->ne; ++i) {
+    for (int i_ = 0; i_ < s->ne; ++i_) {
+        const int i = SRV(i_, s->ne);
         bar += log(pp[i]) + log(nn[i]);
         lin += pp[i] + nn[i];
     }
@@ -2305,6 +2347,26 @@ static double barrier_gd(const Sol* s) {
 }
 
 /* Newton step with IPOPT's inertia correction (delta_w); 0 ok, 1 failed */
+/* NLOT_ORACLE_STEP_JITTER=eps (test infrastructure, tests/test_pinned_iterates_gpu.py): every Newton step's primal
+ * components are scaled by 1 +- eps (a fixed pseudo-random sign per component and step): a model of the rounding
+ * differences of another fp64 summation order in the KKT solve (the GPU's lane-group Riccati sweeps), injected in
+ * every iteration where the fixture's perturbed runs differ only at the start.  0 or unset: off (the default). */
+static void step_jitter(Sol* s) {
+    const char* e = getenv("NLOT_ORACLE_STEP_JITTER");
+    const double eps = e ? atof(e) : 0.0;
+    if (eps == 0.0) return;
+    static __thread unsigned long long ctr = 0;
+    const int nX = (s->N + 1) * s->nx, nU = s->N * s->nu;
+    for (int i = 0; i < nX + nU + s->N + 1; ++i) {
+        unsigned long long h = (++ctr) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 31;
+        const double f = 1.0 + ((h >> 7) & 1 ? eps : -eps);
+        if (i < nX) s->dX[i] *= f;
+        else if (i < nX + nU) s->dU[i - nX] *= f;
+        else s->dS[i - nX - nU] *= f;
+    }
+}
+
 static int newton_step(Sol* s, double* dw_out) {
     double dw = 0.0;
     build(s, MODE_NEWTON, dw);
@@ -2319,6 +2381,7 @@ static int newton_step(Sol* s, double* dw_out) {
         s->dw_last = dw;
     }
     *dw_out = dw;
+    step_jitter(s);
     return 0;
 }
 

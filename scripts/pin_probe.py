@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--case", default="b6")
     ap.add_argument("--inst", type=int, nargs="+", default=[3])
     ap.add_argument("--kmax", type=int, default=24)
+    ap.add_argument("--kmin", type=int, default=1)
+    ap.add_argument("--kstep", type=int, default=1)
+    ap.add_argument("--arith", default="split_bf16", choices=["split_bf16", "f32"])
     ap.add_argument("--form", default="rows")
     a = ap.parse_args()
     import oracle as O
@@ -41,7 +44,7 @@ def main():
         w = MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
     else:
         prob, w = METRIC_PROBLEM, MlpWeights.artefact()
-    hm, mlp = O.HostMlp(w), DeviceMlp(w)
+    hm, mlp = O.HostMlp(w), DeviceMlp(w, a.arith)
     gb = int(f["general_bounds"])
     N, nx, nu = prob.N, prob.nx, prob.nu
     for i in a.inst:
@@ -56,8 +59,8 @@ def main():
                 traces.append(O.solve_trace(prob, x, xg, hm, opt=opt, X_init=xi, cap=a.kmax + 1)["trace"])
         T0 = traces[0]
         print(f"instance {i}: kpin {int(f[f'{a.case}_kpin'][i])}, oracle status {int(f[f'{a.case}_status'][0, i])} "
-              f"iters {int(f[f'{a.case}_iters'][0, i])}, NLOT_MLP={os.environ.get('NLOT_MLP', 'bf16')}", flush=True)
-        for k in range(1, a.kmax + 1):
+              f"iters {int(f[f'{a.case}_iters'][0, i])}, net {a.arith}", flush=True)
+        for k in range(a.kmin, a.kmax + 1, a.kstep):
             o = _abi.default_options(general_bounds=gb, max_iter=k)
             r = solve_batch(prob, x0[None], xg[None], mlp=mlp, X_init=None if xi is None else xi[None], options=o)
             g = np.concatenate([r["X"][0].cpu().numpy().ravel(), r["U"][0].cpu().numpy().ravel()])

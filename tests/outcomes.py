@@ -16,7 +16,8 @@ final cost (ReLU kinks, discrete filter / watchdog / mode decisions; DESIGN.md Â
     the GPU's outcome itself under one of the twelve WIDE starts below is chaotic (b6 fixture instance 18: restoration failure at iteration 404 under
     every start up to x0 +- 1e-7 but x0 + 1e-7 e_y, which ends in max_iter, as the GPU's split-bf16 net does);
   * chaotic: the rest.  There the bar is the oracle's own spread: status agreement with the unperturbed oracle at
-    least as high as the perturbed oracles' (less two instances of sampling slack); among the jointly solved, the
+    least as high as the perturbed oracles' (less the sampling slack: two instances or two binomial standard
+    deviations of the rate on that many instances, whichever is larger); among the jointly solved, the
     share whose final cost differs by more than 1e-4 (another local optimum) at most the perturbed oracles' share
     (plus two instances), and no difference beyond 3x the oracle's own largest (or 1e-4).  Five perturbed runs see
     few of a multimodal instance's local optima: where the GPU's cost lies beyond that bound, the oracle's envelope
@@ -41,10 +42,11 @@ XDEV_REPRO = 1e-6  # a failed run counts as reproducible when every perturbed ru
 
 @contextlib.contextmanager
 def mlp_order(rev):
-    """The oracle's net summation order for the runs inside (process-wide: run batches, not instances, under it)."""
+    """The oracle's net summation order for the runs inside (process-wide: run batches, not instances, under it):
+    False / 0 the default, True / 1 reversed, v >= 2 the permuted order i -> (i m_v) mod H (oracle/nlot_oracle.c)."""
     old = os.environ.get("NLOT_ORACLE_MLP_REV")
     if rev:
-        os.environ["NLOT_ORACLE_MLP_REV"] = "1"
+        os.environ["NLOT_ORACLE_MLP_REV"] = str(int(rev))
     else:
         os.environ.pop("NLOT_ORACLE_MLP_REV", None)
     try:
@@ -225,8 +227,12 @@ def check_outcome_parity(label, sg, cg, out, min_reproducible=0, widen=None, exc
     assert not bad_cost.any(), (label, "cost beyond 1e-4 on oracle-reproducible instances",
                                 np.where(bad_cost)[0].tolist(), rel[bad_cost].tolist(), info)
     if C.any():
-        slack = 2.0 / C.sum()
-        assert info["chaotic_gpu_status_agree"] >= info["chaotic_oracle_self_agree"] - slack, (label, info)
+        # sampling slack: two instances, or two binomial standard deviations of an agreement rate measured on the
+        # chaotic group's n instances (b6: n ~ 23, one instance is 0.04 of the rate)
+        ps = info["chaotic_oracle_self_agree"]
+        slack = max(2.0 / C.sum(), 2.0 * np.sqrt(ps * (1.0 - ps) / C.sum()))
+        info["chaotic_agree_slack"] = float(slack)
+        assert info["chaotic_gpu_status_agree"] >= ps - slack, (label, info)
         if "chaotic_joint_solved" in info:
             # the share of jointly solved chaotic instances whose cost moves beyond 1e-4 (another local optimum) is at
             # most the perturbed oracles' share plus two instances of sampling slack; no difference beyond 3x the

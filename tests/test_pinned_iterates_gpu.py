@@ -18,9 +18,12 @@ it at k_i already (scripts/pin_probe.py: b6 instance 3 at iteration 6 under the 
 oracle's 3.5e-6 spread and 7e-2 one iteration later, while the f32 net tracks the oracle to 1.6e-6 through k_i = 20;
 metric instance 63 the other way round).  The GPU also rounds its fp64 sums (Riccati sweeps, reductions) in other
 orders in every iteration, where the fixture's runs differ only at the start.  So an instance outside 1e-4 is run on
-the oracle from the twelve WIDE starts (x0 +- 1e-11 .. 1e-7, tests/outcomes.py) up to k_i: if one of them leaves the
-pinned iterate by more than 1e-4 there too, k_i was optimistic for the GPU's perturbation size and the instance is
-excused.  Per net every remaining instance but 5 % (at least one), and none may miss under both nets: a miss one net
+the oracle up to k_i from the twelve WIDE starts (x0 +- 1e-11 .. 1e-7, tests/outcomes.py) and with six more orders of
+the net's fp32 sums (NLOT_ORACLE_MLP_REV = 2..7: i -> i m mod H; the fixture's k_i rests on one such sample, the
+reversed order): if one of them leaves the pinned iterate by more than 1e-4 there too, k_i was optimistic for the
+GPU's perturbation size and the instance is excused (b6 variable-bound instance 3: four of the six orders end 5.0
+away at k_i = 87, as both GPU nets do; the oracle is insensitive there to 1e-11 relative noise on every Newton
+step).  Per net every remaining instance but 5 % (at least one), and none may miss under both nets: a miss one net
 does not share is that net's rounding, not the solver."""
 import os
 
@@ -73,7 +76,7 @@ def _wide_excused(f, case, form, idx, artefact):
     from concurrent.futures import ThreadPoolExecutor
 
     import oracle as O
-    from outcomes import WIDE
+    from outcomes import WIDE, mlp_order
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
@@ -97,12 +100,18 @@ def _wide_excused(f, case, form, idx, artefact):
         return max(float(np.abs(r["X"] - f[f"{case}_Xpin"][i]).max()),
                    float(np.abs(r["U"] - f[f"{case}_Upin"][i]).max()))
 
-    jobs = [(int(i), pd) for i in idx for pd in WIDE]
+    orders = (0, 2, 3, 4, 5, 6, 7)  # the net's summation order (one batch per order: the setting is process-wide)
+    devs = np.zeros((len(idx), 0))
     with ThreadPoolExecutor(16) as ex:
-        devs = np.array(list(ex.map(one, jobs))).reshape(len(idx), len(WIDE))
+        for v in orders:
+            starts = WIDE if v == 0 else ((0, 0.0, False),)
+            with mlp_order(v):
+                d = np.array(list(ex.map(one, [(int(i), pd) for i in idx for pd in starts]))).reshape(len(idx), -1)
+            devs = np.concatenate([devs, d], 1)
     for i, d in zip(idx, devs):
         print(f"[pinned] {case} {form} instance {int(i)} (k_i {int(f[f'{case}_kpin'][i])}): oracle from the WIDE starts "
-              f"max |dev| {d.max():.2e}", flush=True)
+              f"max |dev| {d[:len(WIDE)].max():.2e}, with other net orders {np.array2string(d[len(WIDE):], precision=1)}",
+              flush=True)
     return {int(i) for i, d in zip(idx, devs) if d.max() > TOL}
 
 
@@ -138,7 +147,7 @@ def test_pinned_iterates_match_oracle(case, form, artefact):
     union = np.union1d(bad["f32"], bad["split_bf16"])
     exc = _wide_excused(f, case, form, union, artefact) if len(union) else set()
     left = {a: np.array([i for i in bad[a] if int(i) not in exc], int) for a in bad}
-    print(f"[pinned] {case} {form}: excused by the oracle's WIDE starts {sorted(exc)}; left {left}", flush=True)
+    print(f"[pinned] {case} {form}: excused (the oracle leaves the path too) {sorted(exc)}; left {left}", flush=True)
     cap = max(1, int(0.05 * len(kp)))
     assert len(left["f32"]) <= cap and len(left["split_bf16"]) <= cap, left
     assert len(np.intersect1d(left["f32"], left["split_bf16"])) == 0, left
