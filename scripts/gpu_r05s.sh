@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5 final tree, part 1: the whole GPU suite (both NLP forms, both MLP arithmetics in the parity tests)
-OUT=gpurun_out/r05s
+OUT=gpurun_out/r05s2
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p $OUT
 export TMPDIR=/tmp
