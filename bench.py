@@ -73,10 +73,12 @@ def parse():
                     help="at least this many instances for the single-core CPU baseline, one at a time until ~8 s (default 2; 1 stress)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the host's CPU share: min(affinity, cgroup cpu.max quota))")
-    ap.add_argument("--cpu-overlap", choices=["on", "off"], default="on",
-                    help="on (metric / b6, one rank): the CPU baseline runs on the host cores during the untimed warm-up "
-                         "(the GPU stays busy meanwhile) on one thread fewer than the host's share (the solver's launch "
-                         "thread keeps one); it is joined before the timed region starts.  off: after the timed region")
+    ap.add_argument("--cpu-overlap", choices=["on", "off"], default="off",
+                    help="off (default since round 5): the CPU baseline runs after the timed region on the host's whole "
+                         "CPU share.  on (metric / b6, one rank): during the untimed warm-up on one thread fewer (the "
+                         "solver's launch thread keeps one), joined before the timed region; it competes with the "
+                         "solver's host thread and measured 7 % lower (0.485 vs 0.522 traj/s, profiles/r05/"
+                         "bench_r05ab_*.json), so it is no longer the default")
     ap.add_argument("--continuous", choices=["on", "off"], default="on",
                     help="on (metric / stress): the timed steps' batches flow through the solver with --batch slots "
                          "(continuous batching, NlotSolverOptions.max_active; all of them in one solve call), so one "
@@ -535,7 +537,7 @@ def main():
             "cpu_baseline": cpu,
         }
         if opt.general_bounds and not (stress or b6):  # the variable-bound form's figures, measured on the same tree
-            vf = os.path.join(ROOT, "profiles", "r05", "bench_varbounds.json")
+            vf = os.path.join(ROOT, "profiles", "r05", "bench_varbounds_r05ab.json")
             if os.path.exists(vf):
                 with open(vf) as f:
                     v = json.load(f)
