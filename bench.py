@@ -51,6 +51,7 @@ SPLIT_PRODUCTS = 6  # fp32-equivalent product = 6 bf16 MFMA products (nlot_mlp.h
 # (fp32) FLOPs is the dense bf16 peak / 6
 PEAK_SPLIT_TFLOPS = PEAK_BF16_MFMA_TFLOPS / SPLIT_PRODUCTS
 PEAK_HBM_GBS = 8000.0
+TIMING_EVERY = int(os.environ.get("NLOT_BENCH_TIMING_EVERY", "8"))  # hipEvents on one global step in 8 (nlot_set_timing)
 PEAK_F32_MFMA_NOTE = "dense f32-input MFMA peak (v_mfma_f32_16x16x4_f32; exact fp32 products)"
 
 
@@ -204,7 +205,8 @@ def main():
     opt_cont.max_active = slots
     agg_keys = ("mlp_full_ms", "mlp_full_launches", "mlp_points_full", "mlp_value_ms", "mlp_value_launches",
                 "mlp_points_value", "iterations", "iterate_ms", "mlp_points_full_reused", "ric_ms", "ric_launches",
-                "ric_solves", "ric_soc_solves", "ric_resto_solves", "filter_forgotten")
+                "ric_solves", "ric_soc_solves", "ric_resto_solves", "filter_forgotten", "timed_steps",
+                "timed_points_full", "timed_points_full_reused", "timed_points_value", "timed_ric_solves")
     agg = {k: 0 for k in agg_keys}
     agg["filter_peak"] = 0  # max over the timed calls
     timing = {"on": False}
@@ -244,7 +246,7 @@ def main():
     def sync():
         torch.cuda.synchronize()
         timing["on"] = not timing["on"]  # hipEvent timing inside the timed steps only
-        set_timing(timing["on"])
+        set_timing(TIMING_EVERY if timing["on"] else 0)
 
     warm_i = {"i": 0}
 
@@ -306,9 +308,14 @@ def main():
     # rooflines.  Dominant kernel by device time: k_ric (the Newton solve, latency/occupancy-bound fp64 with
     # ~2.8 KB of stage data per knot): HBM roofline on its algorithmic bytes.  The two SDF-MLP launches:
     # split-bf16 MFMA roofline on executed FLOP.
-    n_r = max(agg["ric_launches"], 1)
+    # the *_ms sums cover the event-timed global steps (one in TIMING_EVERY; each timed step queues ~10 event packets:
+    # timing every step cost 1.8 % traj/s, profiles/r05/ab_step_kernel_timing.log): per-launch averages over those
+    # steps' launches and the work they did (NlotSolveStats.timed_*, ABI v14); per-step totals scale by all / timed
+    n_t = max(agg["timed_steps"], 1)
+    t_scale = agg["iterations"] / n_t
+    n_r = n_t
     ric_avg_ms = agg["ric_ms"] / n_r
-    ric_solves_per_launch = agg["ric_solves"] / n_r
+    ric_solves_per_launch = agg["timed_ric_solves"] / n_r
     ric_bytes = ric_bytes_per_solve(prob)
     ric_achieved = ric_solves_per_launch * ric_bytes / (ric_avg_ms * 1e-3) / 1e9 if ric_avg_ms > 0 else 0.0
     # SURVEY.md §8d's algorithmic figure per problem-iteration: 2 * 4 * (nvar + ncon) bytes (read + write the
@@ -333,17 +340,17 @@ def main():
     flop_pt = w.flops_per_point_fwd_grad  # 67,072 for 2-128-128-1, 789,504 for 2-256x4-1
     flop_fwd = w.flops_per_point_fwd      # 33,536 / 394,752
     mlp_peak = PEAK_F32_MFMA_TFLOPS if streaming else PEAK_SPLIT_TFLOPS
-    n_l = max(agg["mlp_full_launches"], 1)
+    n_l = n_t
     avg_ms = agg["mlp_full_ms"] / n_l
-    reused = agg["mlp_points_full_reused"]
-    flop_launch = (agg["mlp_points_full"] * flop_pt - reused * flop_fwd) / n_l
+    reused = agg["timed_points_full_reused"]
+    flop_launch = (agg["timed_points_full"] * flop_pt - reused * flop_fwd) / n_l
     achieved = flop_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     traffic = None
     if pmc is not None:  # HBM bytes per point of the full launch inside the solve at bench size
-        traffic = pmc["mlp_full"]["hbm_bytes_per_point"] * agg["mlp_points_full"] / n_l
-    n_v = max(agg["mlp_value_launches"], 1)
+        traffic = pmc["mlp_full"]["hbm_bytes_per_point"] * agg["timed_points_full"] / n_l
+    n_v = n_t
     v_avg_ms = agg["mlp_value_ms"] / n_v
-    v_achieved = agg["mlp_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
+    v_achieved = agg["timed_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
 
     cpu = cpu_box.get("r")
     if cpu_here and cpu is None:
@@ -387,6 +394,7 @@ def main():
             "solves_per_launch": ric_solves_per_launch,
             "avg_launch_ms": ric_avg_ms,
             "launches": agg["ric_launches"],
+            "timed_launches": agg["timed_steps"],
             "side_stream_solves": {"second_order_corrections": agg["ric_soc_solves"],
                                    "restoration": agg["ric_resto_solves"],
                                    "factorisations_main": agg["ric_solves"]},
@@ -412,12 +420,13 @@ def main():
                          "the f32-input MFMA peak would be 157.3",
             "traffic": traffic if not stress else None,
             "flop_per_point": flop_pt,
-            "forward_reused_frac": reused / max(agg["mlp_points_full"], 1),
+            "forward_reused_frac": agg["mlp_points_full_reused"] / max(agg["mlp_points_full"], 1),
             "flop_counting": f"executed: {flop_pt:,} per point (2-{H}x{L + 1}-1 forward + reverse sweep), less the "
                              f"{flop_fwd:,} forward where it was reused",
-            "points_per_launch": agg["mlp_points_full"] / n_l,
+            "points_per_launch": agg["timed_points_full"] / n_l,
             "avg_launch_ms": avg_ms,
             "launches": agg["mlp_full_launches"],
+            "timed_launches": agg["timed_steps"],
             "traffic_note": (f"HBM bytes per point in the solve at B = 65536 ({os.path.relpath(tf, ROOT)}): "
                              f"{pmc['mlp_full']['hbm_bytes_per_point']:.1f} B/point = "
                              f"{pmc['mlp_full']['ratio_to_algorithmic_with_reuse']:.2f}x the algorithmic "
@@ -433,9 +442,10 @@ def main():
             "unit": "TFLOP/s",
             "frac": v_achieved / mlp_peak,
             "flop_per_point": flop_fwd,
-            "points_per_launch": agg["mlp_points_value"] / n_v,
+            "points_per_launch": agg["timed_points_value"] / n_v,
             "avg_launch_ms": v_avg_ms,
             "launches": agg["mlp_value_launches"],
+            "timed_launches": agg["timed_steps"],
         }
         if os.environ.get("NLOT_EARLY_VALUE", "1") != "0" and not streaming:
             note = ("per step, the value launch runs in two parts, the first on a fourth stream concurrently with the "
@@ -524,9 +534,11 @@ def main():
                             "note": "IPOPT's filters are unbounded lists; 0 forgotten = the GPU's filters behaved as "
                                     "unbounded on every timed instance"},
                 "lockstep_global_steps": agg["iterations"] // max(a.steps, 1),
-                "solver_step_kernel_ms_per_step": agg["iterate_ms"] / max(a.steps, 1),
-                "ric_ms_per_step": agg["ric_ms"] / max(a.steps, 1),
-                "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) / max(a.steps, 1),
+                "solver_step_kernel_ms_per_step": agg["iterate_ms"] * t_scale / max(a.steps, 1),
+                "ric_ms_per_step": agg["ric_ms"] * t_scale / max(a.steps, 1),
+                "mlp_ms_per_step": (agg["mlp_full_ms"] + agg["mlp_value_ms"]) * t_scale / max(a.steps, 1),
+                "event_timing": f"hipEvents on one global step in {TIMING_EVERY} ({agg['timed_steps']} of "
+                                f"{agg['iterations']} steps); the *_ms_per_step figures scale their sums by all / timed",
                 "instance_iterations_rank0": inst_iters,
                 # SDF-MLP work per instance-iteration (DESIGN.md §8f cost model): points the value launches (line-search
                 # candidates, speculative ones included) and the full launches evaluate per accepted iteration

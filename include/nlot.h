@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 13
+#define NLOT_ABI_VERSION 14
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -273,9 +273,19 @@ typedef struct NlotSolveStats {
     int32_t filter_capacity;   /* entries per filter (line search, adaptive-mu progress, restoration); ABI v11 */
     int32_t filter_peak;       /* the largest size any filter reached */
     int64_t filter_forgotten;  /* entries forgotten at capacity (IPOPT's filter is unbounded: 0 = faithful) */
+    /* ABI v14: the *_ms sums above cover the timed global steps only (nlot_set_timing); these count them and the
+     * work their launches did (one full MLP, one value MLP in up to two parts, one k_ric launch per step) */
+    int32_t timed_steps;
+    int32_t timing_every;
+    int64_t timed_points_full;
+    int64_t timed_points_full_reused;
+    int64_t timed_points_value;
+    int64_t timed_ric_solves;
 } NlotSolveStats;
-/* Enable/disable per-launch hipEvent timing of the MLP kernel inside nlot_solve_batch. */
-void nlot_set_timing(int32_t enabled);
+/* hipEvent timing of the MLP, solver-step and k_ric launches inside nlot_solve_batch: 0 off, 1 every global step,
+ * k > 1 one step in each group of k consecutive steps, at the position (group index mod k) (a sample over every
+ * position: each timed step adds ~10 event packets to the queue, ~2 % of the step time when every step is timed). */
+void nlot_set_timing(int32_t every);
 void nlot_last_stats(NlotSolveStats* out);
 
 /* ---- CasADi external compatibility shim (gen/nn_sdf.cpp:36-104) ----------------------------

@@ -75,7 +75,9 @@ class NlotSolveStats(C.Structure):
         ("mlp_points_full_reused", C.c_int64), ("ric_ms", C.c_double), ("ric_launches", C.c_int32),
         ("pad2_", C.c_int32), ("ric_solves", C.c_int64), ("ric_soc_solves", C.c_int64),
         ("ric_resto_solves", C.c_int64), ("filter_capacity", C.c_int32), ("filter_peak", C.c_int32),
-        ("filter_forgotten", C.c_int64),
+        ("filter_forgotten", C.c_int64), ("timed_steps", C.c_int32), ("timing_every", C.c_int32),
+        ("timed_points_full", C.c_int64), ("timed_points_full_reused", C.c_int64), ("timed_points_value", C.c_int64),
+        ("timed_ric_solves", C.c_int64),
     ]
 
 

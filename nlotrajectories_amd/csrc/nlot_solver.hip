@@ -2348,6 +2348,22 @@ static __global__ __launch_bounds__(64) void k_init_state(const NlotProblem* __r
     }
 }
 
+// End of global step s (one wave, after k_accept): the step's counter sets go to the host's pinned ring slot and the
+// free-slot count / admission flag to its flag pair (plain vector stores into mapped host memory, visible once the
+// stream's synchronisation sees the kernel complete); then the finished set C = cnt + CSET q is cleared for step s + 1
+// (its Cn) and the next step's set takes its early value launch's base, Cn[14] = Cn[1] (the candidates listed up to
+// now).  One launch in place of a D2H copy, a fill and a D2D copy per step (each a queue packet of its own).
+static __global__ __launch_bounds__(64) void k_step_end(int* __restrict__ cnt, int q, int* __restrict__ ring,
+                                                        int* __restrict__ hflag) {
+    const int l = threadIdx.x;
+    const int v = l < 2 * CSET + 2 ? cnt[l] : 0;
+    const int base = __shfl(v, CSET * (q ^ 1) + 1);
+    if (l < 2 * CSET) ring[l] = v;
+    else if (l < 2 * CSET + 2) hflag[l - 2 * CSET] = v;
+    if (l >= CSET * q && l < CSET * q + CSET) cnt[l] = 0;
+    else if (l == CSET * (q ^ 1) + 14) cnt[l] = base;
+}
+
 // continuous batching: instances first .. first + n - 1 take the n most recently freed slots, which join the active
 // list of the next step (its count cnt[2]; the position they start at goes to cnt[13] for k_init_state).  The host
 // asks for n <= the free slots (capacity - next active count); a shortfall sets the error flag cnt[2 CSET + 1].
@@ -5041,13 +5057,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
 // NLOT_UNIT = -1 holds the C ABI, the statistics and the dispatch; without NLOT_UNIT (tuning builds) one unit does all.
 #ifndef NLOT_UNIT
 static thread_local NlotSolveStats g_stats;
-static bool g_timing = false;
+static int g_timing = 0;  // nlot_set_timing: 0 off, k: the steps with index % k == 0
 #else
 extern thread_local NlotSolveStats g_stats;
-extern bool g_timing;
+extern int g_timing;
 #if NLOT_UNIT < 0
 thread_local NlotSolveStats g_stats;
-bool g_timing = false;
+int g_timing = 0;
 #endif
 #endif
 
@@ -5145,6 +5161,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     struct Res {
         int* hcnt = nullptr;
         hipEvent_t ev[KPIPE][10] = {};  // [8], [9]: the early value launch (NLOT_EARLY_VALUE) on its stream
+        hipEvent_t noev[10] = {};       // the untimed steps' (no events)
+        bool timed[KPIPE] = {};         // the ring slot's step was timed
         hipStream_t s2 = nullptr, s3 = nullptr, s4 = nullptr;       // side streams: SOC / restoration / early values
         hipEvent_t e_a = nullptr, e_soc = nullptr, e_r = nullptr, e_s = nullptr, e_v0 = nullptr, e_v1 = nullptr;
         ~Res() {
@@ -5160,7 +5178,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         }
     } res;
     // + 2: the free-slot count and k_admit's error flag, read at every synchronisation
-    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, (KPIPE * 2 * CSET + 2) * sizeof(int), hipHostMallocDefault));
+    NLOT_HIP_CHECK(hipHostMalloc((void**)&res.hcnt, (KPIPE * 2 * CSET + 2) * sizeof(int),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
     // The second-order corrections (substitution, short) and the restoration instances' Newton solves (a longer
     // sequential sweep, few instances) touch disjoint instances from the main Newton solve: they run on a side
     // stream, forked after k_iter_a, so their latency hides under k_ric's; k_iter_b joins the corrections, the
@@ -5194,7 +5213,9 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     int soc_fork = 0, early_value = 1;
     if (const char* e = getenv("NLOT_SOC_FORK")) soc_fork = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("NLOT_EARLY_VALUE")) early_value = atoi(e) != 0;
-    if (g_timing)
+    const int t_every = g_timing;
+    g_stats.timing_every = t_every;
+    if (t_every)
         for (int k = 0; k < KPIPE; ++k)
             for (int i = 0; i < 10; ++i) NLOT_HIP_CHECK(hipEventCreate(&res.ev[k][i]));
     MlpOut mo{}, mo_t[2] = {};
@@ -5261,6 +5282,12 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     res.hcnt[0] = capacity;  // step 0's active count (cnt[2] of counter set 0)
     NLOT_HIP_CHECK(hipMemcpyAsync(ws.cnt + 2, res.hcnt, sizeof(int), hipMemcpyHostToDevice, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));  // the pinned source is reused below
+    // the step's counter bookkeeping as one kernel (k_step_end) writing the pinned ring, or (NLOT_STEP_KERNEL=0) as
+    // the D2H / fill / D2D copies it replaces
+    bool step_kernel = true;
+    if (const char* e = getenv("NLOT_STEP_KERNEL")) step_kernel = atoi(e) != 0;
+    int* dcnt = nullptr;
+    NLOT_HIP_CHECK(hipHostGetDevicePointer((void**)&dcnt, res.hcnt, 0));
     // fold the counters of steps synced .. last into g_stats (after a synchronisation); updates n_active
     // NLOT_STEP_LOG=path (diagnostics, scripts/step_trace.py): one line per global step appended to path —
     // step, active, full-eval instances, trial slots, reused points, Newton solves, restoration count, corrections,
@@ -5295,7 +5322,16 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             g_stats.filter_peak = std::max(g_stats.filter_peak, hc[11]);
             g_stats.filter_forgotten += hc[12];
             hipEvent_t* e = res.ev[j];
-            if (e[0] && use_mlp) {
+            if (res.timed[j]) {
+                g_stats.timed_steps++;
+                g_stats.timed_ric_solves += hc[4];
+                if (use_mlp) {
+                    g_stats.timed_points_full += (int64_t)hc[0] * P;
+                    g_stats.timed_points_value += (int64_t)hc[1] * P;
+                    g_stats.timed_points_full_reused += (int64_t)hc[3];
+                }
+            }
+            if (res.timed[j] && use_mlp) {
                 float a = 0, c = 0;
                 (void)hipEventElapsedTime(&a, e[0], e[1]);
                 (void)hipEventElapsedTime(&c, e[2], e[3]);
@@ -5307,7 +5343,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
                     g_stats.mlp_value_ms += v0;
                 }
             }
-            if (e[4]) {
+            if (res.timed[j]) {
                 float a = 0, r = 0;
                 (void)hipEventElapsedTime(&a, e[4], e[5]);
                 (void)hipEventElapsedTime(&r, e[6], e[7]);
@@ -5330,14 +5366,18 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         const int* actr = ws.actr[cur];
         int* nxtr = ws.actr[cur ^ 1];
         const int kq = step % kpipe;
-        hipEvent_t* ev = res.ev[kq];
+        // one step in t_every, at a position in its group of t_every steps that rotates from group to group: the
+        // host's synchronisations (and so admissions, INIT steps) fall at a fixed position of the KPIPE window, so a
+        // fixed sampling phase would time one kind of step only
+        res.timed[kq] = t_every > 0 && step % t_every == (step / t_every) % t_every;
+        hipEvent_t* ev = res.timed[kq] ? res.ev[kq] : res.noev;
         // Point lists are appended to by the kernel that moves an instance into the phase needing them
         // (k_iter_b: first line-search round; k_accept: the new iterate, or the next round), so the lists
         // and counters of step s + 1 fill while step s runs: both alternate by step parity q.
         const int q = step & 1;
         int* C = ws.cnt + CSET * q;
         int* Cn = ws.cnt + CSET * (q ^ 1);
-        NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, CSET * sizeof(int), st));
+        if (!step_kernel) NLOT_HIP_CHECK(hipMemsetAsync(Cn, 0, CSET * sizeof(int), st));
         // the second-order corrections' chain (k_iter_a's SOC pass: their stages; k_ric<DYN, false, true>: the
         // substitutions) needs no MLP evaluation: it forks to the side stream at the start of the step (soc_fork 1),
         // after the full MLP launch (2), or after the one k_iter_a launch that also does the evaluations (0)
@@ -5357,7 +5397,7 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         // [0, C[14]), C[14] = C[1] now) evaluate on a side stream while this step's evaluations and Newton solves run;
         // the second part (after k_iter_b) covers the candidates added since (ranks [C[14], C[1]))
         if (use_mlp && early_value) {
-            NLOT_HIP_CHECK(hipMemcpyAsync(C + 14, C + 1, sizeof(int), hipMemcpyDeviceToDevice, st));
+            if (!step_kernel) NLOT_HIP_CHECK(hipMemcpyAsync(C + 14, C + 1, sizeof(int), hipMemcpyDeviceToDevice, st));
             NLOT_HIP_CHECK(hipEventRecord(res.e_v0, st));
             NLOT_HIP_CHECK(hipStreamWaitEvent(s4, res.e_v0, 0));
             if (ev[0]) (void)hipEventRecord(ev[8], s4);
@@ -5437,12 +5477,19 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
                            use_mlp ? ws.tpts[q ^ 1] : nullptr, use_mlp ? ws.tval[q] : nullptr, nspec);
         NLOT_HIP_CHECK(hipGetLastError());
         // this step's counters (C) and the next step's active count (Cn[2]), before step + 1 clears C
-        NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 2 * CSET * kq, ws.cnt, 2 * CSET * sizeof(int), hipMemcpyDeviceToHost, st));
+        int* hflag = res.hcnt + KPIPE * 2 * CSET;
+        if (step_kernel) {
+            hipLaunchKernelGGL(k_step_end, dim3(1), dim3(64), 0, st, ws.cnt, q, dcnt + 2 * CSET * kq,
+                               dcnt + KPIPE * 2 * CSET);
+        } else {
+            NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt + 2 * CSET * kq, ws.cnt, 2 * CSET * sizeof(int),
+                                          hipMemcpyDeviceToHost, st));
+        }
         cur ^= 1;
         init_step = false;
         if (kq != kpipe - 1) continue;
-        int* hflag = res.hcnt + KPIPE * 2 * CSET;
-        NLOT_HIP_CHECK(hipMemcpyAsync(hflag, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        if (!step_kernel)
+            NLOT_HIP_CHECK(hipMemcpyAsync(hflag, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
         if (hflag[1] != 0) {  // k_admit found fewer free slots than the host asked for: fail now, not at the end
             set_error("nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)");
@@ -5608,7 +5655,7 @@ extern "C" int32_t nlot_solve_batch(const NlotProblem* p, const NlotSolverOption
     return NLOT_ERR_INVALID;
 }
 
-extern "C" void nlot_set_timing(int32_t en) { nlot::g_timing = en != 0; }
+extern "C" void nlot_set_timing(int32_t every) { nlot::g_timing = every > 0 ? every : 0; }
 extern "C" void nlot_last_stats(NlotSolveStats* out) {
     if (out) *out = nlot::g_stats;
 }

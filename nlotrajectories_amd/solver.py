@@ -64,8 +64,10 @@ def workspace_bytes(problem: Problem, B: int, slots: int = 0) -> int:
     return int(lib().nlot_solve_workspace_size_slots(C.byref(problem.to_c()), B, slots))
 
 
-def set_timing(enabled: bool):
-    lib().nlot_set_timing(1 if enabled else 0)
+def set_timing(every):
+    """hipEvent timing inside nlot_solve_batch: False / 0 off, True / 1 every global step, k > 1 one step in k
+    (NlotSolveStats.timed_* count the timed steps and their work; include/nlot.h)."""
+    lib().nlot_set_timing(int(every))
 
 
 def last_stats() -> dict:

@@ -56,6 +56,10 @@ def run(B, G, slots, outdir):
     solve_batch(METRIC_PROBLEM, x0[:256], xg[:256], mlp=mlp, options=_abi.gpu_options())
     torch.cuda.synchronize()
     os.environ["NLOT_STEP_LOG"] = log  # read once, at the first logged solve
+    if os.environ.get("STEP_TIMING") == "1":  # hipEvent timing of the MLP / iterate / k_ric launches, as bench.py's timed steps
+        from nlotrajectories_amd.solver import set_timing
+
+        set_timing(True)
     import time
     t = time.perf_counter()
     r = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)

@@ -6,11 +6,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def dmlp(artefact):
+@pytest.fixture(scope="module", params=["split_bf16", "f32"])
+def dmlp(artefact, request):
+    """The artefact net with each MFMA arithmetic (include/nlot.h NLOT_MLP_ARITH_*; the parity tests run both)."""
     from nlotrajectories_amd.ops import DeviceMlp
 
-    return DeviceMlp(artefact)
+    return DeviceMlp(artefact, request.param)
 
 
 def test_mlp_matches_reference_golden(dmlp, golden):
@@ -53,9 +54,9 @@ def test_mlp_matches_oracle_and_value_path(dmlp, artefact):
 
 
 def test_split_bf16_is_fp32_equivalent(dmlp, golden, artefact):
-    """The 2-128-128-1 kernels run the hidden GEMM as six split-bf16 MFMA products.
-    Their error against the fp64 truth must be no larger than an fp32 evaluation's: at most twice the
-    oracle's (plain fp32 FMA chain) error plus one fp32 ulp of max|f|, for f and for grad f."""
+    """The 2-128-128-1 kernels run the hidden GEMM as six split-bf16 MFMA products, or as f32 MFMA
+    products (NLOT_MLP_ARITH_F32).  Their error against the fp64 truth must be no larger than an fp32 evaluation's: at
+    most twice the oracle's (plain fp32 FMA chain) error plus one fp32 ulp of max|f|, for f and for grad f."""
     import oracle as O
     from nlotrajectories_amd.ops import sdf_mlp_eval
 
