@@ -19,7 +19,8 @@ CLASSES = (  # (class, substrings of the kernel name: all must occur); first mat
     ("iter_a", "k_iter_a"), ("iter_b", "k_iter_b"), ("accept", "k_accept"), ("resto_a", "k_resto_a"),
     ("resto_b", "k_resto_b"), ("resto_ls", "k_resto_ls"), ("points", "k_points"),
     ("mlp_full", "mlp_bf16<128, true"), ("mlp_value", "mlp_bf16<128, false"), ("mlp_full", "mlp_kernel<128, 1, true>"),
-    ("mlp_value", "mlp_kernel<128, 1, false>"), ("admit", "k_admit"), ("init", "k_init_state"))
+    ("mlp_value", "mlp_kernel<128, 1, false>"), ("admit", "k_admit"), ("init", "k_init_state"),
+    ("step_end", "k_step_end"), ("copy", "copyBuffer"), ("fill", "fillBuffer"))
 
 
 def cls(name):
