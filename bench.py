@@ -352,6 +352,23 @@ def main():
     v_avg_ms = agg["mlp_value_ms"] / n_v
     v_achieved = agg["timed_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
 
+    def rocprof_avg(name):
+        """The kernel's average dispatch duration in the committed rocprofv3 --kernel-trace --stats run of the driver's
+        command (the event brackets above run from the previous launch's end, so they also hold the queue's packet
+        processing and the wait for CUs the side streams hold)."""
+        import csv
+
+        path = os.path.join(ROOT, "profiles", "r05", "kernel_stats_r05ao_K20_W5.csv")
+        if not os.path.exists(path):
+            return None
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if name in row["Name"]:
+                    ms = float(row["AverageNs"]) / 1e6
+                    return {"avg_launch_ms": ms, "calls": int(row["Calls"]), "source": os.path.relpath(path, ROOT),
+                            "frac_at_this_avg": ric_solves_per_launch * ric_bytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+        return None
+
     cpu = cpu_box.get("r")
     if cpu_here and cpu is None:
         print("[bench] CPU baseline (oracle) ...", file=sys.stderr, flush=True)
@@ -393,6 +410,7 @@ def main():
                                     "above use the design bytes of the stage layouts"},
             "solves_per_launch": ric_solves_per_launch,
             "avg_launch_ms": ric_avg_ms,
+            "rocprof": rocprof_avg("k_ric<3, false, false>") if not (stress or b6) else None,
             "launches": agg["ric_launches"],
             "timed_launches": agg["timed_steps"],
             "side_stream_solves": {"second_order_corrections": agg["ric_soc_solves"],
@@ -458,7 +476,7 @@ def main():
         # per-dispatch fractions from the profiler (the event brackets above include the streams' overlap): committed
         # from a rocprofv3 --kernel-trace --stats run of this command (scripts/rocprof_fracs.py)
         df = next((d for d in (os.path.join(ROOT, "profiles", "r05", f"mlp_dispatch_fracs_{t}.json")
-                               for t in ("r05u", "r05c")) if os.path.exists(d)), "")
+                               for t in ("r05ao", "r05u", "r05c")) if os.path.exists(d)), "")
         if os.path.exists(df) and not (stress or b6):
             with open(df) as fh:
                 dd = json.load(fh)

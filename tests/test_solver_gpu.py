@@ -269,6 +269,7 @@ def test_continuous_batching_same_results(artefact, case):
     {"NLOT_SOC_FORK": "1"}, {"NLOT_SOC_FORK": "2"},          # correction chain forked at the step start / after the MLP
     {"NLOT_EARLY_VALUE": "0"},                               # no early value launch (default on since round 4)
     {"NLOT_SPEC_THRESHOLD": "100000", "NLOT_SPEC_BULK": "4"},
+    {"NLOT_STEP_KERNEL": "0"},                               # counter copies as D2H / fill / D2D instead of k_step_end
 ])
 def test_scheduling_knobs_same_results(artefact, knobs, monkeypatch):
     """The solver's scheduling (attempt cap per launch, stream layout, speculation) changes when an instance's work
@@ -290,3 +291,40 @@ def test_scheduling_knobs_same_results(artefact, knobs, monkeypatch):
     rb = solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt)
     for k in ("status", "iters", "cost", "X", "U", "S"):
         assert torch.equal(ra[k], rb[k]), (knobs, k)
+
+
+def test_sampled_timing_stats(artefact):
+    """nlot_set_timing(k) (ABI v14): the per-launch event sums cover one global step in k, NlotSolveStats.timed_* count
+    those steps and their work; every step (k = 1) times everything; timing never changes the results."""
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import METRIC_PROBLEM
+    from nlotrajectories_amd.sampling import sample_start_goal
+    from nlotrajectories_amd.solver import last_stats, set_timing, solve_batch
+
+    mlp = DeviceMlp(artefact)
+    tm = artefact.torch_module()
+    sdf = lambda P: tm(torch.tensor(np.asarray(P), dtype=torch.float32)).detach().numpy()[:, 0]
+    x0, xg = sample_start_goal(METRIC_PROBLEM, 64, seed=6, sdf=sdf)
+    opt = _abi.gpu_options(max_iter=200, max_active=32)
+    runs = {}
+    try:
+        for k in (0, 1, 4):
+            set_timing(k)
+            runs[k] = (solve_batch(METRIC_PROBLEM, x0, xg, mlp=mlp, options=opt), last_stats())
+    finally:
+        set_timing(0)
+    for k in (1, 4):
+        for f in ("status", "iters", "cost", "X", "U"):
+            assert torch.equal(runs[0][0][f], runs[k][0][f]), (k, f)
+    s0, s1, s4 = runs[0][1], runs[1][1], runs[4][1]
+    assert s0["timed_steps"] == 0 and s0["mlp_full_ms"] == 0
+    assert s1["timing_every"] == 1 and s1["timed_steps"] == s1["iterations"]
+    for f in ("points_full", "points_full_reused", "points_value"):
+        assert s1[f"timed_{f}"] == s1[f"mlp_{f}"], f
+    assert s1["timed_ric_solves"] == s1["ric_solves"]
+    n = s4["iterations"]
+    want = sum(1 for s in range(n) if s % 4 == (s // 4) % 4)
+    assert s4["timing_every"] == 4 and s4["timed_steps"] == want, (s4["timed_steps"], want, n)
+    assert 0 < s4["timed_points_full"] < s4["mlp_points_full"] and 0 < s4["timed_points_value"] < s4["mlp_points_value"]
+    assert s4["mlp_full_ms"] > 0 and s4["mlp_value_ms"] > 0 and s4["ric_ms"] > 0 and s4["iterate_ms"] > 0
