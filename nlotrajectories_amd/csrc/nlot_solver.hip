@@ -1892,7 +1892,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     double dw = fixed ? fixdw : 0.0, dw_in_hg = dw;
     // an inertia correction this instance started in an earlier launch (the attempt cap deferred it): hg holds
     // dw_in_hg, the next delta_w of IPOPT's sequence is dw (the same sequence as in one launch)
-    const bool resume = !SOC && !RESTO && mode == MODE_NEWTON && !fixed && SC(SC_RETRY) >= 0.0;
+    const bool resume = !SOC && mode == MODE_NEWTON && !fixed && SC(SC_RETRY) >= 0.0;
     if (resume) {
         dw = SC(SC_RETRY);
         dw_in_hg = SC(SC_DWHG);
@@ -1931,9 +1931,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         if (!fail || mode != MODE_NEWTON || fixed) break;
         dw = dw == 0.0 ? (last_dw == 0.0 ? 1e-4 : fmax(1e-20, last_dw / 3.0)) : dw * (last_dw == 0.0 ? 100.0 : 8.0);
         if (dw > 1e40) break;
-        // attempt cap (not RESTO): a wrong inertia after max_tries factorisations in this launch continues in the
-        // next global step's launch, so one instance's long delta_w sequence does not hold the whole launch
-        if (!RESTO && n_tries >= max_tries && (int)SC(SC_PHASE) == PH_EVAL) {
+        // attempt cap: a wrong inertia after max_tries factorisations in this launch continues in the next global
+        // step's launch, so one instance's long delta_w sequence does not hold the whole launch (restoration solves
+        // too: their chain joins the main stream before the second value launch)
+        if (n_tries >= max_tries && (int)SC(SC_PHASE) == PH_EVAL) {
             deferred = true;
             break;
         }
@@ -1947,7 +1948,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
         if (n_tries > 1) atomicAdd(diag + 2, 1);
     }
     if (diag && l == 0 && RESTO) atomicMax(diag, n_tries);  // restoration solves: most factorisations (CSET [15])
-    if (deferred) {  // SC_RIC stays 1: k_iter_b and k_accept pass the instance by, k_iter_a lists it again
+    if (deferred) {  // SC_RIC stays 1: k_iter_b (k_resto_b) and k_accept pass the instance by, k_iter_a lists it
+                     // again (k_resto_a keeps its stages)
         if (l == 0) {
             SC(SC_RETRY) = dw;
             SC(SC_DWHG) = dw_in_hg;
@@ -4276,6 +4278,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RA)
     if (SC(SC_RESTO) == 0.0) return;
     const int ph = (int)SC(SC_PHASE);
     if (ph != PH_RINIT && ph != PH_EVAL) return;
+    // k_ric<DYN, true>'s inertia correction continues (attempt cap): the stages and the delta_w state are kept
+    if (ph == PH_EVAL && SC(SC_RETRY) >= 0.0) return;
     const bool init = ph == PH_RINIT;
     const int N = dm.N, M = dm.M, nc = dm.nc, rank = (int)SC(SC_RANK);
     const int rt = NX + N * NX, rq = rt + nc, rb = rq + (N + 1) * M, ne = RS::n_rows(dm), ngb = ne - rb;
@@ -5253,6 +5257,9 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     int ric_tries = 1, ric_tries_min = 2048;
     if (const char* e = getenv("NLOT_RIC_TRIES")) ric_tries = std::max(1, atoi(e));
     if (const char* e = getenv("NLOT_RIC_TRIES_MIN")) ric_tries_min = atoi(e);
+    // the same cap for the restoration solves (side stream; NLOT_RESTO_TRIES=0: every attempt in one launch)
+    bool resto_tries = true;
+    if (const char* e = getenv("NLOT_RESTO_TRIES")) resto_tries = atoi(e) != 0;
     double progress_s = 0, t_prog = 0;
     if (const char* e = getenv("NLOT_PROGRESS")) progress_s = atof(e);
     t_prog = progress_s;
@@ -5433,7 +5440,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
             NLOT_HIP_CHECK(hipStreamWaitEvent(s3, res.e_a, 0));
             hipLaunchKernelGGL(k_resto_a<DYN>, dim3(n_resto), dim3(64), 0, s3, dP, dD, o, dW, actr, ws.x0s, ws.xgs, C);
             hipLaunchKernelGGL((k_ric<DYN, true>), dim3((n_resto + ric_blocks_per - 1) / ric_blocks_per), dim3(64), 0, s3,
-                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON, C + 15, 1 << 30);
+                               dP, dD, dW, actr, n_resto, C + 5, (int)MODE_NEWTON, C + 15,
+                               resto_tries && n_active > ric_tries_min ? ric_tries : 1 << 30);
             hipLaunchKernelGGL(k_resto_b<DYN>, dim3(n_resto), dim3(64), 0, s3, dP, dD, o, dW, actr, C,
                                use_mlp ? ws.tpts[q] : nullptr);
             NLOT_HIP_CHECK(hipEventRecord(res.e_r, s3));

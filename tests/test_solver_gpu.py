@@ -266,6 +266,7 @@ def test_continuous_batching_same_results(artefact, case):
 
 @pytest.mark.parametrize("knobs", [
     {"NLOT_RIC_TRIES": "1", "NLOT_RIC_TRIES_MIN": "0"},     # every wrong inertia continues in the next step
+    {"NLOT_RIC_TRIES": "1", "NLOT_RIC_TRIES_MIN": "0", "NLOT_RESTO_TRIES": "0"},  # restoration solves not capped
     {"NLOT_SOC_FORK": "1"}, {"NLOT_SOC_FORK": "2"},          # correction chain forked at the step start / after the MLP
     {"NLOT_EARLY_VALUE": "0"},                               # no early value launch (default on since round 4)
     {"NLOT_SPEC_THRESHOLD": "100000", "NLOT_SPEC_BULK": "4"},
