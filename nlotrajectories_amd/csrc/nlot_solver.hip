@@ -1155,9 +1155,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     __shared__ typename R::Sh shg[R::IPW];
     __shared__ __attribute__((aligned(16))) double ring[RING][NDMA][R::IPW][DW];  // DMA'd stage inputs
     const int grp = threadIdx.x / G, l = threadIdx.x % G, gb = grp * G;
-    // RESTO: grid-stride over the restoration list (the host sizes the grid by a stale bound); else one instance
-    // per group
-    const int nlist = std::min(n_active, *nact);
+    // RESTO: grid-stride over the whole restoration list (the host sizes the grid by a stale bound, which the list can
+    // outgrow within a synchronisation window; an instance left out would repeat k_resto_a's evaluation, whose
+    // barrier update is not idempotent); else one instance per group, at most the grid's
+    const int nlist = RESTO ? *nact : std::min(n_active, *nact);
     auto body = [&](const int si) {
     const int b = active[si];
     if ((int)SC(SC_RIC) != 1) return;
