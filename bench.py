@@ -89,6 +89,10 @@ def parse():
                          "workspace holds the slots' state only, ABI v10)")
     ap.add_argument("--mu-strategy", choices=["adaptive", "monotone"], default="adaptive",
                     help="adaptive = the reference's IPOPT setting (runner.py:118-120)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="the multi-rank plumbing alone (self-launch, rank / world, process group, the rank-seeded shards "
+                         "gathered to rank 0 in rank order), no solve: tests/test_bench_launch.py runs it on the CPU "
+                         "under NLOT_DIST_BACKEND=gloo")
     ap.add_argument("--bounds", choices=["rows", "variable"], default="rows",
                     help="rows = the reference's NLP: the control bounds and slack >= 0 as constraint rows, the form "
                          "CasADi's Opti hands IPOPT (runner.py:67-69,101-103; NlotSolverOptions.general_bounds = 1); "
@@ -139,20 +143,86 @@ def ric_bytes_per_solve(prob, nr=2):
     return 8 * (prob.N + 1) * per_knot
 
 
+def self_launch(n, argv):
+    """`--gpus N` (N > 1) with no launcher around this process (WORLD_SIZE unset): start N ranks on this node, one
+    process per GPU, with torch.distributed.run (the driver's own form of the command, rendezvous on 127.0.0.1) as a
+    child process, and return its exit code.  Called before anything in this process touches the GPU: the ranks are
+    children, never an exec of this process."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ, NLOT_BENCH_SELF_LAUNCHED="1"))
+
+
+def draw_b6(batch, seed, rank):
+    """benchmark 6's start / goal, xy + U[-0.05, 0.05]^2, seeded per batch and rank."""
+    rng = np.random.default_rng(seed + 1000003 * rank)
+    x0 = np.repeat(np.array([BENCHMARKS["b6"]["start"]], float), batch, 0)
+    xg = np.repeat(np.array([BENCHMARKS["b6"]["goal"]], float), batch, 0)
+    x0[:, :2] += rng.uniform(-0.05, 0.05, (batch, 2))
+    xg[:, :2] += rng.uniform(-0.05, 0.05, (batch, 2))
+    return x0, xg
+
+
+def launch_check(a, rank, local, world, backend):
+    """--launch-check: what a multi-rank bench run does besides solving.  Each rank draws its own seeded shard (the b6
+    rule: no SDF needed), the shards are gathered to rank 0 with the bench's collective (gather_solutions), and rank 0
+    prints one JSON line: the ranks the process group initialised, the backend, and the gathered shards."""
+    t_dev = "cpu"
+    if world > 1 and backend == "nccl":  # RCCL gathers device tensors: one GPU per rank
+        torch.cuda.set_device(local)
+        t_dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=t_dev)
+    elif world > 1:
+        dist.init_process_group(backend)
+    x0, _ = draw_b6(a.batch or 2, a.seed, rank)
+    g = gather_solutions({"x0": torch.as_tensor(x0, device=t_dev)}, keys=("x0",))
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "process_group_world_size": pg_world, "backend": backend if world > 1 else None,
+                          "self_launched": os.environ.get("NLOT_BENCH_SELF_LAUNCHED") == "1",
+                          "x0": g["x0"].cpu().tolist()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(self_launch(a.gpus, sys.argv[1:]))
     rank, local, world = rank_world()
+    if world != a.gpus:  # the line's n_gpus is the ranks that ran: a mismatch is an error, not a relabelling
+        print(f"[bench] --gpus {a.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)", file=sys.stderr, flush=True)
+        sys.exit(2)
     # NLOT_DIST_BACKEND=gloo: a rehearsal of the multi-rank path with several ranks sharing the visible GPUs
     # (local rank modulo the device count; CPU collectives); the driver's multi-GPU runs use RCCL ("nccl")
     backend = os.environ.get("NLOT_DIST_BACKEND", "nccl")
+    if a.launch_check:
+        return launch_check(a, rank, local, world, backend)
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
     if backend != "nccl":
-        local = local % torch.cuda.device_count()
+        local = local % max(ndev, 1)
+    elif world > 1 and world > ndev:
+        print(f"[bench] {world} ranks over RCCL need {world} GPUs; {ndev} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    pg = {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
+          "backend": dist.get_backend() if dist.is_initialized() else None,
+          "launcher": "bench.py --gpus (torch.distributed.run child)" if os.environ.get("NLOT_BENCH_SELF_LAUNCHED") == "1"
+          else "torch.distributed.run" if world > 1 else "single process"}
+    assert pg["world_size"] == world == a.gpus, pg
     dev = torch.device("cuda", local)
     stress, b6 = a.workload == "stress", a.workload == "b6"
     if a.batch is None:
@@ -176,11 +246,7 @@ def main():
 
     def draw(k):  # batch k (warm-up batches first, then the timed ones): a distinct seeded draw per batch and rank
         if b6:  # benchmark 6's start / goal, xy +- U[-0.05, 0.05]^2
-            rng = np.random.default_rng(a.seed + k + 1000003 * rank)
-            x0 = np.repeat(np.array([BENCHMARKS["b6"]["start"]], float), a.batch, 0)
-            xg = np.repeat(np.array([BENCHMARKS["b6"]["goal"]], float), a.batch, 0)
-            x0[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
-            xg[:, :2] += rng.uniform(-0.05, 0.05, (a.batch, 2))
+            x0, xg = draw_b6(a.batch, a.seed + k, rank)
         else:  # start/goal uniform in [-0.3, 1.3]^2, all corners sdf >= 0.02
             x0, xg = sample_start_goal(prob, a.batch, seed=a.seed + k, sdf=sdf_gpu, rank=rank)
         return (torch.tensor(x0, dtype=torch.float64, device=dev), torch.tensor(xg, dtype=torch.float64, device=dev))
@@ -328,9 +394,8 @@ def main():
     # PMC at bench size (B = 65536): scripts/pmc_traffic.sh + scripts/pmc_traffic.py -> profiles/r05/ (the newest
     # round's file that exists)
     tf = next((t for t in (os.path.join(ROOT, "profiles", r, f) for r, f in
-                           (("r05", "pmc_traffic_r05u_B65536.json"), ("r05", "pmc_traffic_r05_B65536.json"),
-                            ("r04", "pmc_traffic_r04_B65536.json"),
-                            ("r03", "pmc_traffic_r03m_B65536.json"))) if os.path.exists(t)), "")
+                           (("r06", "pmc_traffic_r06_B65536.json"), ("r05", "pmc_traffic_r05u_B65536.json"))
+                           ) if os.path.exists(t)), "")
     pmc = None
     if os.path.exists(tf):
         with open(tf) as f:
@@ -352,21 +417,25 @@ def main():
     v_avg_ms = agg["mlp_value_ms"] / n_v
     v_achieved = agg["timed_points_value"] / n_v * flop_fwd / (v_avg_ms * 1e-3) / 1e12 if v_avg_ms > 0 else 0.0
 
+    def committed(path, **fields):
+        """A figure read from a committed profile (not measured by this run): tagged with its file."""
+        return dict(fields, source=os.path.relpath(path, ROOT), measured_in_this_run=False)
+
     def rocprof_avg(name):
         """The kernel's average dispatch duration in the committed rocprofv3 --kernel-trace --stats run of the driver's
-        command (the event brackets above run from the previous launch's end, so they also hold the queue's packet
-        processing and the wait for CUs the side streams hold)."""
+        command (the event brackets of this run start at the previous launch's end, so they also hold the queue's packet
+        processing and the wait for CUs the side streams hold).  Committed, not this run's."""
         import csv
 
-        path = os.path.join(ROOT, "profiles", "r05", "kernel_stats_r05ao_K20_W5.csv")
+        path = os.path.join(ROOT, "profiles", "r06", "kernel_stats_r06_K20_W5.csv")
+        if not os.path.exists(path):
+            path = os.path.join(ROOT, "profiles", "r05", "kernel_stats_r05ao_K20_W5.csv")
         if not os.path.exists(path):
             return None
         with open(path) as fh:
             for row in csv.DictReader(fh):
                 if name in row["Name"]:
-                    ms = float(row["AverageNs"]) / 1e6
-                    return {"avg_launch_ms": ms, "calls": int(row["Calls"]), "source": os.path.relpath(path, ROOT),
-                            "frac_at_this_avg": ric_solves_per_launch * ric_bytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+                    return committed(path, avg_launch_ms=float(row["AverageNs"]) / 1e6, calls=int(row["Calls"]))
         return None
 
     cpu = cpu_box.get("r")
@@ -399,15 +468,19 @@ def main():
         ric = {
             "kernel": "k_ric (lane-group Riccati Newton solve, fp64)",
             "bound": "hbm",
-            "achieved": ric_achieved,
+            # SURVEY.md §8d's algorithmic bytes per problem-iteration (2 * 4 * (nvar + ncon): read + write the
+            # primal-dual iterate) x the solves of one launch / this run's event-timed launch average
+            "achieved": ric_alg,
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",
-            "frac": ric_achieved / PEAK_HBM_GBS,
+            "frac": ric_alg / PEAK_HBM_GBS,
             "traffic": ric_traffic if not stress else None,
-            "bytes_per_solve": ric_bytes,
-            "algorithmic": {"bytes_per_solve": alg_bytes, "achieved": ric_alg, "frac": ric_alg / PEAK_HBM_GBS,
-                            "note": "SURVEY.md §8d: 2 * 4 * (nvar + ncon) bytes per problem-iteration; achieved and frac "
-                                    "above use the design bytes of the stage layouts"},
+            "algorithmic_bytes_per_solve": alg_bytes,
+            "basis": "SURVEY.md §8d algorithmic bytes (2 * 4 * (nvar + ncon) per problem-iteration) per launch / the "
+                     "event-timed average launch (hipEvents on the solver's stream, this run)",
+            "design_bytes": {"bytes_per_solve": ric_bytes, "achieved": ric_achieved, "frac": ric_achieved / PEAK_HBM_GBS,
+                             "note": "the stage layouts k_ric reads and writes (bench.ric_bytes_per_solve, DESIGN.md §7: "
+                                     "H, g, A, B, c, M in; gains and value function out and back; 2 right-hand sides)"},
             "solves_per_launch": ric_solves_per_launch,
             "avg_launch_ms": ric_avg_ms,
             "rocprof": rocprof_avg("k_ric<3, false, false>") if not (stress or b6) else None,
@@ -416,15 +489,14 @@ def main():
             "side_stream_solves": {"second_order_corrections": agg["ric_soc_solves"],
                                    "restoration": agg["ric_resto_solves"],
                                    "factorisations_main": agg["ric_solves"]},
-            "note": "algorithmic bytes per instance solve from the stage layouts (bench.ric_bytes_per_solve, "
-                    "2 right-hand sides); the kernel is fp64-latency/occupancy-bound, HBM is its roofline.  The "
-                    "second-order corrections (substitution with the stored factors, k_ric<DYN, false, true>) and the "
-                    "restoration solves run on a side stream and are not counted in this launch's solves",
-            "pmc_note": (f"traffic = HBM bytes per solve from {os.path.relpath(tf, ROOT)} (FETCH_SIZE x2 + WRITE_SIZE "
-                         f"at B = 65536: {pmc['k_ric']['ratio_to_algorithmic']:.2f}x the algorithmic bytes) x solves per "
-                         "launch; phase timers (profiles/r03/kric_phase_timers_r03n.log): one solve takes ~160 us alone, "
-                         "~400 us at B = 65536 (the forward sweep's memory passes 4x slower under load)")
-                        if pmc else "no PMC traffic file",
+            "note": "the kernel is fp64-latency/occupancy-bound; HBM is its roofline.  The second-order corrections "
+                    "(substitution with the stored factors, k_ric<DYN, false, true>) and the restoration solves run on "
+                    "side streams and are not counted in this launch's solves",
+            "traffic_source": (committed(tf, hbm_bytes_per_solve=pmc["k_ric"]["hbm_bytes_per_solve"],
+                                         ratio_to_design_bytes=pmc["k_ric"]["ratio_to_algorithmic"],
+                                         note="PMC FETCH_SIZE x2 + WRITE_SIZE at B = 65536 (scripts/pmc_traffic.sh); "
+                                              "traffic = that x this run's solves per launch")
+                               if pmc else "no PMC traffic file"),
         }
         mlp_full = {
             "kernel": kname % "full" + ": SDF-MLP value + gradient + Hessian",
@@ -445,12 +517,11 @@ def main():
             "avg_launch_ms": avg_ms,
             "launches": agg["mlp_full_launches"],
             "timed_launches": agg["timed_steps"],
-            "traffic_note": (f"HBM bytes per point in the solve at B = 65536 ({os.path.relpath(tf, ROOT)}): "
-                             f"{pmc['mlp_full']['hbm_bytes_per_point']:.1f} B/point = "
-                             f"{pmc['mlp_full']['ratio_to_algorithmic_with_reuse']:.2f}x the algorithmic "
-                             f"{pmc['mlp_full']['algorithmic_bytes_per_point_with_reuse']:.1f} B/point with forward reuse "
-                             "(coordinates, the trial's coordinates, value and ReLU pattern in; value + gradient + "
-                             "Hessian out)") if pmc else "no PMC traffic file",
+            "traffic_source": (committed(tf, hbm_bytes_per_point=pmc["mlp_full"]["hbm_bytes_per_point"],
+                                         ratio_to_algorithmic_with_reuse=pmc["mlp_full"]["ratio_to_algorithmic_with_reuse"],
+                                         note="PMC in the solve at B = 65536; traffic = that x this run's points per "
+                                              "launch (coordinates, the trial's coordinates, value and ReLU pattern in; "
+                                              "value + gradient + Hessian out)") if pmc else "no PMC traffic file"),
         }
         mlp_value = {
             "kernel": kname % "value" + ": line-search trial points, value only",
@@ -475,16 +546,16 @@ def main():
                                         "step's candidates (fourth stream); its event-timed duration includes that")
         # per-dispatch fractions from the profiler (the event brackets above include the streams' overlap): committed
         # from a rocprofv3 --kernel-trace --stats run of this command (scripts/rocprof_fracs.py)
-        df = next((d for d in (os.path.join(ROOT, "profiles", "r05", f"mlp_dispatch_fracs_{t}.json")
-                               for t in ("r05ao", "r05u", "r05c")) if os.path.exists(d)), "")
+        df = next((d for d in (os.path.join(ROOT, "profiles", r, f"mlp_dispatch_fracs_{t}.json")
+                               for r, t in (("r06", "r06"), ("r05", "r05ao"))) if os.path.exists(d)), "")
         if os.path.exists(df) and not (stress or b6):
             with open(df) as fh:
                 dd = json.load(fh)
             src = os.path.relpath(df, ROOT)
-            mlp_full["rocprof_dispatch_frac"] = {"frac": dd["full"]["frac"], "avg_dispatch_ms": dd["full"]["avg_dispatch_ms"],
-                                                 "source": src}
-            mlp_value["rocprof_dispatch_frac"] = {"frac": dd["value"]["frac"], "avg_step_ms": dd["value"]["avg_step_ms"],
-                                                  "source": src}
+            mlp_full["rocprof_dispatch_frac"] = committed(df, frac=dd["full"]["frac"],
+                                                          avg_dispatch_ms=dd["full"]["avg_dispatch_ms"])
+            mlp_value["rocprof_dispatch_frac"] = committed(df, frac=dd["value"]["frac"],
+                                                           avg_step_ms=dd["value"]["avg_step_ms"])
         # the dominant kernel by device time: k_ric on the metric workload, the SDF-MLP on the stress workload
         if stress:
             rooflines = {"roofline": mlp_full, "roofline_mlp_value": mlp_value, "roofline_ric": ric}
@@ -528,6 +599,7 @@ def main():
                 "global_batch": B_all,
                 "knots": prob.N + 1,
                 "parallelism": f"instances sharded over {world} GPU(s); RCCL gather of solutions to rank 0",
+                "process_group": pg,
                 "scheduling": (f"continuous batching: the {a.steps} timed batches of {a.batch} instances in "
                                f"{len(calls)} solve call(s) through {slots} concurrent slots (NlotSolverOptions.max_active; "
                                "slot-indexed state, a finished instance's slot goes to the next one); each instance runs "
@@ -566,15 +638,6 @@ def main():
             **rooflines,
             "cpu_baseline": cpu,
         }
-        if opt.general_bounds and not (stress or b6):  # the variable-bound form's figures, measured on the same tree
-            vf = os.path.join(ROOT, "profiles", "r05", "bench_varbounds_r05ab.json")
-            if os.path.exists(vf):
-                with open(vf) as f:
-                    v = json.load(f)
-                line["config"]["variable_bounds_reference"] = {
-                    "value": v["value"], "status_counts_rank0": v["config"]["status_counts_rank0"],
-                    "mean_iters_solved": v["config"]["mean_iters_solved"], "source": os.path.relpath(vf, ROOT),
-                    "note": "the same command with --bounds variable (committed measurement, not this run)"}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

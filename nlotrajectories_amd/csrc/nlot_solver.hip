@@ -360,6 +360,27 @@ static Ws carve(const Dims& d, int64_t B, bool mlp, void* base) {
         }                                                                          \
         off += n_;                                                                 \
     }
+// Host grid bounds ("lists and their grid bounds").  The phase kernels' grids are the host's last known
+// active count and the Newton / correction solves' grids that count over the group size: upper bounds of the device's
+// counts (the active set only shrinks between admissions, and a solve list is a subset of it).  Should a device count
+// ever exceed its grid, the instances past it would skip their step silently; block 0 checks, sets the error flag
+// cnt[2 CSET + 1] to `code` (GRID_*), and the host fails the call at its next synchronisation.  The restoration kernels
+// do not need it: they stride over their exact list count (the host's bound for them is a heuristic).
+enum { GRID_ADMIT = 1, GRID_ACTIVE = 2, GRID_SOLVE = 3 };
+__device__ __forceinline__ void grid_guard(const Ws& ws, int count, int per_block, int code) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && count > (int)gridDim.x * per_block) ws.cnt[2 * CSET + 1] = code;
+}
+
+// the host's message for the error flag cnt[2 CSET + 1] (grid_guard codes)
+static const char* grid_error(int code) {
+    switch (code) {
+    case GRID_ADMIT: return "nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)";
+    case GRID_ACTIVE: return "nlot_solve_batch: an active list outgrew its launch grid (host bound below the device count)";
+    case GRID_SOLVE: return "nlot_solve_batch: a solve list outgrew its launch grid (host bound below the device count)";
+    default: return "nlot_solve_batch: unknown device error flag";
+    }
+}
+
 __device__ inline void iter_io(const Ws& ws, int64_t b, int lane, double* buf, bool save) {
     int off = 0;
     NLOT_ITER_ARRAYS(NLOT_IO)
@@ -1159,6 +1180,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RicWpe<DYN, 
     // outgrow within a synchronisation window; an instance left out would repeat k_resto_a's evaluation, whose
     // barrier update is not idempotent); else one instance per group, at most the grid's
     const int nlist = RESTO ? *nact : std::min(n_active, *nact);
+    if constexpr (!RESTO) grid_guard(ws, *nact, R::IPW, GRID_SOLVE);
     auto body = [&](const int si) {
     const int b = active[si];
     if ((int)SC(SC_RIC) != 1) return;
@@ -2375,7 +2397,7 @@ static __global__ __launch_bounds__(1024) void k_admit(int* __restrict__ act, in
                                                         int n) {
     const int base = cnt[2], nf = gcnt[0];
     if (nf < n) {
-        if (threadIdx.x == 0) gcnt[1] = 1;
+        if (threadIdx.x == 0) gcnt[1] = GRID_ADMIT;
         n = nf;
     }
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
@@ -2453,8 +2475,9 @@ __device__ void emit_points(const NlotProblem& p, const Dims& dm, const Ws& ws, 
 // first global step: the corners of every instance (phase INIT)
 static __global__ __launch_bounds__(64) void k_points(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_,
                                                const Ws* __restrict__ ws_, const int* __restrict__ active, int* cnt) {
-    if ((int)blockIdx.x >= cnt[2]) return;  // the host's count may exceed the device's (k_admit shortfall)
     const Ws& ws = *ws_;
+    grid_guard(ws, cnt[2], 1, GRID_ACTIVE);
+    if ((int)blockIdx.x >= cnt[2]) return;  // the host's count may exceed the device's (k_admit shortfall)
     const int b = active[blockIdx.x];
     if ((int)SC(SC_PHASE) != PH_INIT) return;
     emit_points(*pp_, *dd_, ws, b, threadIdx.x, cnt, false, nullptr, 1, 0.0);
@@ -2634,6 +2657,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
                                                const int* __restrict__ active, const double* __restrict__ x0,
                                                const double* __restrict__ xg, int pass, int* cnt, int* cnt_next) {
     const bool init_pass = pass == PASS_INIT;
+    grid_guard(*ws_, cnt[2], 1, GRID_ACTIVE);
     if ((int)blockIdx.x >= cnt[2]) return;  // grid sized by a stale (larger) host count: steps run ahead of the host
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -3185,6 +3209,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_A))
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_B))) void k_iter_b(const NlotProblem* __restrict__ pp_, const Dims* __restrict__ dd_, NlotSolverOptions o, const Ws* __restrict__ ws_,
                                                const int* __restrict__ active, int* cnt, float* tp, int* cnt_next) {
+    grid_guard(*ws_, cnt[2], 1, GRID_ACTIVE);
     if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -3808,6 +3833,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_ACC
                                                int* __restrict__ nextr, const double* __restrict__ x0,
                                                const double* __restrict__ xg, int* cnt, int* cnt_next, float* tp_next,
                                                const float* tval, int nspec_next) {
+    grid_guard(*ws_, cnt[2], 1, GRID_ACTIVE);
     if ((int)blockIdx.x >= cnt[2]) return;
     const NlotProblem& p = *pp_;
     const Dims& dm = *dd_;
@@ -5285,7 +5311,12 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     bool init_step = true;  // this step runs the INIT pass (step 0, and the step after an admission)
     // grid bound of the restoration kernels (they read the exact list count on the device): every active instance
     // until a synchronisation shows how many are restoring (an instance enters at most one step before)
-    int resto_bound = o.resto ? Bi : 0;
+    // NLOT_RESTO_BOUND=n (test knob, tests/test_resto_gpu.py::test_resto_grid_bound_same_results): the bound forced to
+    // at most n, so that the restoration lists outgrow their grids and the kernels' stride over the exact count runs on
+    // every restoring step (the results must not change)
+    int resto_force = 0;
+    if (const char* e = getenv("NLOT_RESTO_BOUND")) resto_force = std::max(1, atoi(e));
+    int resto_bound = o.resto ? (resto_force ? std::min(Bi, resto_force) : Bi) : 0;
     int rc = NLOT_OK, n_active = capacity, cur = 0, synced = 0;
     int64_t step = 0;
     NLOT_HIP_CHECK(hipMemsetAsync(ws.cnt, 0, 64 * sizeof(int), st));  // both sets, the free-slot count, error flag
@@ -5502,14 +5533,15 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
         if (!step_kernel)
             NLOT_HIP_CHECK(hipMemcpyAsync(hflag, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         NLOT_HIP_CHECK(hipStreamSynchronize(st));
-        if (hflag[1] != 0) {  // k_admit found fewer free slots than the host asked for: fail now, not at the end
-            set_error("nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)");
+        if (hflag[1] != 0) {  // k_admit's shortfall or a list that outgrew its grid (grid_guard): fail now, not at the end
+            set_error(grid_error(hflag[1]));
             return NLOT_ERR_INVALID;
         }
         // restoration lists of the window: the next launches' grid bound (their kernels read the exact count)
         int rmax = 0;
         for (int j = 0; j <= kq; ++j) rmax = std::max(rmax, res.hcnt[2 * CSET * j + CSET * (((step - kq + j) & 1) ^ 1) + 5]);
         resto_bound = std::min(Bi, 2 * rmax + 256);
+        if (resto_force) resto_bound = std::min(resto_bound, resto_force);
         fold(step);
         if (progress_s > 0) {  // NLOT_PROGRESS=seconds: a line on stderr now and then (long continuous calls)
             const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_prog0).count();
@@ -5590,7 +5622,8 @@ int run(const NlotProblem& p, const NlotSolverOptions& o, const NlotMlp* mlp, co
     NLOT_HIP_CHECK(hipMemcpyAsync(res.hcnt, ws.cnt + 2 * CSET, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     NLOT_HIP_CHECK(hipStreamSynchronize(st));
     if (res.hcnt[1] != 0 || res.hcnt[0] != capacity) {
-        set_error("nlot_solve_batch: slot bookkeeping mismatch (admission found fewer free slots than expected)");
+        set_error(res.hcnt[1] != 0 ? grid_error(res.hcnt[1])
+                                   : "nlot_solve_batch: slot bookkeeping mismatch (free slots at the end != capacity)");
         return NLOT_ERR_INVALID;
     }
     return NLOT_OK;

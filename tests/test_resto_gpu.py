@@ -114,3 +114,50 @@ def test_restoration_statuses_on_metric(artefact):
     print("metric gpu", np.bincount(sg, minlength=7).tolist(), "oracle", np.bincount(so, minlength=7).tolist(), flush=True)
     assert (sg == _abi.NLOT_LS_FAILED).sum() == 0 and (so == _abi.NLOT_LS_FAILED).sum() == 0
     assert ((sg == 4) | (sg == 5)).sum() > 0 and ((so == 4) | (so == 5)).sum() > 0
+
+
+def test_resto_grid_bound_same_results(tmp_path, monkeypatch):
+    """Regression test of the restoration-list bound.  The restoration kernels' grid is a host
+    bound that the list can outgrow between synchronisations; they stride over the exact device count (k_ric<DYN, true>
+    since 4e8db73: before, an instance past the bound skipped its solve and repeated k_resto_a's non-idempotent barrier
+    update, so its arithmetic depended on the batch).  NLOT_RESTO_BOUND=1 forces the bound to one instance, so every
+    restoring step takes the stride path; with it, and with it under continuous batching in few slots, benchmark 6's
+    fixture instances (restoration-heavy: RRT starts, no slack) must give bitwise the default's statuses, iterations,
+    costs and trajectories.  The step log shows the lists really outgrew the grids."""
+    import os
+
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp
+    from nlotrajectories_amd.problem import B6_PROBLEM
+    from nlotrajectories_amd.solver import solve_batch
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    f = dict(np.load(os.path.join(here, "golden", "oracle_outcomes.npz")))
+    mlp = DeviceMlp(MlpWeights.load(os.path.join(os.path.dirname(here), "nlotrajectories_amd", "data",
+                                                 "b6_mlp128_seed0.npz")))
+    keys = ("status", "iters", "cost", "X", "U")
+
+    def run(max_active=0, bound=None):
+        opt = _abi.default_options(general_bounds=int(f["general_bounds"]), max_iter=300, max_active=max_active)
+        if bound is None:
+            monkeypatch.delenv("NLOT_RESTO_BOUND", raising=False)
+        else:
+            monkeypatch.setenv("NLOT_RESTO_BOUND", str(bound))
+        r = solve_batch(B6_PROBLEM, f["b6_x0"], f["b6_xg"], mlp=mlp, X_init=f["b6_xinit"], options=opt)
+        return {k: r[k].cpu().numpy() for k in keys}
+
+    ref = run()
+    log = tmp_path / "steps.log"
+    monkeypatch.setenv("NLOT_STEP_LOG", str(log))
+    forced = run(bound=1)
+    monkeypatch.delenv("NLOT_STEP_LOG")
+    rows = np.loadtxt(log, dtype=np.int64, ndmin=2)
+    restoring = rows[:, 7]  # counter 5 of each step: instances in the restoration phase (scripts/step_trace.py)
+    print("statuses", np.bincount(ref["status"], minlength=7).tolist(), "max restoring per step", int(restoring.max()),
+          "steps with > 4 restoring", int((restoring > 4).sum()), flush=True)
+    assert restoring.max() > 4  # past one k_resto_a wave and one k_ric block (4 groups): the stride path ran
+    few_slots = run(max_active=6, bound=1)
+    for name, r in (("NLOT_RESTO_BOUND=1", forced), ("NLOT_RESTO_BOUND=1, max_active 6", few_slots)):
+        for k in keys:
+            assert np.array_equal(ref[k], r[k]), (name, k)

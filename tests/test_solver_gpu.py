@@ -265,8 +265,12 @@ def test_continuous_batching_same_results(artefact, case):
 
 
 @pytest.mark.parametrize("knobs", [
-    {"NLOT_RIC_TRIES": "1", "NLOT_RIC_TRIES_MIN": "0"},     # every wrong inertia continues in the next step
-    {"NLOT_RIC_TRIES": "1", "NLOT_RIC_TRIES_MIN": "0", "NLOT_RESTO_TRIES": "0"},  # restoration solves not capped
+    # the default caps every k_ric launch at one delta_w attempt (a wrong inertia continues in the next step's launch);
+    # uncapped: every attempt in one launch (the default below 2048 active instances until round 5)
+    {"NLOT_RIC_TRIES_MIN": "100000000"},
+    {"NLOT_RIC_TRIES_MIN": "100000000", "NLOT_RESTO_TRIES": "0"},  # uncapped, the restoration solves too
+    {"NLOT_RESTO_TRIES": "0"},                               # capped Newton solves, uncapped restoration solves
+    {"NLOT_RESTO_BOUND": "1"},                               # restoration grids of one instance: the stride path
     {"NLOT_SOC_FORK": "1"}, {"NLOT_SOC_FORK": "2"},          # correction chain forked at the step start / after the MLP
     {"NLOT_EARLY_VALUE": "0"},                               # no early value launch (default on since round 4)
     {"NLOT_SPEC_THRESHOLD": "100000", "NLOT_SPEC_BULK": "4"},
