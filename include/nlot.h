@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NLOT_ABI_VERSION 14
+#define NLOT_ABI_VERSION 15
 
 /* ---- error codes ------------------------------------------------------------------------- */
 #define NLOT_OK 0
@@ -214,9 +214,13 @@ NlotMlp* nlot_mlp_create(const NlotMlpDesc* desc);
  * differ in the MFMA sums' order and so at the rounding level:
  *   NLOT_MLP_ARITH_SPLIT_BF16  operands split into three bf16 parts, six bf16 MFMA products per fp32 product (the
  *                              default of nlot_mlp_create: 2.65x the f32-MFMA peak)
- *   NLOT_MLP_ARITH_F32         v_mfma_f32 products (the reference's fp32 net, gen/nn_sdf.cpp, at the f32 peak) */
+ *   NLOT_MLP_ARITH_F32         v_mfma_f32 products (the reference's fp32 net, gen/nn_sdf.cpp, at the f32 peak)
+ *   NLOT_MLP_ARITH_SEQ         (ABI v15; ReLU nets) every sum a sequential fp32 FMA chain in index order, one thread per
+ *                              point: a fixed, documented summation order (the test oracle's), for bitwise-reproducible
+ *                              comparisons; not a throughput path */
 #define NLOT_MLP_ARITH_SPLIT_BF16 0
 #define NLOT_MLP_ARITH_F32 1
+#define NLOT_MLP_ARITH_SEQ 2
 NlotMlp* nlot_mlp_create_ex(const NlotMlpDesc* desc, int32_t arith);
 void nlot_mlp_destroy(NlotMlp* mlp);
 

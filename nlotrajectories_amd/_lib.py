@@ -79,7 +79,7 @@ def lib():
     L.nlot_rrt_init.restype = C.c_int32
     L.nlot_casadi_bind.argtypes = [vp]
     L.nlot_casadi_bind.restype = C.c_int32
-    if L.nlot_abi_version() != 14:
+    if L.nlot_abi_version() != 15:
         raise NlotError("libnlot.so ABI version mismatch")
     _lib = L
     return L

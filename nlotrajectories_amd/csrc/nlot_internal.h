@@ -43,6 +43,7 @@ void casadi_unbind(const NlotMlp* m);
 
 // Device-resident learned-SDF weights (opaque NlotMlp of the ABI).
 struct MlpDev {
+    int arith;       // NLOT_MLP_ARITH_* (nlot_mlp_create_ex)
     int in_kind;     // NLOT_MLP_IN_*
     int H;           // hidden width
     int n_hidden;    // HxH layers

@@ -1358,9 +1358,133 @@ static int launch_smooth(const MlpDev& w, const float* pts, int64_t n, const int
     return NLOT_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// NLOT_MLP_ARITH_SEQ (ABI v15): the ReLU net in the reference order of every sum.  One thread per point; each dot
+// product is a sequential fmaf chain over its index in increasing order with the bias added after it, FMA
+// contraction off: the expression sequence of the oracle's default order (oracle/nlot_oracle.c oracle_mlp_point,
+// NLOT_ORACLE_MLP_REV unset).  For a Linear + ReLU input layer (benchmark 6's trained net, l4casadi's naive MLP) the
+// outputs are bitwise the oracle's; a Fourier input layer goes through the device's cosf / sinf, within an ulp of the
+// host libm's.  Test arithmetic: it takes the net's rounding out of a GPU-vs-oracle comparison, so that what is left
+// is the solver's fp64 (tests/test_pinned_iterates_gpu.py).  Not a throughput path: VALU chains, per-thread arrays
+// in scratch.  The value launches write no ReLU patterns and the full launches reuse no forward (both optional).
+// ---------------------------------------------------------------------------------------------
+template <int H, bool FULL>
+__global__ __launch_bounds__(64) void mlp_seq(MlpDev w, const float* __restrict__ pts, int64_t cnt_host,
+                                              const int* __restrict__ cnt_dev, int P_per, int64_t ld,
+                                              const float* __restrict__ lam, MlpOut out) {
+#pragma clang fp contract(off)
+    constexpr int MW = H / 32;
+    const int64_t cnt = cnt_dev ? (int64_t)(*cnt_dev) : cnt_host;
+    const int64_t npts = cnt * P_per;
+    const int L = w.n_hidden;
+    const bool fourier = w.in_kind == NLOT_MLP_IN_FOURIER;
+    for (int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gi < npts; gi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t pi = ld == 0 ? gi : (gi % cnt) + (gi / cnt) * ld;
+        const float px = pts[2 * pi], py = pts[2 * pi + 1];
+        float z0[H], h[H], hn[H];
+        uint32_t mask[kMaxStreamLayers + 1][MW];
+        for (int k = 0; k < H; ++k) {  // p @ A + b0 (graph ___torch_mangle_0.py)
+            const float z = fmaf(py, w.A[H + k], px * w.A[k]) + w.b0[k];
+            z0[k] = z;
+            h[k] = fourier ? cosf(z) * w.scale : (z > 0.f ? z : 0.f);
+        }
+        for (int q = 0; q < MW; ++q) {
+            uint32_t m = 0;
+            for (int t = 0; t < 32; ++t) m |= (fourier || z0[32 * q + t] > 0.f) ? (1u << t) : 0u;
+            mask[0][q] = m;
+        }
+        for (int l = 0; l < L; ++l) {
+            const float* W = w.W + (size_t)l * H * H;
+            for (int j = 0; j < H; ++j) {
+                float a = 0.f;
+                for (int k = 0; k < H; ++k) a = fmaf(W[(size_t)j * H + k], h[k], a);
+                a += w.b[(size_t)l * H + j];
+                hn[j] = a > 0.f ? a : 0.f;
+            }
+            for (int q = 0; q < MW; ++q) {
+                uint32_t m = 0;
+                for (int t = 0; t < 32; ++t) m |= hn[32 * q + t] > 0.f ? (1u << t) : 0u;
+                mask[l + 1][q] = m;
+            }
+            for (int j = 0; j < H; ++j) h[j] = hn[j];
+        }
+        float f = 0.f;
+        for (int j = 0; j < H; ++j) f = fmaf(w.w_out[j], h[j], f);
+        out.val[pi * out.sv] = f + w.b_out;
+        if constexpr (FULL) {
+            // reverse sweep: d = df/dh_l, each column sum dn[k] = sum_j W[j][k] d[j] over j in increasing order
+            const float lm = lam ? lam[pi] : 1.f;
+            float* d = h;
+            float* dn = hn;
+            for (int j = 0; j < H; ++j) d[j] = lm * w.w_out[j];
+            for (int l = L - 1; l >= 0; --l) {
+                const float* W = w.W + (size_t)l * H * H;
+                for (int j = 0; j < H; ++j) d[j] = (mask[l + 1][j >> 5] >> (j & 31)) & 1u ? d[j] : 0.f;
+                for (int k = 0; k < H; ++k) {
+                    float t = 0.f;
+                    for (int j = 0; j < H; ++j) t = fmaf(W[(size_t)j * H + k], d[j], t);
+                    dn[k] = t;
+                }
+                float* s = d;
+                d = dn;
+                dn = s;
+            }
+            float gx = 0.f, gy = 0.f, hxx = 0.f, hxy = 0.f, hyy = 0.f;
+            for (int k = 0; k < H; ++k) {
+                const float ax = w.A[k], ay = w.A[H + k];
+                float dz, c2;
+                if (fourier) {
+                    dz = d[k] * (-w.scale * sinf(z0[k]));
+                    c2 = d[k] * (-w.scale * cosf(z0[k]));
+                } else {
+                    dz = (mask[0][k >> 5] >> (k & 31)) & 1u ? d[k] : 0.f;
+                    c2 = 0.f;  // ReLU input layer: piecewise linear, Hessian 0 a.e.
+                }
+                gx = fmaf(ax, dz, gx);
+                gy = fmaf(ay, dz, gy);
+                hxx = fmaf(ax * ax, c2, hxx);
+                hxy = fmaf(ax * ay, c2, hxy);
+                hyy = fmaf(ay * ay, c2, hyy);
+            }
+            if (out.gx) {
+                out.gx[pi * out.sg] = gx;
+                out.gy[pi * out.sg] = gy;
+            }
+            if (out.hxx) {
+                out.hxx[pi * out.sh] = hxx;
+                out.hxy[pi * out.sh] = hxy;
+                if (out.hyx != out.hxy) out.hyx[pi * out.sh] = hxy;
+                out.hyy[pi * out.sh] = hyy;
+            }
+        }
+    }
+}
+
+template <int H, bool FULL>
+static int launch_seq(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
+                      const float* lam, const MlpOut& out, hipStream_t stream) {
+    const int64_t blocks = (n * P_per + 63) / 64;
+    const int64_t cap = (int64_t)device_cus() * 16;
+    const int grid = (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+    hipLaunchKernelGGL((mlp_seq<H, FULL>), dim3(grid), dim3(64), 0, stream, w, pts, n, n_dev, P_per, ld, lam, out);
+    NLOT_HIP_CHECK(hipGetLastError());
+    return NLOT_OK;
+}
+
 int launch_mlp_strided(const MlpDev& w, const float* pts, int64_t n, const int* n_dev, int P_per, int64_t ld,
                        const float* lam, const MlpOut& out, bool full, hipStream_t stream, const MlpReuse* reuse) {
     if (n <= 0) return NLOT_OK;
+    if (w.arith == NLOT_MLP_ARITH_SEQ) {  // ReLU nets only (nlot_mlp_create_ex checks)
+#define NLOT_SEQ_CASE(HH)                                                                      \
+    if (w.H == HH) return full ? launch_seq<HH, true>(w, pts, n, n_dev, P_per, ld, lam, out, stream) \
+                               : launch_seq<HH, false>(w, pts, n, n_dev, P_per, ld, lam, out, stream);
+        NLOT_SEQ_CASE(64)
+        NLOT_SEQ_CASE(128)
+        NLOT_SEQ_CASE(256)
+#undef NLOT_SEQ_CASE
+        set_error("MLP kernel: hidden width must be 64, 128 or 256 (DESIGN.md §7)");
+        return NLOT_ERR_INVALID;
+    }
     if (w.act != NLOT_ACT_RELU) {  // smooth activations: forward hyper-duals (the ReLU masks / reuse do not apply)
         if (w.n_hidden < 0 || w.n_hidden > kMaxStreamLayers) {
             set_error("MLP kernel: 0 to 4 hidden HxH layers are supported for smooth activations");
@@ -1413,8 +1537,12 @@ extern "C" NlotMlp* nlot_mlp_create(const NlotMlpDesc* d) { return nlot_mlp_crea
 
 extern "C" NlotMlp* nlot_mlp_create_ex(const NlotMlpDesc* d, int32_t arith) {
     using namespace nlot;
-    if (arith != NLOT_MLP_ARITH_SPLIT_BF16 && arith != NLOT_MLP_ARITH_F32) {
-        set_error("nlot_mlp_create_ex: arith must be NLOT_MLP_ARITH_SPLIT_BF16 or NLOT_MLP_ARITH_F32");
+    if (arith != NLOT_MLP_ARITH_SPLIT_BF16 && arith != NLOT_MLP_ARITH_F32 && arith != NLOT_MLP_ARITH_SEQ) {
+        set_error("nlot_mlp_create_ex: arith must be NLOT_MLP_ARITH_SPLIT_BF16, NLOT_MLP_ARITH_F32 or NLOT_MLP_ARITH_SEQ");
+        return nullptr;
+    }
+    if (arith == NLOT_MLP_ARITH_SEQ && d && d->act != NLOT_ACT_RELU) {
+        set_error("nlot_mlp_create_ex: NLOT_MLP_ARITH_SEQ is defined for ReLU nets only");
         return nullptr;
     }
     if (!d || !d->A || !d->b0 || !d->w_out || (d->n_hidden > 0 && (!d->W || !d->b))) {
@@ -1455,6 +1583,7 @@ extern "C" NlotMlp* nlot_mlp_create_ex(const NlotMlpDesc* d, int32_t arith) {
     m->block = blk;
     m->device = 0;
     (void)hipGetDevice(&m->device);
+    m->dev.arith = arith;
     m->dev.in_kind = d->in_kind;
     m->dev.H = H;
     m->dev.n_hidden = L;

@@ -14,9 +14,10 @@ from .nn import MlpWeights
 class DeviceMlp:
     """Device-resident learned-SDF weights (NlotMlp handle).  arith: "split_bf16" (the default: three-way bf16 operand
     split, six MFMA products per fp32 product) or "f32" (v_mfma_f32 products, the reference's fp32 net); both fp32
-    arithmetic, differing at the rounding level (include/nlot.h, NLOT_MLP_ARITH_*)."""
+    arithmetic, differing at the rounding level (include/nlot.h, NLOT_MLP_ARITH_*).  "seq" (ReLU nets; tests): every
+    sum a sequential fp32 FMA chain in index order, the oracle's default order, one thread per point."""
 
-    ARITH = {"split_bf16": 0, "f32": 1}
+    ARITH = {"split_bf16": 0, "f32": 1, "seq": 2}
 
     def __init__(self, weights: MlpWeights, arith: str = "split_bf16"):
         require_gpu()

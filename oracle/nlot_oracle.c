@@ -224,7 +224,8 @@ static void oracle_mlp_point_smooth(const NlotMlpDesc* m, float px, float py, fl
  * a solve whose outcome changes under it is not reproducible at the GPU's arithmetic.  Read per call (toggled
  * between whole batches by the Python side).  NLOT_ORACLE_MLP_REV=v >= 2: the index order i -> (i * m_v) mod H with
  * an odd multiplier m_v (a permutation for H a power of two): more samples of the same kind of difference
- * (tests/test_pinned_iterates_gpu.py). */
+ * (tests/test_pinned_iterates_gpu.py).  v >= 8 (round 6): a pseudo-random permutation of the index seeded by v
+ * (Fisher-Yates over a splitmix64 stream), the same one for every sum of the call. */
 static int mlp_rev(void) {
     const char* e = getenv("NLOT_ORACLE_MLP_REV");
     return e ? atoi(e) : 0;
@@ -233,13 +234,30 @@ static int mlp_perm_mult(int v) {
     static const int m[8] = {1, 1, 3, 5, 7, 11, 13, 17};
     return m[v & 7];
 }
+static void mlp_perm_random(int v, int H, int* perm) {
+    uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(v + 1);
+    for (int i = 0; i < H; ++i) perm[i] = i;
+    for (int i = H - 1; i > 0; --i) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        const int j = (int)(z % (uint64_t)(i + 1));
+        const int t = perm[i];
+        perm[i] = perm[j];
+        perm[j] = t;
+    }
+}
 
 void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int want, float out[6]) {
     enum { HM = 256, LM = 8 };
     const int H = m->hidden;
     const int rv = mlp_rev();
     const int rvm = mlp_perm_mult(rv);
-#define RIX(i) (rv == 0 ? (i) : rv == 1 ? H - 1 - (i) : ((i) * rvm) % H)
+    int perm[HM];
+    if (rv >= 8) mlp_perm_random(rv, H, perm);
+#define RIX(i) (rv == 0 ? (i) : rv == 1 ? H - 1 - (i) : rv >= 8 ? perm[i] : ((i) * rvm) % H)
     if (m->act != NLOT_ACT_RELU) {
         oracle_mlp_point_smooth(m, px, py, lam, want, out);
         return;

@@ -12,6 +12,7 @@
 #   rocprof=K,W      rocprofv3 --kernel-trace --stats over bench.py --steps K --warmup W
 #   pmc=K,W,COUNTERS rocprofv3 --pmc COUNTERS (one pass) over bench.py --steps K --warmup W --cpu-sample 0
 #   py=SCRIPT[,ARGS] python3 SCRIPT [ARGS]  (a script under scripts/, 600 s limit)
+#   regress          the restoration grid-bound test against libnlot_regress.so (scripts/resto_bound_regress.sh): must fail
 TAG=$1
 shift
 OUT=gpurun_out/$TAG
@@ -52,6 +53,11 @@ for step in "$@"; do
       timeout -s KILL 600 rocprofv3 --pmc "${A[@]:2}" -d "$OUT/pmc$n" -o run -- \
         python3 bench.py --gpus 1 --steps "${A[0]}" --warmup "${A[1]}" --cpu-sample 0 > "$OUT/$n.bench.json" 2> "$log"
       rc=$? ;;
+    regress)  # scripts/resto_bound_regress.sh's library: the restoration grid-bound test must FAIL on it
+      NLOT_LIB=libnlot_regress.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 500 \
+        --timeout-method thread -k resto_grid_bound > "$log" 2>&1
+      r=$?; tail -1 "$log"
+      if [ $r -eq 1 ]; then echo "[gpu.sh] regress: the test failed on the old clamp, as it must"; rc=0; else rc=1; fi ;;
     py)
       timeout -k 10 600 python3 -u "${A[@]}" > "$log" 2>&1
       rc=$?; tail -3 "$log" ;;

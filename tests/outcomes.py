@@ -35,6 +35,10 @@ PERTURB = 1e-13
 # (start coordinate, offset, net summed in reverse order)
 PERTURBATIONS = ((0, 0.0, False), (0, PERTURB, False), (0, -PERTURB, False), (1, PERTURB, False),
                  (1, -PERTURB, False), (0, 0.0, True))
+# the fixtures' runs (tests/golden/make_oracle_outcomes.py): the six above and the net's fp32 sums in 14 more orders
+# (NLOT_ORACLE_MLP_REV = 2..7 strided, 8..15 seeded random permutations)
+NET_ORDERS = tuple((0, 0.0, v) for v in range(2, 16))
+FIXTURE_PERTURBATIONS = PERTURBATIONS + NET_ORDERS
 WIDE = tuple((c, s * d, False) for d in (1e-11, 1e-9, 1e-7) for c in (0, 1) for s in (1, -1))
 COST_REPRO = 1e-8
 XDEV_REPRO = 1e-6  # a failed run counts as reproducible when every perturbed run stops at the same point (max |dX|, |dU|)

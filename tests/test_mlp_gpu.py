@@ -105,3 +105,50 @@ def test_mlp_relu_two_layer_vs_torch():
     np.testing.assert_allclose(v.cpu().numpy(), f.detach().numpy(), atol=1e-4 * max(1, f.abs().max().item()))
     np.testing.assert_allclose(gg.cpu().numpy(), g.numpy(), atol=1e-4 * max(1, g.abs().max().item()))
     assert float(hh.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("net", ["b6_trained", "relu_64x2", "relu_256x3"])
+def test_seq_arith_bitwise_oracle(net):
+    """NLOT_MLP_ARITH_SEQ (include/nlot.h, ABI v15): every sum a sequential fp32 FMA chain in index order, the oracle's
+    default order (oracle/nlot_oracle.c oracle_mlp_point).  For ReLU-input nets (benchmark 6's trained 2-128-128-1 net,
+    l4casadi's naive MLPs) value, lam*gradient and the value-only launch are bitwise the oracle's."""
+    import os
+
+    import oracle as O
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    if net == "b6_trained":
+        w = MlpWeights.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                         "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
+    elif net == "relu_64x2":
+        w = MlpWeights.random_relu_mlp(hidden=64, n_hidden=2, seed=1)
+    else:
+        w = MlpWeights.random_relu_mlp(hidden=256, n_hidden=3, seed=2)
+    rng = np.random.default_rng(7)
+    pts = rng.uniform(-0.2, 1.4, size=(5000, 2)).astype(np.float32)
+    lam = rng.uniform(-2, 2, size=5000).astype(np.float32)
+    dm = DeviceMlp(w, "seq")
+    t = torch.tensor(pts, device="cuda")
+    v, g, h = (x.cpu().numpy() for x in sdf_mlp_eval(dm, t, lam=torch.tensor(lam, device="cuda")))
+    vv, _, _ = sdf_mlp_eval(dm, t, derivatives=False)
+    ov, og, oh = O.mlp_eval(O.HostMlp(w), pts, lam)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(vv.cpu().numpy(), ov)
+    np.testing.assert_array_equal(g, og)
+    np.testing.assert_array_equal(h, oh)
+
+
+def test_seq_arith_fourier_within_libm_ulp(artefact):
+    """The artefact FourierMLP through NLOT_MLP_ARITH_SEQ: the same sums as the oracle's; the input layer's cos / sin
+    are the device's (ocml) against the host's libm, so agreement is to the rounding of those, not bitwise."""
+    import oracle as O
+    from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
+
+    pts = np.random.default_rng(8).uniform(-0.3, 1.3, size=(4000, 2)).astype(np.float32)
+    v, g, _ = (x.cpu().numpy() for x in sdf_mlp_eval(DeviceMlp(artefact, "seq"), torch.tensor(pts, device="cuda")))
+    ov, og, _ = O.mlp_eval(O.HostMlp(artefact), pts)
+    same = float((v == ov).mean())
+    print(f"[seq] Fourier net: {same:.3f} of the values bitwise equal, max |dv| {np.abs(v - ov).max():.2e}", flush=True)
+    np.testing.assert_allclose(v, ov, atol=2e-6)
+    np.testing.assert_allclose(g, og, atol=2e-5 * max(1, np.abs(og).max()))
