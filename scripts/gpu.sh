@@ -12,6 +12,7 @@
 #   rocprof=K,W      rocprofv3 --kernel-trace --stats over bench.py --steps K --warmup W
 #   pmc=K,W,COUNTERS rocprofv3 --pmc COUNTERS (one pass) over bench.py --steps K --warmup W --cpu-sample 0
 #   py=SCRIPT[,ARGS] python3 SCRIPT [ARGS]  (a script under scripts/, 600 s limit)
+#   sh=SCRIPT[,ARGS] bash SCRIPT [ARGS]     (900 s limit)
 #   regress          the restoration grid-bound test against libnlot_regress.so (scripts/resto_bound_regress.sh): must fail
 TAG=$1
 shift
@@ -58,6 +59,9 @@ for step in "$@"; do
         --timeout-method thread -k resto_grid_bound > "$log" 2>&1
       r=$?; tail -1 "$log"
       if [ $r -eq 1 ]; then echo "[gpu.sh] regress: the test failed on the old clamp, as it must"; rc=0; else rc=1; fi ;;
+    sh)
+      timeout -k 10 900 bash "${A[@]}" > "$log" 2>&1
+      rc=$?; tail -3 "$log" ;;
     py)
       timeout -k 10 600 python3 -u "${A[@]}" > "$log" 2>&1
       rc=$?; tail -3 "$log" ;;

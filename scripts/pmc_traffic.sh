@@ -4,7 +4,7 @@
 # (solve, point) by scripts/pmc_traffic.py.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
-OUT="$R/gpurun_out/${OUT_TAG:-r04pmc}"
+OUT="$R/gpurun_out/${1:-${OUT_TAG:-r06pmc}}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
