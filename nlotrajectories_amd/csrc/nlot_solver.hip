@@ -5088,7 +5088,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NLOT_WPE_RLS
 // NLOT_UNIT = -1 holds the C ABI, the statistics and the dispatch; without NLOT_UNIT (tuning builds) one unit does all.
 #ifndef NLOT_UNIT
 static thread_local NlotSolveStats g_stats;
-static int g_timing = 0;  // nlot_set_timing: 0 off, k: the steps with index % k == 0
+static int g_timing = 0;  // nlot_set_timing: 0 off; k: one step in each group of k, at position (step / k) % k (rotating)
 #else
 extern thread_local NlotSolveStats g_stats;
 extern int g_timing;
