@@ -47,11 +47,13 @@ for step in "$@"; do
       rc=$?
       [ $rc -eq 0 ] && python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('bench', d['value'], d['ms_per_step'], d['config']['status_counts_rank0'], 'frac', r['frac'], r['avg_launch_ms'])" "$OUT/$n.bench.json" ;;
     rocprof)
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- \
+      # the kernel trace is too large to copy back: it stays in /tmp, the --stats summary comes back
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "/tmp/rocprof_$TAG" -o run -- \
         python3 bench.py --gpus 1 --steps "${A[0]}" --warmup "${A[1]}" --cpu-sample 0 > "$OUT/$n.bench.json" 2> "$log"
-      rc=$? ;;
+      rc=$?
+      find "/tmp/rocprof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/$n.kernel_stats.csv" \; ;;
     pmc)
-      timeout -s KILL 600 rocprofv3 --pmc "${A[@]:2}" -d "$OUT/pmc$n" -o run -- \
+      timeout -s KILL 600 rocprofv3 --pmc "${A[@]:2}" -d "/tmp/pmc_${TAG}_$n" -o run -- \
         python3 bench.py --gpus 1 --steps "${A[0]}" --warmup "${A[1]}" --cpu-sample 0 > "$OUT/$n.bench.json" 2> "$log"
       rc=$? ;;
     regress)  # scripts/resto_bound_regress.sh's library: the restoration grid-bound test must FAIL on it
