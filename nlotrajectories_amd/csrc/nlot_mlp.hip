@@ -1363,8 +1363,9 @@ static int launch_smooth(const MlpDev& w, const float* pts, int64_t n, const int
 // product is a sequential fmaf chain over its index in increasing order with the bias added after it, FMA
 // contraction off: the expression sequence of the oracle's default order (oracle/nlot_oracle.c oracle_mlp_point,
 // NLOT_ORACLE_MLP_REV unset).  For a Linear + ReLU input layer (benchmark 6's trained net, l4casadi's naive MLP) the
-// outputs are bitwise the oracle's; a Fourier input layer goes through the device's cosf / sinf, within an ulp of the
-// host libm's.  Test arithmetic: it takes the net's rounding out of a GPU-vs-oracle comparison, so that what is left
+// outputs are bitwise the oracle's; a Fourier input layer's cos / sin are the fp64 functions rounded to fp32 on both
+// sides (the correctly rounded fp32 values except where the two libms' fp64 results straddle an fp32 rounding
+// boundary, about once in 2^28 evaluations).  Test arithmetic: it takes the net's rounding out of a GPU-vs-oracle comparison, so that what is left
 // is the solver's fp64 (tests/test_pinned_iterates_gpu.py).  Not a throughput path: VALU chains, per-thread arrays
 // in scratch.  The value launches write no ReLU patterns and the full launches reuse no forward (both optional).
 // ---------------------------------------------------------------------------------------------
@@ -1386,7 +1387,7 @@ __global__ __launch_bounds__(64) void mlp_seq(MlpDev w, const float* __restrict_
         for (int k = 0; k < H; ++k) {  // p @ A + b0 (graph ___torch_mangle_0.py)
             const float z = fmaf(py, w.A[H + k], px * w.A[k]) + w.b0[k];
             z0[k] = z;
-            h[k] = fourier ? cosf(z) * w.scale : (z > 0.f ? z : 0.f);
+            h[k] = fourier ? (float)cos((double)z) * w.scale : (z > 0.f ? z : 0.f);
         }
         for (int q = 0; q < MW; ++q) {
             uint32_t m = 0;
@@ -1434,8 +1435,8 @@ __global__ __launch_bounds__(64) void mlp_seq(MlpDev w, const float* __restrict_
                 const float ax = w.A[k], ay = w.A[H + k];
                 float dz, c2;
                 if (fourier) {
-                    dz = d[k] * (-w.scale * sinf(z0[k]));
-                    c2 = d[k] * (-w.scale * cosf(z0[k]));
+                    dz = d[k] * (-w.scale * (float)sin((double)z0[k]));
+                    c2 = d[k] * (-w.scale * (float)cos((double)z0[k]));
                 } else {
                     dz = (mask[0][k >> 5] >> (k & 31)) & 1u ? d[k] : 0.f;
                     c2 = 0.f;  // ReLU input layer: piecewise linear, Hessian 0 a.e.

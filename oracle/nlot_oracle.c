@@ -269,7 +269,11 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
         float z = fmaf(py, m->A[H + k], px * m->A[k]) + m->b0[k];
         z0[k] = z;
         if (m->in_kind == NLOT_MLP_IN_FOURIER) {
-            h[k] = cosf(z) * m->fourier_scale; /* nn_architectures.py:38 */
+            /* nn_architectures.py:38.  The fp32 cos as the fp64 cos rounded to fp32: correctly rounded in all but
+             * ~2^-28 of the arguments, so any fp32 libm (libtorch's included) is within an ulp of it, and the GPU's
+             * NLOT_MLP_ARITH_SEQ net forms the same value (round 6; cosf of glibc and of the device differ in the last
+             * bit on ~60 % of the artefact's arguments) */
+            h[k] = (float)cos((double)z) * m->fourier_scale;
             mask[0][k] = 1;
         } else {
             mask[0][k] = z > 0.f;
@@ -314,8 +318,8 @@ void oracle_mlp_point(const NlotMlpDesc* m, float px, float py, float lam, int w
         const int k = RIX(kq);
         float ax = m->A[k], ay = m->A[H + k], dz, c2;
         if (m->in_kind == NLOT_MLP_IN_FOURIER) {
-            dz = d[k] * (-m->fourier_scale * sinf(z0[k]));
-            c2 = d[k] * (-m->fourier_scale * cosf(z0[k]));
+            dz = d[k] * (-m->fourier_scale * (float)sin((double)z0[k]));
+            c2 = d[k] * (-m->fourier_scale * (float)cos((double)z0[k]));
         } else {
             dz = mask[0][k] ? d[k] : 0.f;
             c2 = 0.f; /* ReLU input layer: piecewise linear, Hessian 0 a.e. */

@@ -48,7 +48,7 @@ for step in "$@"; do
       [ $rc -eq 0 ] && python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('bench', d['value'], d['ms_per_step'], d['config']['status_counts_rank0'], 'frac', r['frac'], r['avg_launch_ms'])" "$OUT/$n.bench.json" ;;
     rocprof)
       # the kernel trace is too large to copy back: it stays in /tmp, the --stats summary comes back
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "/tmp/rocprof_$TAG" -o run -- \
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/rocprof_$TAG" -o run -- \
         python3 bench.py --gpus 1 --steps "${A[0]}" --warmup "${A[1]}" --cpu-sample 0 > "$OUT/$n.bench.json" 2> "$log"
       rc=$?
       find "/tmp/rocprof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/$n.kernel_stats.csv" \; ;;

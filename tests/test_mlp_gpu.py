@@ -139,16 +139,23 @@ def test_seq_arith_bitwise_oracle(net):
     np.testing.assert_array_equal(h, oh)
 
 
-def test_seq_arith_fourier_within_libm_ulp(artefact):
+def test_seq_arith_fourier_nearly_bitwise(artefact):
     """The artefact FourierMLP through NLOT_MLP_ARITH_SEQ: the same sums as the oracle's; the input layer's cos / sin
-    are the device's (ocml) against the host's libm, so agreement is to the rounding of those, not bitwise."""
+    are the fp64 functions rounded to fp32 on both sides (device ocml vs host libm), which differ only where the two
+    fp64 results straddle an fp32 rounding boundary (~2^-28 of the arguments): all but a few of 4000 points x 128 units
+    bitwise, and the outputs bitwise on at least 99.9 % of the points."""
     import oracle as O
     from nlotrajectories_amd.ops import DeviceMlp, sdf_mlp_eval
 
-    pts = np.random.default_rng(8).uniform(-0.3, 1.3, size=(4000, 2)).astype(np.float32)
-    v, g, _ = (x.cpu().numpy() for x in sdf_mlp_eval(DeviceMlp(artefact, "seq"), torch.tensor(pts, device="cuda")))
-    ov, og, _ = O.mlp_eval(O.HostMlp(artefact), pts)
-    same = float((v == ov).mean())
-    print(f"[seq] Fourier net: {same:.3f} of the values bitwise equal, max |dv| {np.abs(v - ov).max():.2e}", flush=True)
+    rng = np.random.default_rng(8)
+    pts = rng.uniform(-0.3, 1.3, size=(4000, 2)).astype(np.float32)
+    lam = rng.uniform(-2, 2, size=4000).astype(np.float32)
+    v, g, h = (x.cpu().numpy() for x in sdf_mlp_eval(DeviceMlp(artefact, "seq"), torch.tensor(pts, device="cuda"),
+                                                    lam=torch.tensor(lam, device="cuda")))
+    ov, og, oh = O.mlp_eval(O.HostMlp(artefact), pts, lam)
+    same = float(((v == ov) & (g == og).all(1) & (h == oh).all((1, 2))).mean())
+    print(f"[seq] Fourier net: {same:.4f} of the points bitwise equal (value, gradient, Hessian), max |dv| "
+          f"{np.abs(v - ov).max():.2e}", flush=True)
+    assert same >= 0.999
     np.testing.assert_allclose(v, ov, atol=2e-6)
     np.testing.assert_allclose(g, og, atol=2e-5 * max(1, np.abs(og).max()))
