@@ -13,6 +13,7 @@
 #   pmc=K,W,COUNTERS rocprofv3 --pmc COUNTERS (one pass) over bench.py --steps K --warmup W --cpu-sample 0
 #   py=SCRIPT[,ARGS] python3 SCRIPT [ARGS]  (a script under scripts/, 600 s limit)
 #   sh=SCRIPT[,ARGS] bash SCRIPT [ARGS]     (900 s limit)
+#   rehearse=K,W[,B] NLOT_DIST_BACKEND=gloo bench.py --gpus 2 (self-launched ranks sharing this GPU), B per rank
 #   regress          the restoration grid-bound test against libnlot_regress.so (scripts/resto_bound_regress.sh): must fail
 TAG=$1
 shift
@@ -46,6 +47,11 @@ for step in "$@"; do
         > "$OUT/$n.bench.json" 2> "$log"
       rc=$?
       [ $rc -eq 0 ] && python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('bench', d['value'], d['ms_per_step'], d['config']['status_counts_rank0'], 'frac', r['frac'], r['avg_launch_ms'])" "$OUT/$n.bench.json" ;;
+    rehearse)  # bench.py --gpus 2 with no launcher: it starts 2 ranks itself; gloo collectives, both ranks on this GPU
+      NLOT_DIST_BACKEND=gloo timeout -k 10 900 python -u bench.py --gpus 2 --steps "${A[0]}" --warmup "${A[1]}" \
+        --batch "${A[2]:-4096}" --slots "${A[2]:-4096}" > "$OUT/$n.bench.json" 2> "$log"
+      rc=$?
+      [ $rc -eq 0 ] && python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('rehearsal n_gpus', d['n_gpus'], d['config']['process_group'], d['value'], [r['status_counts'] for r in d['config']['per_rank']])" "$OUT/$n.bench.json" ;;
     rocprof)
       # the kernel trace is too large to copy back: it stays in /tmp, the --stats summary comes back
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/rocprof_$TAG" -o run -- \
