@@ -841,6 +841,7 @@ typedef struct {
     NlotProblem prel;
     double *sb, *yb, *zbl, *zbu, *rcb, *dsb, *yb_n, *dzbl, *dzbu;
     double *arena;
+    unsigned long long jit_ctr; /* NLOT_ORACLE_STEP_JITTER's stream position (per solve: deterministic) */
 } Sol;
 static int row_d(const Sol* s, int k, int i) { return s->nx + k * s->nx + i; }
 static int row_t(const Sol* s, int j) { return s->nx + s->N * s->nx + j; }
@@ -2372,15 +2373,16 @@ static double barrier_gd(const Sol* s) {
 /* NLOT_ORACLE_STEP_JITTER=eps (test infrastructure, tests/test_pinned_iterates_gpu.py): every Newton step's primal
  * components are scaled by 1 +- eps (a fixed pseudo-random sign per component and step): a model of the rounding
  * differences of another fp64 summation order in the KKT solve (the GPU's lane-group Riccati sweeps), injected in
- * every iteration where the fixture's perturbed runs differ only at the start.  0 or unset: off (the default). */
+ * every iteration where the fixture's perturbed runs differ only at the start.  0 or unset: off (the default).  The
+ * sign stream restarts with every solve (round 6: it was per thread, so a run depended on the runs its thread did
+ * before). */
 static void step_jitter(Sol* s) {
     const char* e = getenv("NLOT_ORACLE_STEP_JITTER");
     const double eps = e ? atof(e) : 0.0;
     if (eps == 0.0) return;
-    static __thread unsigned long long ctr = 0;
     const int nX = (s->N + 1) * s->nx, nU = s->N * s->nu;
     for (int i = 0; i < nX + nU + s->N + 1; ++i) {
-        unsigned long long h = (++ctr) * 0x9E3779B97F4A7C15ull;
+        unsigned long long h = (++s->jit_ctr) * 0x9E3779B97F4A7C15ull;
         h ^= h >> 31;
         const double f = 1.0 + ((h >> 7) & 1 ? eps : -eps);
         if (i < nX) s->dX[i] *= f;

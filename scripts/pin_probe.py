@@ -3,7 +3,7 @@
 iterate at max_iter = k for k = 1..K against the unperturbed oracle trace (oracle_solve_trace) and the oracle's own
 perturbed runs (the +-1e-13 starts and the reverse-order net), one line per k.
 
-    python scripts/pin_probe.py --case b6 --inst 3 --kmax 24 [--form rows]
+    python scripts/pin_probe.py --case b6 --inst 3 --kmax 24 [--arith split_bf16|f32|seq]
 
 GPU box; test infrastructure (runs the oracle as the checker).  NLOT_MLP=f32 in the environment switches the GPU's
 SDF net to its fp32 path for an A/B against the split-bf16 default."""
@@ -26,8 +26,7 @@ def main():
     ap.add_argument("--kmax", type=int, default=24)
     ap.add_argument("--kmin", type=int, default=1)
     ap.add_argument("--kstep", type=int, default=1)
-    ap.add_argument("--arith", default="split_bf16", choices=["split_bf16", "f32"])
-    ap.add_argument("--form", default="rows")
+    ap.add_argument("--arith", default="split_bf16", choices=["split_bf16", "f32", "seq"])
     a = ap.parse_args()
     import oracle as O
     from outcomes import PERTURBATIONS, mlp_order
@@ -37,8 +36,7 @@ def main():
     from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
     from nlotrajectories_amd.solver import solve_batch
 
-    f = dict(np.load(os.path.join(ROOT, "tests", "golden",
-                                  "oracle_outcomes.npz" if a.form == "rows" else "oracle_outcomes_varbounds.npz")))
+    f = dict(np.load(os.path.join(ROOT, "tests", "golden", "oracle_outcomes.npz")))
     if a.case == "b6":
         prob = B6_PROBLEM
         w = MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
@@ -58,7 +56,8 @@ def main():
             with mlp_order(rev):
                 traces.append(O.solve_trace(prob, x, xg, hm, opt=opt, X_init=xi, cap=a.kmax + 1)["trace"])
         T0 = traces[0]
-        print(f"instance {i}: kpin {int(f[f'{a.case}_kpin'][i])}, oracle status {int(f[f'{a.case}_status'][0, i])} "
+        print(f"instance {i}: kpin {int(f[f'{a.case}_kpin'][i])}, kseq {int(f[f'{a.case}_kseq'][i])}, "
+              f"oracle status {int(f[f'{a.case}_status'][0, i])} "
               f"iters {int(f[f'{a.case}_iters'][0, i])}, net {a.arith}", flush=True)
         for k in range(a.kmin, a.kmax + 1, a.kstep):
             o = _abi.default_options(general_bounds=gb, max_iter=k)

@@ -26,8 +26,9 @@ Per-instance pinned iterates: every run records its iterate at the top of each i
   {case}_kpin[i] = k_i, the last iteration (at most PIN_CAP = 200, at most the shortest run) up to which all 19
       perturbed runs stay within PIN_TOL = 1e-5 (max |dX|, |dU|) of the unperturbed run: where the GPU's MFMA nets
       (split-bf16, f32) must still be on the oracle's path;
-  {case}_kseq[i], the same over rows 1-4 only: where the GPU with the oracle's own net arithmetic
-      (NLOT_MLP_ARITH_SEQ: the net bitwise the oracle's for ReLU-input nets) must still be on it;
+  {case}_kseq[i], the same over fp64-sized perturbations only (rows 1-4, the merit function's sums reversed, and
+      +-1e-13 relative noise on every Newton step: SEQ_EXTRA, runs capped at 201 iterations): where the GPU with the
+      oracle's own net arithmetic (NLOT_MLP_ARITH_SEQ: the net bitwise the oracle's) must still be on it;
   {case}_Xpin / _Upin / _Xseq / _Useq: the unperturbed iterate there (what max_iter = k returns);
   {case}_stpin / _stseq: the unperturbed run's status at max_iter = k (max_iter, or the final status where the run
       ends at the top of iteration k; a restoration line-search failure at k = iters happens inside iteration k and
@@ -111,6 +112,56 @@ def pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads):
         return np.array(list(ex.map(one, range(len(X0)))), np.int32)
 
 
+# k_seq's fp64-sized perturbations besides the four start ones: the merit sums reversed, and +-1e-13 relative noise
+# on every Newton step (oracle/nlot_oracle.c NLOT_ORACLE_SUM_REV, NLOT_ORACLE_STEP_JITTER): the GPU rounds its fp64
+# reductions and Riccati sweeps differently in every iteration, which a start perturbation models only at the start
+SEQ_EXTRA = ({"NLOT_ORACLE_SUM_REV": "1"}, {"NLOT_ORACLE_STEP_JITTER": "1e-13"}, {"NLOT_ORACLE_STEP_JITTER": "-1e-13"})
+
+
+def seq_pin(O, prob, X0, XG, hm, opt, Xi, threads):
+    """k_seq over the four start perturbations and SEQ_EXTRA, from runs capped at PIN_CAP + 1 iterations (traces
+    only: a capped run's trace equals the full run's up to the cap)."""
+    from outcomes import PERTURBATIONS
+
+    n = len(X0)
+    o = type(opt).from_buffer_copy(opt)
+    o.max_iter = PIN_CAP + 1
+    runs = [(pd, {}) for pd in PERTURBATIONS[:N_START]] + [((0, 0.0, False), e) for e in SEQ_EXTRA]
+
+    def one(args):
+        i, (c, d, _) = args
+        x = X0[i].copy()
+        x[c] += d
+        return O.solve_trace(prob, x, XG[i], hm, opt=o, X_init=None if Xi is None else Xi[i], cap=PIN_CAP + 1)
+
+    m = len(runs)
+    its = np.zeros((m, n), np.int32)
+    dev = np.full((m, n, PIN_CAP + 1), np.nan)
+    T0 = None
+    with ThreadPoolExecutor(threads) as ex:
+        for p, (pd, env) in enumerate(runs):
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            try:
+                rs = list(ex.map(one, [(i, pd) for i in range(n)]))
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            T = np.stack([r["trace"] for r in rs])
+            if T0 is None:
+                T0 = T
+            its[p] = [r["iters"] for r in rs]
+            dev[p] = np.abs(T - T0).max(2)
+    kseq, _ = pin(dev, its, range(1, m))
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    XUp = T0[np.arange(n), kseq]
+    return {"kseq": kseq, "Xseq": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx),
+            "Useq": XUp[:, (N + 1) * nx:].reshape(n, N, nu), "stseq": pin_status(O, prob, X0, XG, hm, opt, Xi, kseq, threads)}
+
+
 def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
     """Outcomes under every perturbation, with the per-instance pinned iterates."""
     from outcomes import FIXTURE_PERTURBATIONS, mlp_order
@@ -148,15 +199,12 @@ def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
             print(f"  perturbation {p} {pd}: {time.time() - t:.0f} s, statuses {np.bincount(st[p], minlength=7).tolist()}",
                   flush=True)
     kpin, spread = pin(dev, its, range(1, m))
-    kseq, _ = pin(dev, its, range(1, N_START))
     N, nx, nu = prob.N, prob.nx, prob.nu
+    XUp = T0[np.arange(n), kpin]
     out = {"status": st, "cost": cost, "iters": its, "xdev": xdev, "trials": trials, "kpin": kpin, "pin_spread": spread,
-           "kseq": kseq}
-    for tag, k in (("pin", kpin), ("seq", kseq)):
-        XUp = T0[np.arange(n), k]
-        out[f"X{tag}"] = XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx)
-        out[f"U{tag}"] = XUp[:, (N + 1) * nx:].reshape(n, N, nu)
-        out[f"st{tag}"] = pin_status(O, prob, X0, XG, hm, opt, Xi, k, threads)
+           "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx), "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu),
+           "stpin": pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads)}
+    out.update(seq_pin(O, prob, X0, XG, hm, opt, Xi, threads))
     return out
 
 
@@ -165,6 +213,7 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
+    ap.add_argument("--seq-pin", action="store_true", help="recompute only {case}_kseq / Xseq / Useq / stseq in --out")
     a = ap.parse_args()
     import oracle as O
     from nlotrajectories_amd import _abi
@@ -174,6 +223,23 @@ def main():
     opt = _abi.default_options(general_bounds=1)
     data = dict(np.load(a.out)) if (a.only and os.path.exists(a.out)) else {}
     data["general_bounds"] = np.array(opt.general_bounds)
+
+    if a.seq_pin:
+        data = dict(np.load(a.out))
+        hm6 = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz")))
+        for case, prob, hm, xi in (("b6", B6_PROBLEM, hm6, "b6_xinit"), ("metric", METRIC_PROBLEM,
+                                                                         O.HostMlp(MlpWeights.artefact()), None)):
+            if f"{case}_x0" not in data or a.only not in (None, case):
+                continue
+            t = time.time()
+            out = seq_pin(O, prob, data[f"{case}_x0"], data[f"{case}_xg"], hm, opt, data.get(xi) if xi else None,
+                          a.threads)
+            data.update({f"{case}_{k}": v for k, v in out.items()})
+            kp = out["kseq"]
+            print(f"{case} kseq: min / median / max {kp.min()} / {int(np.median(kp))} / {kp.max()} ({time.time() - t:.0f} s)",
+                  flush=True)
+        np.savez_compressed(a.out, **data)
+        return
 
     def report(case, out, t):
         for k in ("kpin", "kseq"):
