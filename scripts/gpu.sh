@@ -5,6 +5,7 @@
 #
 # Each STEP runs under its own time limit; the first failing step ends the call (no retries).  Output goes to
 # gpurun_out/TAG/.  Steps:
+#   env=VAR=VALUE    export VAR=VALUE for the following steps (unenv=VAR unsets it)
 #   suite            python -m pytest tests -m gpu (verbose, per-test timeout)
 #   smoke            __graft_entry__.smoke()
 #   test=EXPR        python -m pytest tests -m gpu -k EXPR (quote EXPR; spaces as '+')
@@ -31,6 +32,10 @@ for step in "$@"; do
   log=$OUT/$n.$name.log
   echo "[gpu.sh] step $n: $step" >&2
   case $name in
+    env)  # env=VAR=VALUE: exported for the following steps
+      export "$arg"; rc=0 ;;
+    unenv)
+      unset "$arg"; rc=0 ;;
     suite)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
       rc=$?; tail -1 "$log" ;;
