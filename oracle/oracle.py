@@ -12,12 +12,14 @@ import numpy as np
 from nlotrajectories_amd import _abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle_nlot.so")
+# NLOT_ORACLE_LIB=liboracle_nlot_fma.so: the FMA-contracted build (oracle/Makefile; fixture generation only)
+LIB_PATH = os.path.join(HERE, os.environ.get("NLOT_ORACLE_LIB", "liboracle_nlot.so"))
 
 
 def build(force: bool = False) -> str:
     srcs = [os.path.join(HERE, "nlot_oracle.c"), os.path.join(HERE, "..", "include", "nlot.h")]
-    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs):
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs) \
+            or not os.path.exists(os.path.join(HERE, "liboracle_nlot_fma.so")):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
     return LIB_PATH
 

@@ -30,6 +30,9 @@ def main():
     a = ap.parse_args()
     import oracle as O
     from outcomes import PERTURBATIONS, mlp_order
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_oracle_outcomes import SEQ_EXTRA
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
     from nlotrajectories_amd.ops import DeviceMlp
@@ -50,11 +53,19 @@ def main():
         xi = f[f"{a.case}_xinit"][i] if f"{a.case}_xinit" in f else None
         opt = _abi.default_options(general_bounds=gb)
         traces = []
-        for c, d, rev in PERTURBATIONS:
+        o_tr = _abi.default_options(general_bounds=gb, max_iter=a.kmax + 1)
+        if a.arith == "seq":  # the fp64-sized perturbations of k_seq (make_oracle_outcomes.SEQ_EXTRA)
+            runs = [(pd, {}) for pd in PERTURBATIONS[:5]] + [((0, 0.0, False), e) for e in SEQ_EXTRA]
+        else:
+            runs = [(pd, {}) for pd in PERTURBATIONS]
+        for (c, d, rev), env in runs:
             x = x0.copy()
             x[c] += d
+            os.environ.update(env)
             with mlp_order(rev):
-                traces.append(O.solve_trace(prob, x, xg, hm, opt=opt, X_init=xi, cap=a.kmax + 1)["trace"])
+                traces.append(O.solve_trace(prob, x, xg, hm, opt=o_tr, X_init=xi, cap=a.kmax + 1)["trace"])
+            for k_ in env:
+                os.environ.pop(k_, None)
         T0 = traces[0]
         print(f"instance {i}: kpin {int(f[f'{a.case}_kpin'][i])}, kseq {int(f[f'{a.case}_kseq'][i])}, "
               f"oracle status {int(f[f'{a.case}_status'][0, i])} "
@@ -64,11 +75,12 @@ def main():
             r = solve_batch(prob, x0[None], xg[None], mlp=mlp, X_init=None if xi is None else xi[None], options=o)
             g = np.concatenate([r["X"][0].cpu().numpy().ravel(), r["U"][0].cpu().numpy().ravel()])
             dg = float(np.nanmax(np.abs(g - T0[k])))
-            dself = max(float(np.nanmax(np.abs(t[k] - T0[k]))) for t in traces[1:])
+            dall = [float(np.nanmax(np.abs(t[k] - T0[k]))) for t in traces[1:]]
+            dself = max(dall)
             dX = np.abs(g[:(N + 1) * nx] - T0[k][:(N + 1) * nx]).reshape(N + 1, nx)
             kk, jj = np.unravel_index(int(np.nanargmax(dX)), dX.shape)
-            print(f"  k {k:3d} status {int(r['status'][0])} |gpu - oracle| {dg:.3e}  oracle self {dself:.3e}  "
-                  f"argmax X[{kk},{jj}]", flush=True)
+            print(f"  k {k:3d} status {int(r['status'][0])} |gpu - oracle| {dg:.3e}  oracle self {dself:.3e} "
+                  f"({' '.join(f'{v:.1e}' for v in dall)})  argmax X[{kk},{jj}]", flush=True)
 
 
 if __name__ == "__main__":

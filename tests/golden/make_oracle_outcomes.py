@@ -24,11 +24,12 @@ IPOPT's settings (default_options: max_iter 1000, tol 1e-4, adaptive mu, restora
 
 Per-instance pinned iterates: every run records its iterate at the top of each iteration (oracle_solve_trace).
   {case}_kpin[i] = k_i, the last iteration (at most PIN_CAP = 200, at most the shortest run) up to which all 19
-      perturbed runs stay within PIN_TOL = 1e-5 (max |dX|, |dU|) of the unperturbed run: where the GPU's MFMA nets
-      (split-bf16, f32) must still be on the oracle's path;
-  {case}_kseq[i], the same over fp64-sized perturbations only (rows 1-4, the merit function's sums reversed, and
-      +-1e-13 relative noise on every Newton step: SEQ_EXTRA, runs capped at 201 iterations): where the GPU with the
-      oracle's own net arithmetic (NLOT_MLP_ARITH_SEQ: the net bitwise the oracle's) must still be on it;
+      perturbed runs stay within PIN_TOL = 1e-5 (max |dX|, |dU|) of the unperturbed run, and at most k_seq below:
+      where the GPU's MFMA nets (split-bf16, f32) must still be on the oracle's path;
+  {case}_kseq[i], the same over fp64-sized perturbations only (rows 1-4, the merit function's sums reversed,
+      +-1e-13 relative noise on every Newton step, and the oracle compiled with FMA contraction: SEQ_EXTRA / FMA_LIB,
+      runs capped at 201 iterations): where the GPU with the oracle's own net arithmetic (NLOT_MLP_ARITH_SEQ: the net
+      bitwise the oracle's) must still be on it;
   {case}_Xpin / _Upin / _Xseq / _Useq: the unperturbed iterate there (what max_iter = k returns);
   {case}_stpin / _stseq: the unperturbed run's status at max_iter = k (max_iter, or the final status where the run
       ends at the top of iteration k; a restoration line-search failure at k = iters happens inside iteration k and
@@ -116,6 +117,32 @@ def pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads):
 # on every Newton step (oracle/nlot_oracle.c NLOT_ORACLE_SUM_REV, NLOT_ORACLE_STEP_JITTER): the GPU rounds its fp64
 # reductions and Riccati sweeps differently in every iteration, which a start perturbation models only at the start
 SEQ_EXTRA = ({"NLOT_ORACLE_SUM_REV": "1"}, {"NLOT_ORACLE_STEP_JITTER": "1e-13"}, {"NLOT_ORACLE_STEP_JITTER": "-1e-13"})
+# and the oracle compiled with FMA contraction (oracle/Makefile liboracle_nlot_fma.so): every fp64 operation rounded
+# otherwise, as the GPU's code is compiled.  The restoration phase's entry amplifies that to 1e-10 .. 1e-8 within two
+# iterations on benchmark 6 (instances 3, 7: 3.5e-10 / 2.0e-11 at iteration 7 where the other perturbations give
+# 1e-12), which the start and step perturbations above do not reproduce.  Run in a child process (one library per
+# process).
+FMA_LIB = "liboracle_nlot_fma.so"
+
+
+def fma_traces(case, prob_name, data_path, threads, out_path):
+    """Child-process side of seq_pin's FMA row: the unperturbed runs' traces (capped) with the FMA-contracted oracle."""
+    import oracle as O
+    from nlotrajectories_amd import _abi
+    from nlotrajectories_amd.nn import MlpWeights
+    from nlotrajectories_amd.problem import B6_PROBLEM, METRIC_PROBLEM
+
+    assert os.path.basename(O.LIB_PATH) == FMA_LIB, O.LIB_PATH
+    d = dict(np.load(data_path))
+    prob = B6_PROBLEM if case == "b6" else METRIC_PROBLEM
+    hm = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
+                   if case == "b6" else MlpWeights.artefact())
+    X0, XG, Xi = d["x0"], d["xg"], d.get("xinit")
+    o = _abi.default_options(general_bounds=int(d["general_bounds"]), max_iter=PIN_CAP + 1)
+    with ThreadPoolExecutor(threads) as ex:
+        rs = list(ex.map(lambda i: O.solve_trace(prob, X0[i], XG[i], hm, opt=o, X_init=None if Xi is None else Xi[i],
+                                                 cap=PIN_CAP + 1), range(len(X0))))
+    np.savez(out_path, trace=np.stack([r["trace"] for r in rs]), iters=np.array([r["iters"] for r in rs], np.int32))
 
 
 def seq_pin(O, prob, X0, XG, hm, opt, Xi, threads):
@@ -155,11 +182,34 @@ def seq_pin(O, prob, X0, XG, hm, opt, Xi, threads):
                 T0 = T
             its[p] = [r["iters"] for r in rs]
             dev[p] = np.abs(T - T0).max(2)
-    kseq, _ = pin(dev, its, range(1, m))
+    # the FMA-contracted build's unperturbed run (child process)
+    import subprocess
+    import tempfile
+
+    case = "b6" if prob.N == 100 else "metric"
+    with tempfile.TemporaryDirectory() as td:
+        src, dst = os.path.join(td, "in.npz"), os.path.join(td, "out.npz")
+        np.savez(src, x0=X0, xg=XG, general_bounds=np.array(opt.general_bounds),
+                 **({"xinit": Xi} if Xi is not None else {}))
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--fma-traces", case, src, dst,
+                        "--threads", str(threads)], check=True, env=dict(os.environ, NLOT_ORACLE_LIB=FMA_LIB))
+        r = np.load(dst)
+        its = np.concatenate([its, r["iters"][None]])
+        dev = np.concatenate([dev, np.abs(r["trace"] - T0).max(2)[None]])
+    kseq, _ = pin(dev, its, range(1, m + 1))
     N, nx, nu = prob.N, prob.nx, prob.nu
     XUp = T0[np.arange(n), kseq]
     return {"kseq": kseq, "Xseq": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx),
             "Useq": XUp[:, (N + 1) * nx:].reshape(n, N, nu), "stseq": pin_status(O, prob, X0, XG, hm, opt, Xi, kseq, threads)}
+
+
+def clamp_kpin(data, case):
+    """k_i covers every perturbation, the fp64-sized ones of k_seq included (the MFMA nets' GPU runs differ from the
+    oracle in the fp64 arithmetic too): where k_seq < k_i, k_i = k_seq with k_seq's iterate and status."""
+    lo = data[f"{case}_kseq"] < data[f"{case}_kpin"]
+    for a, b in (("kpin", "kseq"), ("Xpin", "Xseq"), ("Upin", "Useq"), ("stpin", "stseq")):
+        data[f"{case}_{a}"] = np.where(lo.reshape((-1,) + (1,) * (data[f"{case}_{a}"].ndim - 1)),
+                                       data[f"{case}_{b}"], data[f"{case}_{a}"])
 
 
 def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
@@ -205,7 +255,9 @@ def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
            "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx), "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu),
            "stpin": pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads)}
     out.update(seq_pin(O, prob, X0, XG, hm, opt, Xi, threads))
-    return out
+    d = {f"c_{k}": v for k, v in out.items()}
+    clamp_kpin(d, "c")
+    return {k[2:]: v for k, v in d.items()}
 
 
 def main():
@@ -214,7 +266,10 @@ def main():
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
     ap.add_argument("--seq-pin", action="store_true", help="recompute only {case}_kseq / Xseq / Useq / stseq in --out")
+    ap.add_argument("--fma-traces", nargs=3, default=None, help=argparse.SUPPRESS)  # CASE IN.npz OUT.npz (seq_pin)
     a = ap.parse_args()
+    if a.fma_traces:
+        return fma_traces(a.fma_traces[0], None, a.fma_traces[1], a.threads, a.fma_traces[2])
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
@@ -235,6 +290,7 @@ def main():
             out = seq_pin(O, prob, data[f"{case}_x0"], data[f"{case}_xg"], hm, opt, data.get(xi) if xi else None,
                           a.threads)
             data.update({f"{case}_{k}": v for k, v in out.items()})
+            clamp_kpin(data, case)
             kp = out["kseq"]
             print(f"{case} kseq: min / median / max {kp.min()} / {int(np.median(kp))} / {kp.max()} ({time.time() - t:.0f} s)",
                   flush=True)
