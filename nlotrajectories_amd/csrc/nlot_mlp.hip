@@ -383,6 +383,32 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
     l = (__bf16)(r - (float)m);    // exact difference
 }
 
+// The five smaller split products of one k block from a zero accumulator, then the hi x hi products into the running
+// sum, then the two added by a VALU add (round to nearest).  One v_mfma_f32_32x32x16_bf16 aligns its addends (the
+// accumulator and its 16 products) to the largest of them and keeps about two bits below that one's fp32 ulp
+// (scripts/mfma_round_probe.hip), so small products added straight to a large running sum lose their low bits.
+__device__ __forceinline__ f32x16 mfma6s(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bm, const bf16x8& bl, f32x16 acc) {
+    f32x16 acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, f32x16{}, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acs, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    return acc + acs;
+}
+// Where it is used (round 6, profiles/r06/ab_split_two_acc/): in the reverse sweep (G = W^T e, the
+// gradient and Hessian) by default — there the direct accumulation had raised the artefact net's gradient error spread
+// 1.1-2.5x above every fp32 summation order's, and with mfma6s it is the fp32 orders' (scripts/net_bias_probe.py), at
+// -9 % of the full launch; in the forward GEMMs only with NLOT_MLP_TWOACC_FWD=1 (it halves the value's -5e-9 offset
+// but the value kernel spills at 3 waves per SIMD: -20 % there, -5 % traj/s)
+#ifndef NLOT_MLP_TWOACC_FWD
+#define NLOT_MLP_TWOACC_FWD 0
+#endif
+#ifndef NLOT_MLP_TWOACC_REV
+#define NLOT_MLP_TWOACC_REV 1
+#endif
+
 // six split-bf16 products, smallest terms first
 __device__ __forceinline__ f32x16 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
                                         const bf16x8& bm, const bf16x8& bl, f32x16 acc) {
@@ -553,7 +579,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                     const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
                     const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
                     const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
-                    acc[t] = mfma6(ah, am, al, bh, bm, bl, acc[t]);
+                    acc[t] = NLOT_MLP_TWOACC_FWD ? mfma6s(ah, am, al, bh, bm, bl, acc[t]) : mfma6(ah, am, al, bh, bm, bl, acc[t]);
 #pragma unroll
                     for (int u = 0; u < EPT; ++u) {
                         const int jj = t * EPT + u;
@@ -692,7 +718,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                 const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp);
                 const bf16x8 am = *reinterpret_cast<const bf16x8*>(rowp + (size_t)H * RS);
                 const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + (size_t)2 * H * RS);
-                acc[t] = mfma6(ah, am, al, bh, bm, bl, acc[t]);
+                acc[t] = NLOT_MLP_TWOACC_FWD ? mfma6s(ah, am, al, bh, bm, bl, acc[t]) : mfma6(ah, am, al, bh, bm, bl, acc[t]);
             }
         }
         // ---------------- bias + ReLU + output layer (accumulator layout of the f32 MFMA: acc_row) ----------------
@@ -801,7 +827,7 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
                     const bf16x8 ah = wt_frag<RS>(sWp, jbase, 32 * tk, lane);
                     const bf16x8 am = wt_frag<RS>(sWp + (size_t)H * RS, jbase, 32 * tk, lane);
                     const bf16x8 al = wt_frag<RS>(sWp + (size_t)2 * H * RS, jbase, 32 * tk, lane);
-                    g = mfma6(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g);
+                    g = NLOT_MLP_TWOACC_REV ? mfma6s(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g) : mfma6(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g);
                     if (tk > 0) contract2(gprev, tk - 1, 2 * blk);
                 }
                 gprev = g;
