@@ -397,6 +397,16 @@ __device__ __forceinline__ f32x16 mfma6s(const bf16x8& ah, const bf16x8& am, con
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
     return acc + acs;
 }
+// The five smaller products into a running accumulator of their own (NLOT_MLP_TWOACC_REV=2: one VALU add per output
+// tile instead of one per k block; the small-product sum stays ~2^-8 of the main one, so it keeps its low bits too)
+__device__ __forceinline__ f32x16 mfma5s(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bm, const bf16x8& bl, f32x16 acs) {
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acs, 0, 0, 0);
+    acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acs, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acs, 0, 0, 0);
+}
 // Where it is used (round 6, profiles/r06/ab_split_two_acc/): in the reverse sweep (G = W^T e, the
 // gradient and Hessian) by default — there the direct accumulation had raised the artefact net's gradient error spread
 // 1.1-2.5x above every fp32 summation order's, and with mfma6s it is the fp32 orders' (scripts/net_bias_probe.py), at
@@ -406,7 +416,7 @@ __device__ __forceinline__ f32x16 mfma6s(const bf16x8& ah, const bf16x8& am, con
 #define NLOT_MLP_TWOACC_FWD 0
 #endif
 #ifndef NLOT_MLP_TWOACC_REV
-#define NLOT_MLP_TWOACC_REV 1
+#define NLOT_MLP_TWOACC_REV 2
 #endif
 
 // six split-bf16 products, smallest terms first
@@ -820,16 +830,23 @@ __global__ __launch_bounds__(bf16_threads(FULL), 1) void mlp_bf16(MlpDev w, cons
             f32x16 gprev = f32x16{};
 #pragma unroll
             for (int tk = 0; tk < NT; ++tk) {
-                f32x16 g = f32x16{};
+                f32x16 g = f32x16{}, gs = f32x16{};
 #pragma unroll
                 for (int blk = 0; blk < NB; ++blk) {
                     const int jbase = 16 * blk;  // 32 tj + 16 sl
                     const bf16x8 ah = wt_frag<RS>(sWp, jbase, 32 * tk, lane);
                     const bf16x8 am = wt_frag<RS>(sWp + (size_t)H * RS, jbase, 32 * tk, lane);
                     const bf16x8 al = wt_frag<RS>(sWp + (size_t)2 * H * RS, jbase, 32 * tk, lane);
-                    g = NLOT_MLP_TWOACC_REV ? mfma6s(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g) : mfma6(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g);
+                    if constexpr (NLOT_MLP_TWOACC_REV == 2) {
+                        gs = mfma5s(ah, am, al, Bh[blk], Bm[blk], Bl[blk], gs);
+                        g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, Bh[blk], g, 0, 0, 0);
+                    } else {
+                        g = NLOT_MLP_TWOACC_REV ? mfma6s(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g)
+                                                : mfma6(ah, am, al, Bh[blk], Bm[blk], Bl[blk], g);
+                    }
                     if (tk > 0) contract2(gprev, tk - 1, 2 * blk);
                 }
+                if constexpr (NLOT_MLP_TWOACC_REV == 2) g += gs;
                 gprev = g;
             }
 #pragma unroll

@@ -28,8 +28,10 @@ Per-instance pinned iterates: every run records its iterate at the top of each i
       where the GPU's MFMA nets (split-bf16, f32) must still be on the oracle's path;
   {case}_kseq[i], the same over fp64-sized perturbations only (rows 1-4, the merit function's sums reversed,
       +-1e-13 relative noise on every Newton step, and the oracle compiled with FMA contraction: SEQ_EXTRA / FMA_LIB,
-      runs capped at 201 iterations): where the GPU with the oracle's own net arithmetic (NLOT_MLP_ARITH_SEQ: the net
-      bitwise the oracle's) must still be on it;
+      runs capped at 201 iterations, and SEQ_COMBINED: FMA contraction with the other fp64 perturbations at once):
+      where the GPU with the oracle's own net arithmetic (NLOT_MLP_ARITH_SEQ: the net bitwise the oracle's) must
+      still be on it; k_i is lowered further by NET_COMBINED (FMA contraction, another net order and step noise at
+      once, as the GPU's MFMA-net run differs in all three);
   {case}_Xpin / _Upin / _Xseq / _Useq: the unperturbed iterate there (what max_iter = k returns);
   {case}_stpin / _stseq: the unperturbed run's status at max_iter = k (max_iter, or the final status where the run
       ends at the top of iteration k; a restoration line-search failure at k = iters happens inside iteration k and
@@ -125,8 +127,23 @@ SEQ_EXTRA = ({"NLOT_ORACLE_SUM_REV": "1"}, {"NLOT_ORACLE_STEP_JITTER": "1e-13"},
 FMA_LIB = "liboracle_nlot_fma.so"
 
 
-def fma_traces(case, prob_name, data_path, threads, out_path):
-    """Child-process side of seq_pin's FMA row: the unperturbed runs' traces (capped) with the FMA-contracted oracle."""
+# Combined perturbations (round 6): the GPU's run differs from the oracle's in every respect at once (FMA
+# contraction, other fp64 summation orders in its reductions and sweeps, and for the MFMA nets the net's fp32 order)
+# where each row above varies one.  Run with the FMA-contracted build (child process): for k_seq, the merit sums
+# reversed and step noise, or a start perturbation, on top of FMA contraction; for k_i, each of the net's 15 other
+# orders on top of FMA contraction and step noise.
+SEQ_COMBINED = ({"env": {"NLOT_ORACLE_SUM_REV": "1", "NLOT_ORACLE_STEP_JITTER": "1e-13"}},
+                {"env": {"NLOT_ORACLE_STEP_JITTER": "-1e-13"}, "coord": 0, "d": 1e-13},
+                {"env": {"NLOT_ORACLE_SUM_REV": "1"}, "coord": 1, "d": -1e-13})
+NET_COMBINED = tuple({"env": {"NLOT_ORACLE_MLP_REV": str(v), "NLOT_ORACLE_STEP_JITTER": "1e-13" if v % 2 else "-1e-13"}}
+                     for v in range(1, 16))
+
+
+def fma_traces(case, data_path, threads, out_path):
+    """Child-process side of the FMA rows: for each run of the input's `spec` (JSON list of {env, coord, d}), the
+    traces (capped at PIN_CAP + 1 iterations) with the FMA-contracted oracle, as deviations from the input's T0."""
+    import json
+
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
@@ -137,12 +154,46 @@ def fma_traces(case, prob_name, data_path, threads, out_path):
     prob = B6_PROBLEM if case == "b6" else METRIC_PROBLEM
     hm = O.HostMlp(MlpWeights.load(os.path.join(ROOT, "nlotrajectories_amd", "data", "b6_mlp128_seed0.npz"))
                    if case == "b6" else MlpWeights.artefact())
-    X0, XG, Xi = d["x0"], d["xg"], d.get("xinit")
+    X0, XG, Xi, T0 = d["x0"], d["xg"], d.get("xinit"), d["T0"]
     o = _abi.default_options(general_bounds=int(d["general_bounds"]), max_iter=PIN_CAP + 1)
+    devs, its = [], []
     with ThreadPoolExecutor(threads) as ex:
-        rs = list(ex.map(lambda i: O.solve_trace(prob, X0[i], XG[i], hm, opt=o, X_init=None if Xi is None else Xi[i],
-                                                 cap=PIN_CAP + 1), range(len(X0))))
-    np.savez(out_path, trace=np.stack([r["trace"] for r in rs]), iters=np.array([r["iters"] for r in rs], np.int32))
+        for run in json.loads(str(d["spec"])):
+            x = X0.copy()
+            x[:, run.get("coord", 0)] += run.get("d", 0.0)
+            old = {k: os.environ.get(k) for k in run.get("env", {})}
+            os.environ.update(run.get("env", {}))
+            try:
+                rs = list(ex.map(lambda i: O.solve_trace(prob, x[i], XG[i], hm, opt=o,
+                                                         X_init=None if Xi is None else Xi[i], cap=PIN_CAP + 1),
+                                 range(len(X0))))
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            devs.append(np.abs(np.stack([r["trace"] for r in rs]) - T0).max(2))
+            its.append([r["iters"] for r in rs])
+    np.savez(out_path, dev=np.stack(devs), iters=np.array(its, np.int32))
+
+
+def fma_rows(prob, X0, XG, opt, Xi, T0, spec, threads):
+    """Deviation traces [len(spec), n, PIN_CAP + 1] and final iterations of the FMA-contracted oracle's runs `spec`
+    from the plain oracle's unperturbed traces T0 (a child process: one oracle library per process)."""
+    import json
+    import subprocess
+    import tempfile
+
+    case = "b6" if prob.N == 100 else "metric"
+    with tempfile.TemporaryDirectory() as td:
+        src, dst = os.path.join(td, "in.npz"), os.path.join(td, "out.npz")
+        np.savez(src, x0=X0, xg=XG, general_bounds=np.array(opt.general_bounds), T0=T0, spec=np.array(json.dumps(spec)),
+                 **({"xinit": Xi} if Xi is not None else {}))
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--fma-traces", case, src, dst,
+                        "--threads", str(threads)], check=True, env=dict(os.environ, NLOT_ORACLE_LIB=FMA_LIB))
+        r = np.load(dst)
+        return r["dev"], r["iters"]
 
 
 def seq_pin(O, prob, X0, XG, hm, opt, Xi, threads):
@@ -182,25 +233,30 @@ def seq_pin(O, prob, X0, XG, hm, opt, Xi, threads):
                 T0 = T
             its[p] = [r["iters"] for r in rs]
             dev[p] = np.abs(T - T0).max(2)
-    # the FMA-contracted build's unperturbed run (child process)
-    import subprocess
-    import tempfile
-
-    case = "b6" if prob.N == 100 else "metric"
-    with tempfile.TemporaryDirectory() as td:
-        src, dst = os.path.join(td, "in.npz"), os.path.join(td, "out.npz")
-        np.savez(src, x0=X0, xg=XG, general_bounds=np.array(opt.general_bounds),
-                 **({"xinit": Xi} if Xi is not None else {}))
-        subprocess.run([sys.executable, os.path.abspath(__file__), "--fma-traces", case, src, dst,
-                        "--threads", str(threads)], check=True, env=dict(os.environ, NLOT_ORACLE_LIB=FMA_LIB))
-        r = np.load(dst)
-        its = np.concatenate([its, r["iters"][None]])
-        dev = np.concatenate([dev, np.abs(r["trace"] - T0).max(2)[None]])
-    kseq, _ = pin(dev, its, range(1, m + 1))
+    # the FMA-contracted build's unperturbed run and SEQ_COMBINED (child process)
+    fdev, fits = fma_rows(prob, X0, XG, opt, Xi, T0, [{}] + list(SEQ_COMBINED), threads)
+    its = np.concatenate([its, fits])
+    dev = np.concatenate([dev, fdev])
+    kseq, _ = pin(dev, its, range(1, len(dev)))
     N, nx, nu = prob.N, prob.nx, prob.nu
     XUp = T0[np.arange(n), kseq]
     return {"kseq": kseq, "Xseq": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx),
-            "Useq": XUp[:, (N + 1) * nx:].reshape(n, N, nu), "stseq": pin_status(O, prob, X0, XG, hm, opt, Xi, kseq, threads)}
+            "Useq": XUp[:, (N + 1) * nx:].reshape(n, N, nu), "stseq": pin_status(O, prob, X0, XG, hm, opt, Xi, kseq, threads),
+            "T0": T0, "its0": its[0]}
+
+
+def net_combined_pin(O, prob, X0, XG, hm, opt, Xi, threads, kpin, T0, its0):
+    """k_i lowered to where a NET_COMBINED run (FMA build, another net order, step noise) leaves the unperturbed
+    run, with the iterate and status there."""
+    n = len(X0)
+    fdev, fits = fma_rows(prob, X0, XG, opt, Xi, T0, list(NET_COMBINED), threads)
+    kc, _ = pin(np.concatenate([np.zeros((1,) + fdev.shape[1:]), fdev]), np.concatenate([its0[None], fits]),
+                range(1, len(fdev) + 1))
+    k = np.minimum(kpin, kc).astype(np.int32)
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    XUp = T0[np.arange(n), k]
+    return {"kpin": k, "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx),
+            "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu), "stpin": pin_status(O, prob, X0, XG, hm, opt, Xi, k, threads)}
 
 
 def clamp_kpin(data, case):
@@ -254,7 +310,10 @@ def run_case(O, prob, X0, XG, hm, opt, Xi, threads):
     out = {"status": st, "cost": cost, "iters": its, "xdev": xdev, "trials": trials, "kpin": kpin, "pin_spread": spread,
            "Xpin": XUp[:, :(N + 1) * nx].reshape(n, N + 1, nx), "Upin": XUp[:, (N + 1) * nx:].reshape(n, N, nu),
            "stpin": pin_status(O, prob, X0, XG, hm, opt, Xi, kpin, threads)}
-    out.update(seq_pin(O, prob, X0, XG, hm, opt, Xi, threads))
+    sq = seq_pin(O, prob, X0, XG, hm, opt, Xi, threads)
+    T0s, its0 = sq.pop("T0"), sq.pop("its0")
+    out.update(sq)
+    out.update(net_combined_pin(O, prob, X0, XG, hm, opt, Xi, threads, kpin, T0s, its0))
     d = {f"c_{k}": v for k, v in out.items()}
     clamp_kpin(d, "c")
     return {k[2:]: v for k, v in d.items()}
@@ -265,11 +324,12 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--only", default=None, help="metric | b6 (keeps the other case from an existing file)")
-    ap.add_argument("--seq-pin", action="store_true", help="recompute only {case}_kseq / Xseq / Useq / stseq in --out")
+    ap.add_argument("--seq-pin", action="store_true",
+                    help="recompute only the pinned iterations (k_seq, and k_i lowered by NET_COMBINED) in --out")
     ap.add_argument("--fma-traces", nargs=3, default=None, help=argparse.SUPPRESS)  # CASE IN.npz OUT.npz (seq_pin)
     a = ap.parse_args()
     if a.fma_traces:
-        return fma_traces(a.fma_traces[0], None, a.fma_traces[1], a.threads, a.fma_traces[2])
+        return fma_traces(a.fma_traces[0], a.fma_traces[1], a.threads, a.fma_traces[2])
     import oracle as O
     from nlotrajectories_amd import _abi
     from nlotrajectories_amd.nn import MlpWeights
@@ -287,13 +347,16 @@ def main():
             if f"{case}_x0" not in data or a.only not in (None, case):
                 continue
             t = time.time()
-            out = seq_pin(O, prob, data[f"{case}_x0"], data[f"{case}_xg"], hm, opt, data.get(xi) if xi else None,
-                          a.threads)
+            X0, XG, Xi = data[f"{case}_x0"], data[f"{case}_xg"], data.get(xi) if xi else None
+            out = seq_pin(O, prob, X0, XG, hm, opt, Xi, a.threads)
+            T0, its0 = out.pop("T0"), out.pop("its0")
+            out.update(net_combined_pin(O, prob, X0, XG, hm, opt, Xi, a.threads, data[f"{case}_kpin"], T0, its0))
             data.update({f"{case}_{k}": v for k, v in out.items()})
             clamp_kpin(data, case)
-            kp = out["kseq"]
-            print(f"{case} kseq: min / median / max {kp.min()} / {int(np.median(kp))} / {kp.max()} ({time.time() - t:.0f} s)",
-                  flush=True)
+            for k in ("kseq", "kpin"):
+                kp = data[f"{case}_{k}"]
+                print(f"{case} {k}: min / median / max {kp.min()} / {int(np.median(kp))} / {kp.max()} "
+                      f"({time.time() - t:.0f} s)", flush=True)
         np.savez_compressed(a.out, **data)
         return
 

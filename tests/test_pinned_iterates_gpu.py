@@ -18,7 +18,15 @@ restoration-failed alike.  k per net arithmetic (include/nlot.h NLOT_MLP_ARITH_*
 
 Round 5 pinned the MFMA nets at a k_i measured with one other net order, so k_i was optimistic for them, and an
 excusal (the oracle leaving the path too under other orders or wider starts, checked after the fact) with a 5 %-per-net
-cap covered the difference.  Both are gone: the perturbation set that defines k_i is now the one that excused."""
+cap covered the difference.  Both are gone: the perturbation set that defines k_i is now the one that excused, plus
+(round 6) combined perturbations, the FMA-contracted oracle with another net order and step noise at once, as the
+GPU's run differs in all of them together.
+
+The bar: the product net (split_bf16) leaves the pinned path on no instance.  The selectable alternatives (f32, seq)
+are held to the sampling bound of the definition itself: k is the minimum over K perturbed runs, so a run
+exchangeable with them leaves before all of them with probability 1 / (K + 1) per instance, and a strict zero would
+fail a correct net on most 24-instance batches; the count may not exceed the binomial 99.9 % quantile (miss_bound).
+Every miss is printed with its k, deviation and statuses (DESIGN.md §5 lists them)."""
 import os
 
 import numpy as np
@@ -28,6 +36,18 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 TOL = 1e-4
+PRODUCT_NET = "split_bf16"
+# perturbed runs that define k (tests/golden/make_oracle_outcomes.py): k_seq over the four starts, SEQ_EXTRA's 3,
+# the FMA build and SEQ_COMBINED's 3; k_i over the fixture's 19, k_seq's 7 others and NET_COMBINED's 15
+K_RUNS = {"pin": 19 + 7 + 15, "seq": 4 + 3 + 1 + 3}
+
+
+def miss_bound(n, k_runs, alpha=1e-3):
+    """Largest count of instances on which a run exchangeable with the k_runs perturbed ones leaves the path before
+    all of them (probability 1 / (k_runs + 1) each, independent instances), at false-failure rate alpha."""
+    from scipy.stats import binom
+
+    return int(binom.isf(alpha, n, 1.0 / (k_runs + 1)))
 
 
 def _setup(case, artefact, arith):
@@ -84,7 +104,7 @@ def test_pinned_iterates_match_oracle(case, arith, artefact):
                   f"{kp[g].min()} / {int(np.median(kp[g]))} / {kp[g].max()}, max |gpu - oracle| {dev[g].max():.2e}",
                   flush=True)
     bad = np.nonzero((dev > TOL) | (sg != want))[0]
-    print(f"[pinned] {case} {arith}: {len(bad)} of {len(kp)} outside", [(int(i), int(kp[i]), float(dev[i]),
-                                                                         int(sg[i]), int(want[i])) for i in bad],
-          flush=True)
-    assert len(bad) == 0, [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in bad]
+    allowed = 0 if arith == PRODUCT_NET else miss_bound(len(kp), K_RUNS[tag])
+    print(f"[pinned] {case} {arith}: {len(bad)} of {len(kp)} outside (allowed {allowed})",
+          [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in bad], flush=True)
+    assert len(bad) <= allowed, [(int(i), int(kp[i]), float(dev[i]), int(sg[i]), int(want[i])) for i in bad]
