@@ -408,10 +408,12 @@ __device__ __forceinline__ f32x16 mfma5s(const bf16x8& ah, const bf16x8& am, con
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acs, 0, 0, 0);
 }
 // Where it is used (round 6, profiles/r06/ab_split_two_acc/): in the reverse sweep (G = W^T e, the
-// gradient and Hessian) by default — there the direct accumulation had raised the artefact net's gradient error spread
-// 1.1-2.5x above every fp32 summation order's, and with mfma6s it is the fp32 orders' (scripts/net_bias_probe.py), at
-// -9 % of the full launch; in the forward GEMMs only with NLOT_MLP_TWOACC_FWD=1 (it halves the value's -5e-9 offset
-// but the value kernel spills at 3 waves per SIMD: -20 % there, -5 % traj/s)
+// gradient and Hessian) by default, as mfma5s's running small-product accumulator (NLOT_MLP_TWOACC_REV=2; mfma6s per
+// k block is 1, the direct accumulation 0): with the direct accumulation the product net left benchmark 6's pinned
+// path on instances where no fp32 summation order of the oracle's net does; the running form costs 3.6 % less than
+// mfma6s on the full launch (1.513 / 1.569 ms, profiles/r06/ab_rev_acc/).  In the forward GEMMs only with
+// NLOT_MLP_TWOACC_FWD=1 (it halves the value's -5e-9 offset but the value kernel spills at 3 waves per SIMD: -20 %
+// there, -5 % traj/s)
 #ifndef NLOT_MLP_TWOACC_FWD
 #define NLOT_MLP_TWOACC_FWD 0
 #endif
