@@ -427,10 +427,10 @@ def main():
         processing and the wait for CUs the side streams hold).  Committed, not this run's."""
         import csv
 
-        path = os.path.join(ROOT, "profiles", "r06", "kernel_stats_r06_K20_W5.csv")
-        if not os.path.exists(path):
-            path = os.path.join(ROOT, "profiles", "r05", "kernel_stats_r05ao_K20_W5.csv")
-        if not os.path.exists(path):
+        path = next((p for p in (os.path.join(ROOT, "profiles", r, f"kernel_stats_{t}_K20_W5.csv")
+                                 for r, t in (("r06", "r06s"), ("r06", "r06"), ("r05", "r05ao"))) if os.path.exists(p)),
+                    None)
+        if path is None:
             return None
         with open(path) as fh:
             for row in csv.DictReader(fh):
@@ -547,7 +547,7 @@ def main():
         # per-dispatch fractions from the profiler (the event brackets above include the streams' overlap): committed
         # from a rocprofv3 --kernel-trace --stats run of this command (scripts/rocprof_fracs.py)
         df = next((d for d in (os.path.join(ROOT, "profiles", r, f"mlp_dispatch_fracs_{t}.json")
-                               for r, t in (("r06", "r06"), ("r05", "r05ao"))) if os.path.exists(d)), "")
+                               for r, t in (("r06", "r06s"), ("r06", "r06"), ("r05", "r05ao"))) if os.path.exists(d)), "")
         if os.path.exists(df) and not (stress or b6):
             with open(df) as fh:
                 dd = json.load(fh)
