@@ -37,7 +37,7 @@ for step in "$@"; do
     unenv)
       unset "$arg"; rc=0 ;;
     suite)
-      timeout -k 10 1150 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$log" 2>&1
+      timeout -k 10 1150 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > "$log" 2>&1
       rc=$?; tail -1 "$log" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1
